@@ -1,0 +1,88 @@
+"""ctypes binding of libcf2sim.so (the C ABI declared in include/cf2sim.h).
+
+The shared library is built in-tree by ``cf2sim.build.build_native()`` (hipcc, gfx950) and
+loaded here.  There is no fallback: if the library or a GPU is missing, every entry point
+raises.  torch must be imported first so that the HIP runtime torch ships
+(soname libamdhip64.so.7) is the one libcf2sim binds to, and device pointers / streams
+handed over from torch are valid in it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the process' HIP runtime before libcf2sim)
+
+from .config import CF2Config
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libcf2sim.so")
+REPO_INCLUDE = os.path.abspath(os.path.join(PKG_DIR, "..", "..", "include", "cf2sim.h"))
+
+# every symbol include/cf2sim.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    "cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
+    "cf2_create", "cf2_destroy", "cf2_layout_get", "cf2_bind_hj_tables", "cf2_reset", "cf2_step",
+    "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
+)
+
+
+class CF2Layout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in (
+        "num_envs", "num_float_fields", "num_int_fields", "obs_dim", "obs_len",
+        "f_pos", "f_quat", "f_vel", "f_omega", "f_rpy", "f_motor", "f_ou", "f_abuf", "f_bias", "f_lpf", "f_held",
+        "f_obs_prev", "f_hist_act", "f_param", "f_dstb", "i_ep_step", "i_rng", "i_flags", "i_level", "i_gust",
+        "num_params")]
+
+
+class CF2Error(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libcf2sim.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CF2Error(f"{LIB_PATH} not found: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                       "(hipcc --offload-arch=gfx950) first")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, vp = ctypes.POINTER, ctypes.c_void_p
+    lib.cf2_abi_version.restype = ctypes.c_int
+    lib.cf2_config_sizeof.restype = ctypes.c_size_t
+    lib.cf2_status_string.restype = ctypes.c_char_p
+    lib.cf2_status_string.argtypes = [ctypes.c_int]
+    lib.cf2_last_hip_error.restype = ctypes.c_int
+    lib.cf2_create.argtypes = [P(CF2Config), P(vp)]
+    lib.cf2_destroy.argtypes = [vp]
+    lib.cf2_layout_get.argtypes = [vp, P(CF2Layout)]
+    lib.cf2_bind_hj_tables.argtypes = [vp, vp, ctypes.c_int, P(ctypes.c_int32)]
+    lib.cf2_reset.argtypes = [vp, vp, vp, vp]
+    lib.cf2_step.argtypes = [vp] * 11
+    lib.cf2_rollout.argtypes = [vp, ctypes.c_int, vp, ctypes.c_size_t, vp, vp, vp, vp]
+    lib.cf2_get_state.argtypes = [vp, vp, vp, vp]
+    lib.cf2_set_state.argtypes = [vp, vp, vp, vp]
+    lib.cf2_hj_disturbance.argtypes = [P(CF2Config), vp, vp, ctypes.c_uint32, ctypes.c_float, vp, vp, vp]
+    for name in EXPORTED_SYMBOLS:
+        if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error"):
+            getattr(lib, name).restype = ctypes.c_int
+    if lib.cf2_config_sizeof() != ctypes.sizeof(CF2Config):
+        raise CF2Error(f"cf2_config size mismatch: C {lib.cf2_config_sizeof()} vs Python {ctypes.sizeof(CF2Config)}")
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "cf2 call"):
+    if status != 0:
+        lib = load()
+        msg = lib.cf2_status_string(status).decode()
+        raise CF2Error(f"{what} failed: {msg} (status {status}, hip error {lib.cf2_last_hip_error()})")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None passes NULL)."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,165 @@
+"""BatchedCrazyflieEnv: N hover environments stepped by one fused HIP kernel per env-step.
+
+This is the torch-ROCm face of the C ABI (include/cf2sim.h).  All tensors live on the
+current HIP device; every call is asynchronous on torch's current stream; there is no CPU
+fallback (construction fails loudly without a GPU or without libcf2sim.so).
+
+Semantics per env follow the reference's single-process ``gym.make(id)`` env wrapped in
+gym's ``TimeLimit(max_episode_steps=500)`` (phoenix_drone_simulation/__init__.py:8-109):
+``step`` returns ``(obs, reward, done, info)`` where ``done = terminal or truncated``; envs
+that finish are reset inside the same kernel (vector-env auto-reset) and their pre-reset
+observation is returned in ``info['final_obs']`` when requested.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native
+from .config import CF2Config, DSTB_EXTERNAL, DSTB_HJ, build_config, obs_dim, spec_for_id
+from .spaces import make_box
+
+
+class BatchedCrazyflieEnv:
+    def __init__(self, env_id: str, num_envs: int, seed: int = 0, device=None, env_id_offset: int = 0,
+                 auto_reset: bool = True, want_final_obs: bool = False, config: CF2Config | None = None,
+                 **env_kwargs):
+        if not torch.cuda.is_available():
+            raise _native.CF2Error("BatchedCrazyflieEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.env_id = env_id
+        self.spec = spec_for_id(env_id) if config is None else None
+        self.cfg = config if config is not None else build_config(
+            env_id, num_envs, seed=seed, env_id_offset=env_id_offset, auto_reset=auto_reset, **env_kwargs)
+        self.num_envs = int(self.cfg.num_envs)
+        self.obs_dim = obs_dim(self.cfg)
+        self.lib = _native.load()
+        self._ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.cf2_create(ctypes.byref(self.cfg), ctypes.byref(self._ctx)), "cf2_create")
+        lay = _native.CF2Layout()
+        _native.check(self.lib.cf2_layout_get(self._ctx, ctypes.byref(lay)), "cf2_layout_get")
+        self.layout = lay
+        n, d = self.num_envs, self.device
+        self.obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=d)
+        self.rew = torch.zeros(n, dtype=torch.float32, device=d)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=d)
+        self.trunc = torch.zeros(n, dtype=torch.uint8, device=d)
+        self.cost = torch.zeros(n, dtype=torch.float32, device=d)
+        self.level = torch.zeros(n, dtype=torch.float32, device=d)
+        self.want_final_obs = want_final_obs
+        self.final_obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=d) if want_final_obs else None
+        self._tables = None
+        # spaces (envs/base.py:139-148)
+        self.observation_space = make_box(-1000.0, 1000.0, shape=(self.obs_dim,), dtype=np.float32)
+        self.action_space = make_box(-1.0, 1.0, shape=(4,), dtype=np.float32)
+
+    # ---- lifecycle ----
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            torch.cuda.synchronize(self.device)
+            self.lib.cf2_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    @property
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # ---- HJ tables (distur_gener.py:155 loads fastrack_{level}_15x15.npy each call; here once) ----
+    def bind_hj_tables(self, V: torch.Tensor, table_of_level=None):
+        """V: [T, 15,15,15,15,15,15] (or [T, 15**6]) float32 device tensor.  table_of_level maps the
+        Boltzmann level index (0.0, 0.1, ..., 2.0) to a row of V; default: fixed-level envs use row 0."""
+        V = V.reshape(V.shape[0], -1).contiguous().to(self.device, torch.float32)
+        if V.shape[1] != 15 ** 6:
+            raise ValueError("HJ value tables must be 15^6 grids")
+        if table_of_level is None:
+            table_of_level = [0] * int(self.cfg.num_levels)
+        t = (ctypes.c_int32 * int(self.cfg.num_levels))(*[int(x) for x in table_of_level])
+        _native.check(self.lib.cf2_bind_hj_tables(self._ctx, V.data_ptr(), V.shape[0], t), "cf2_bind_hj_tables")
+        self._tables = V   # keep alive
+
+    # ---- gym-like API ----
+    def reset(self, mask: torch.Tensor | None = None) -> torch.Tensor:
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        _native.check(self.lib.cf2_reset(self._ctx, _native.ptr(m), self.obs.data_ptr(), self.stream), "cf2_reset")
+        return self.obs
+
+    def step(self, actions: torch.Tensor, dstb: torch.Tensor | None = None):
+        a = actions
+        if a.device != self.device or a.dtype != torch.float32 or not a.is_contiguous() or a.data_ptr() % 16:
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        if a.shape != (self.num_envs, 4):
+            raise ValueError(f"actions must be [{self.num_envs}, 4], got {tuple(a.shape)}")
+        d = None
+        if self.cfg.disturbance == DSTB_EXTERNAL:
+            if dstb is None:
+                raise ValueError("this env takes an external disturbance tensor dstb[N,3]")
+            d = dstb.to(device=self.device, dtype=torch.float32).contiguous()
+        if self.cfg.disturbance == DSTB_HJ and self._tables is None:
+            raise _native.CF2Error("HJ-adversary env: bind value tables with bind_hj_tables() first")
+        _native.check(self.lib.cf2_step(
+            self._ctx, a.data_ptr(), _native.ptr(d), self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
+            self.trunc.data_ptr(), self.cost.data_ptr(), self.level.data_ptr(), _native.ptr(self.final_obs),
+            self.stream), "cf2_step")
+        info = {"cost": self.cost, "truncated": self.trunc, "disturbance_level": self.level}
+        if self.final_obs is not None:
+            info["final_obs"] = self.final_obs
+        return self.obs, self.rew, self.done, info
+
+    def step_raw(self, act_ptr: int, obs_ptr: int | None = None):
+        """Launch one env-step with raw device pointers (benchmark / graph-capture helper)."""
+        _native.check(self.lib.cf2_step(
+            self._ctx, act_ptr, None, obs_ptr or self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
+            None, None, None, None, self.stream), "cf2_step")
+
+    # ---- state snapshot ----
+    def get_state(self):
+        sf = torch.empty(self.layout.num_float_fields, self.num_envs, dtype=torch.float32, device=self.device)
+        si = torch.empty(self.layout.num_int_fields, self.num_envs, dtype=torch.int32, device=self.device)
+        _native.check(self.lib.cf2_get_state(self._ctx, sf.data_ptr(), si.data_ptr(), self.stream), "cf2_get_state")
+        return sf, si
+
+    def set_state(self, sf: torch.Tensor, si: torch.Tensor):
+        sf = sf.to(self.device, torch.float32).contiguous()
+        si = si.to(self.device, torch.int32).contiguous()
+        if sf.shape != (self.layout.num_float_fields, self.num_envs) or si.shape != (self.layout.num_int_fields, self.num_envs):
+            raise ValueError("state tensors do not match cf2_layout")
+        _native.check(self.lib.cf2_set_state(self._ctx, sf.data_ptr(), si.data_ptr(), self.stream), "cf2_set_state")
+
+    def gather_observations(self, group=None) -> torch.Tensor:
+        """RCCL all-gather of every rank's obs slab (optional policy-side exchange; the physics
+        itself needs no collective).  Returns [world * N, obs_dim]."""
+        import torch.distributed as dist
+        world = dist.get_world_size(group)
+        out = torch.empty(world * self.num_envs, self.obs_dim, dtype=self.obs.dtype, device=self.device)
+        dist.all_gather_into_tensor(out, self.obs, group=group)
+        return out
+
+
+def hj_disturbance(V: torch.Tensor, states: torch.Tensor, level: float, cfg: CF2Config | None = None):
+    """Batched ``distur_gener(states, level)`` (distur_gener.py:19-183) on the GPU:
+    states [n, 6] = [roll, pitch, yaw, p, q, r] -> (u_opt [n,3], d_opt [n,3])."""
+    lib = _native.load()
+    if cfg is None:
+        cfg = build_config("DroneHoverBulletFreeEnvWithAdversary-v0", 1)
+    if not float(level) <= 3.0:
+        raise AssertionError("disturbance level must be <= 3.0 (distur_gener.py:154)")
+    s = states.to(torch.float32).contiguous()
+    n = s.shape[0]
+    d = torch.empty(n, 3, dtype=torch.float32, device=s.device)
+    u = torch.empty(n, 3, dtype=torch.float32, device=s.device)
+    Vf = V.reshape(-1).to(s.device, torch.float32).contiguous()
+    _native.check(lib.cf2_hj_disturbance(ctypes.byref(cfg), Vf.data_ptr(), s.data_ptr(), n, float(level),
+                                         d.data_ptr(), u.data_ptr(), torch.cuda.current_stream(s.device).cuda_stream),
+                  "cf2_hj_disturbance")
+    return u, d

@@ -1,0 +1,314 @@
+// cf2sim_api.cpp -- C ABI (include/cf2sim.h) over the HIP kernels.
+//
+// The context owns the SoA state in HBM; every I/O buffer is a caller-owned device pointer.
+// No entry point allocates, frees or synchronises after cf2_create, so cf2_step /
+// cf2_reset can be captured into a hipGraph by the caller.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+#include <new>
+
+#include "../../include/cf2sim.h"
+#include "cf2sim_internal.h"
+
+using namespace cf2;
+
+struct cf2_ctx {
+    cf2_config cfg;
+    KParams P;
+    KTables T;
+    KTables* tab_dev = nullptr;
+    float* sf = nullptr;
+    int32_t* si = nullptr;
+    int device = 0;
+};
+
+static thread_local int g_last_hip_error = 0;
+
+static int hip_fail(hipError_t e) {
+    g_last_hip_error = (int)e;
+    return e == hipErrorOutOfMemory ? CF2_ERR_OUT_OF_MEMORY : CF2_ERR_HIP;
+}
+
+static int validate(const cf2_config* c) {
+    if (!c) return CF2_ERR_INVALID_ARG;
+    if (c->num_envs == 0 || c->num_envs > CF2_MAX_ENVS_PER_CTX) return CF2_ERR_INVALID_ARG;
+    if (c->physics != CF2_PHYS_BULLET && c->physics != CF2_PHYS_SIMPLE) return CF2_ERR_INVALID_ARG;
+    if (c->task != CF2_TASK_HOVER && c->task != CF2_TASK_HOVER_FREE) return CF2_ERR_INVALID_ARG;
+    if (c->disturbance < CF2_DSTB_NONE || c->disturbance > CF2_DSTB_HJ) return CF2_ERR_INVALID_ARG;
+    if (c->level_mode != CF2_LEVEL_FIXED && c->level_mode != CF2_LEVEL_BOLTZMANN) return CF2_ERR_INVALID_ARG;
+    if (c->aggregate_phy_steps < 1 || c->aggregate_phy_steps > 4) return CF2_ERR_UNSUPPORTED;
+    if (c->obs_rate < 1) return CF2_ERR_INVALID_ARG;
+    if (c->buf_size < 1 || c->buf_size > 4) return CF2_ERR_UNSUPPORTED;
+    if (c->num_levels < 1 || c->num_levels > CF2_NUM_LEVELS_MAX) return CF2_ERR_INVALID_ARG;
+    if (c->time_step <= 0.0 || c->mass <= 0.0) return CF2_ERR_INVALID_ARG;
+    return CF2_OK;
+}
+
+static void fill_tables(const cf2_config* c, KTables& T) {
+    memset(&T, 0, sizeof(T));
+    for (int k = 0; k < CF2_NUM_LEVELS_MAX; ++k) {
+        T.level_values[k] = (float)c->level_values[k];
+        T.level_cdf[k] = c->level_cdf[k];
+        T.table_of_level[k] = -1;
+    }
+    for (int d = 0; d < 6; ++d)
+        for (int k = 0; k < HJ_PTS; ++k) T.hj_grid[d][k] = c->hj_grid_points[d][k];
+}
+
+static void fill_params(const cf2_config* c, KParams& P) {
+    memset(&P, 0, sizeof(P));
+    P.N = c->num_envs;
+    P.gid_off = c->env_id_offset;
+    P.key0 = (uint32_t)(c->seed & 0xffffffffu);
+    P.key1 = (uint32_t)(c->seed >> 32);
+    P.agg = c->aggregate_phy_steps;
+    P.obs_rate = c->obs_rate;
+    P.buf_size = c->buf_size;
+    P.use_latency = c->use_latency;
+    P.use_motor_dyn = c->use_motor_dynamics;
+    P.max_steps = c->max_episode_steps;
+    P.auto_reset = c->auto_reset;
+    P.reset_dist = c->enable_reset_distribution;
+    P.dstb_mode = c->disturbance;
+    P.level_mode = c->level_mode;
+    P.num_levels = c->num_levels;
+    P.gust_dur = c->gust_duration;
+    P.noise = c->observation_noise_on;
+    P.dr = c->domain_randomization_on;
+    P.phys = c->physics;
+    P.held_persistent = (c->aggregate_phy_steps % c->obs_rate) != 0;
+    P.time_step = (float)c->time_step;
+    P.mass = (float)c->mass;
+    P.ixx = (float)c->ixx; P.iyy = (float)c->iyy; P.izz = (float)c->izz;
+    P.ft0 = (float)c->ft0; P.ft1 = (float)c->ft1;
+    P.K = (float)c->K; P.A = (float)c->A; P.B = (float)c->B;
+    P.hover_x = (float)c->hover_x; P.hover_action = (float)c->hover_action;
+    P.ou_sigma = (float)(0.2 * c->motor_thrust_noise);          // agents.py:206
+    P.drag_xy = (float)c->drag_xy; P.drag_z = (float)c->drag_z;
+    P.g_world = (float)c->gravity_world; P.g_agent = (float)c->gravity_agent;
+    P.arm = (float)c->arm;
+    P.prop_xy = (float)c->prop_xy; P.prop_z = (float)c->prop_z;
+    P.prop_mass = (float)c->prop_mass; P.prop_inertia = (float)c->prop_inertia;
+    P.prop_speed_gain = (float)c->prop_speed_gain;
+    P.lin_damping = (float)c->lin_damping; P.ang_damping = (float)c->ang_damping;
+    P.vmax = (float)c->max_coord_velocity;
+    for (int k = 0; k < 3; ++k) P.init_xyz[k] = (float)c->init_xyz[k];
+    P.pos_lim = (float)c->reset_pos_lim; P.angle_lim = (float)c->reset_angle_lim; P.yaw_lim = (float)c->reset_yaw_lim;
+    P.vel_lim = (float)c->reset_vel_lim; P.rate_lim = (float)c->reset_rate_lim;
+    P.yaw_rate_lim = (float)c->reset_yaw_rate_lim;
+    P.action_std = (float)c->action_init_std; P.motor_std = (float)c->motor_init_std;
+    const double f = c->domain_randomization;
+    const double dr_val[9] = {c->time_step, c->mass, c->ixx, c->iyy, c->izz, c->ft0, c->ft1,
+                              c->motor_time_constant, c->thrust2weight};
+    for (int k = 0; k < 9; ++k) {                                  // base.py:253-259 bounds
+        P.dr_lo[k] = (float)(dr_val[k] - f * dr_val[k]);
+        P.dr_hi[k] = (float)(dr_val[k] + f * dr_val[k]);
+    }
+    P.pos_std = (float)c->pos_norm_std; P.pos_unif = (float)c->pos_unif_range;
+    P.vel_std = (float)c->vel_norm_std;
+    P.rot_std = (float)c->rot_norm_std; P.rot_unif = (float)c->rot_unif_range;
+    {                                                              // sensors.py:123-127
+        const double dt = 1.0 / c->sim_freq;
+        const double sgd = c->gyro_noise_density / sqrt(dt);
+        const double sbgd = sqrt(-(sgd * sgd) * (c->gyro_bias_corr_time / 2.0) *
+                                 (exp(-2.0 * dt / c->gyro_bias_corr_time) - 1.0));
+        P.pgd = (float)exp(-dt / c->gyro_bias_corr_time);
+        P.sbgd = (float)sbgd;
+    }
+    P.gyro_rw = (float)c->gyro_random_walk; P.gyro_ton = (float)c->gyro_turn_on_bias_sigma;
+    P.lpf_gain = (float)c->lpf_gain; P.lpf_ratio = (float)c->lpf_ratio;
+    P.pen_action = (float)c->penalty_action; P.pen_angle = (float)c->penalty_angle;
+    P.pen_spin = (float)c->penalty_spin; P.pen_term = (float)c->penalty_terminal;
+    P.pen_vel = (float)c->penalty_velocity; P.pen_z = (float)c->penalty_z;
+    P.pen_arp = (float)c->penalty_arp; P.pen_dist = (float)c->penalty_dist;
+    for (int k = 0; k < 3; ++k) {
+        P.target_pos[k] = (float)c->target_pos[k];
+        P.target_rpy[k] = (float)c->target_rpy[k];
+        P.target_rate[k] = (float)c->target_rate[k];
+    }
+    P.done_rp = (float)c->done_rp_limit; P.done_rate_deg = (float)c->done_rate_limit_deg;
+    P.done_zmin = (float)c->done_z_min;
+    P.cost_xy = (float)c->cost_xy_lim; P.cost_z = (float)c->cost_z_lim; P.cost_rp = (float)c->cost_rp_lim;
+    P.cost_vel = (float)c->cost_vel_lim; P.cost_rate = (float)c->cost_rate_lim;
+    P.level_fixed = (float)c->dstb_level;
+    for (int k = 0; k < 3; ++k) {
+        P.umax[k] = (float)c->dstb_umax[k];
+        P.umax_d[k] = c->dstb_umax[k];
+        P.uni_hi[k] = c->dstb_uniform_hi[k];
+    }
+    P.gust_p = (float)c->gust_onset_prob;
+    P.gust_max = (float)c->gust_max_level;
+    P.tab = nullptr;
+    P.V = nullptr;
+}
+
+extern "C" {
+
+int cf2_abi_version(void) { return CF2SIM_ABI_VERSION; }
+size_t cf2_config_sizeof(void) { return sizeof(cf2_config); }
+int cf2_last_hip_error(void) { return g_last_hip_error; }
+
+const char* cf2_status_string(int s) {
+    switch (s) {
+    case CF2_OK: return "ok";
+    case CF2_ERR_INVALID_ARG: return "invalid argument";
+    case CF2_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case CF2_ERR_HIP: return "HIP runtime error";
+    case CF2_ERR_UNSUPPORTED: return "unsupported configuration";
+    case CF2_ERR_NO_TABLE: return "HJ disturbance requested but no value table bound";
+    default: return "unknown status";
+    }
+}
+
+int cf2_create(const cf2_config* cfg, cf2_ctx** out_ctx) {
+    if (!out_ctx) return CF2_ERR_INVALID_ARG;
+    *out_ctx = nullptr;
+    const int v = validate(cfg);
+    if (v) return v;
+    cf2_ctx* ctx = new (std::nothrow) cf2_ctx();
+    if (!ctx) return CF2_ERR_OUT_OF_MEMORY;
+    ctx->cfg = *cfg;
+    fill_params(cfg, ctx->P);
+    fill_tables(cfg, ctx->T);
+    hipError_t e = hipGetDevice(&ctx->device);
+    if (e != hipSuccess) { delete ctx; return hip_fail(e); }
+    const size_t N = cfg->num_envs;
+    e = hipMalloc((void**)&ctx->tab_dev, sizeof(KTables));
+    if (e == hipSuccess) e = hipMemcpy(ctx->tab_dev, &ctx->T, sizeof(KTables), hipMemcpyHostToDevice);
+    ctx->P.tab = ctx->tab_dev;
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->sf, sizeof(float) * NF * N);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->si, sizeof(int32_t) * NI * N);
+    if (e == hipSuccess) e = launch_init(ctx->P, ctx->sf, ctx->si, 0);
+    if (e == hipSuccess) e = hipStreamSynchronize(0);
+    if (e != hipSuccess) {
+        (void)hipFree(ctx->sf);
+        (void)hipFree(ctx->si);
+        (void)hipFree(ctx->tab_dev);
+        delete ctx;
+        return hip_fail(e);
+    }
+    *out_ctx = ctx;
+    return CF2_OK;
+}
+
+int cf2_destroy(cf2_ctx* ctx) {
+    if (!ctx) return CF2_ERR_INVALID_ARG;
+    hipError_t e1 = hipFree(ctx->sf);
+    hipError_t e2 = hipFree(ctx->si);
+    (void)hipFree(ctx->tab_dev);
+    delete ctx;
+    if (e1 != hipSuccess) return hip_fail(e1);
+    if (e2 != hipSuccess) return hip_fail(e2);
+    return CF2_OK;
+}
+
+int cf2_layout_get(const cf2_ctx* ctx, cf2_layout* o) {
+    if (!ctx || !o) return CF2_ERR_INVALID_ARG;
+    memset(o, 0, sizeof(*o));
+    o->num_envs = ctx->cfg.num_envs;
+    o->num_float_fields = NF;
+    o->num_int_fields = NI;
+    o->obs_len = ctx->cfg.observation_noise_on ? 13 : 17;
+    o->obs_dim = 2 * (o->obs_len + 4);
+    o->f_pos = F_POS; o->f_quat = F_QUAT; o->f_vel = F_VEL; o->f_omega = F_OMEGA; o->f_rpy = F_RPY;
+    o->f_motor = F_MOTOR; o->f_ou = F_OU; o->f_abuf = F_ABUF; o->f_bias = F_BIAS; o->f_lpf = F_LPF;
+    o->f_held = F_HELD; o->f_obs_prev = F_OBS_PREV; o->f_hist_act = F_HIST_ACT; o->f_param = F_PARAM;
+    o->f_dstb = F_DSTB;
+    o->i_ep_step = I_EP_STEP; o->i_rng = I_RNG; o->i_flags = I_FLAGS; o->i_level = I_LEVEL; o->i_gust = I_GUST;
+    o->num_params = NUM_PARAMS;
+    return CF2_OK;
+}
+
+int cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables, const int32_t* table_of_level) {
+    if (!ctx || !V_dev || num_tables <= 0 || !table_of_level) return CF2_ERR_INVALID_ARG;
+    for (int l = 0; l < ctx->cfg.num_levels; ++l)
+        if (table_of_level[l] >= num_tables) return CF2_ERR_INVALID_ARG;
+    for (int l = 0; l < ctx->cfg.num_levels; ++l) ctx->T.table_of_level[l] = table_of_level[l];
+    const hipError_t e = hipMemcpy(ctx->tab_dev, &ctx->T, sizeof(KTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e);
+    ctx->P.V = V_dev;
+    return CF2_OK;
+}
+
+int cf2_reset(cf2_ctx* ctx, const uint8_t* mask_dev, float* obs_dev, void* stream) {
+    if (!ctx) return CF2_ERR_INVALID_ARG;
+    const hipError_t e = launch_reset(ctx->P, ctx->sf, ctx->si, mask_dev, obs_dev, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* obs_dev, float* rew_dev,
+             uint8_t* done_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, float* final_obs_dev,
+             void* stream) {
+    if (!ctx || !act_dev || !obs_dev || !rew_dev || !done_dev) return CF2_ERR_INVALID_ARG;
+    if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL && !dstb_dev) return CF2_ERR_INVALID_ARG;
+    if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
+    if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
+    if (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
+    StepIO io{ctx->sf, ctx->si, act_dev, dstb_dev, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev,
+              final_obs_dev};
+    const hipError_t e = launch_step(ctx->P, io, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems, float* obs_dev, float* rew_dev,
+                uint8_t* done_dev, void* stream) {
+    if (!ctx || K < 1 || !act_dev) return CF2_ERR_INVALID_ARG;
+    if (act_stride_elems < (size_t)ctx->cfg.num_envs * 4 && K > 1) return CF2_ERR_INVALID_ARG;
+    for (int k = 0; k < K; ++k) {
+        const int r = cf2_step(ctx, act_dev + (size_t)k * act_stride_elems, nullptr, obs_dev, rew_dev, done_dev,
+                               nullptr, nullptr, nullptr, nullptr, stream);
+        if (r) return r;
+    }
+    return CF2_OK;
+}
+
+int cf2_get_state(const cf2_ctx* ctx, float* state_f_dev, int32_t* state_i_dev, void* stream) {
+    if (!ctx || !state_f_dev || !state_i_dev) return CF2_ERR_INVALID_ARG;
+    const size_t N = ctx->cfg.num_envs;
+    hipError_t e = hipMemcpyAsync(state_f_dev, ctx->sf, sizeof(float) * NF * N, hipMemcpyDeviceToDevice,
+                                  (hipStream_t)stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(state_i_dev, ctx->si, sizeof(int32_t) * NI * N, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+int cf2_set_state(cf2_ctx* ctx, const float* state_f_dev, const int32_t* state_i_dev, void* stream) {
+    if (!ctx || !state_f_dev || !state_i_dev) return CF2_ERR_INVALID_ARG;
+    const size_t N = ctx->cfg.num_envs;
+    hipError_t e = hipMemcpyAsync(ctx->sf, state_f_dev, sizeof(float) * NF * N, hipMemcpyDeviceToDevice,
+                                  (hipStream_t)stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->si, state_i_dev, sizeof(int32_t) * NI * N, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+int cf2_hj_disturbance(const cf2_config* cfg, const float* V_dev, const float* states_dev, uint32_t n, float level,
+                       float* dstb_dev, float* uopt_dev, void* stream) {
+    if (!cfg || !V_dev || !states_dev || !dstb_dev) return CF2_ERR_INVALID_ARG;
+    if (!(level <= 3.0f)) return CF2_ERR_INVALID_ARG;            // assert disturbance <= 3.0 (distur_gener.py:154)
+    // the grid nodes travel in a small per-call device table; no allocation on the hot path:
+    // the table lives in a static device buffer sized for one KTables.
+    static KTables* s_tab = nullptr;
+    static int s_dev = -1;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e);
+    if (!s_tab || s_dev != dev) {
+        e = hipMalloc((void**)&s_tab, sizeof(KTables));
+        if (e != hipSuccess) return hip_fail(e);
+        s_dev = dev;
+    }
+    KParams P;
+    KTables T;
+    fill_params(cfg, P);
+    fill_tables(cfg, T);
+    e = hipStreamSynchronize((hipStream_t)stream);   // previous users of s_tab on this stream are done
+    if (e == hipSuccess) e = hipMemcpy(s_tab, &T, sizeof(KTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e);
+    P.tab = s_tab;
+    e = launch_hj(P, V_dev, states_dev, n, level, dstb_dev, uopt_dev, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+}  // extern "C"

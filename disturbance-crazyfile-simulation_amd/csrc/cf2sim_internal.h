@@ -1,0 +1,94 @@
+// cf2sim_internal.h -- kernel parameter block and SoA field map shared by the HIP kernels
+// and the C-ABI layer (not part of the public ABI; see include/cf2sim.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cf2 {
+
+// ---- float state fields: state_f[field * N + env] (DESIGN.md "State layout") ----
+enum : int {
+    F_POS = 0,          // 3  base position, world
+    F_QUAT = 3,         // 4  base orientation (x,y,z,w), world
+    F_VEL = 7,          // 3  base linear velocity, world
+    F_OMEGA = 10,       // 3  bullet: angular velocity, world  | simple: body rates (drone.rpy_dot)
+    F_RPY = 13,         // 3  simple only: integrated rpy (drone.rpy)
+    F_MOTOR = 16,       // 4  first-order motor state x
+    F_OU = 20,          // 4  OU thrust-noise state
+    F_ABUF = 24,        // 16 latency ring action_buffer[4][4] (buf_size rows used)
+    F_BIAS = 40,        // 3  gyro bias (SensorNoise.gyro_bias)
+    F_LPF = 43,         // 3  gyro low-pass filter state
+    F_HELD = 46,        // 10 held 100 Hz measurement (xyz, quat, vel); persistent only if agg % obs_rate
+    F_OBS_PREV = 56,    // 17 previous observation o_{k-1} (13 used with noise)
+    F_HIST_ACT = 73,    // 8  action_history [2][4]
+    F_PARAM = 81,       // 19 per-env DR params: dt, m, Jx, Jy, Jz, k0, k1, A[4], B[4], K[4]
+    F_DSTB = 100,       // 3  per-episode / current-gust disturbance torque
+    F_LEVEL = 103,      // 1  disturbance level of the episode
+    NF = 104
+};
+// ---- int state fields ----
+enum : int {
+    I_EP_STEP = 0,      // env-steps since reset (TimeLimit, iteration = ep_step * agg)
+    I_RNG = 1,          // Philox counter (one per env-step / reset)
+    I_FLAGS = 2,        // bits 0-3 action_idx, 4-5 action_history alias bits, 6 last_action alias
+    I_LEVEL = 3,        // Boltzmann level index / HJ table row
+    I_GUST = 4,         // env-steps left in the current gust
+    NI = 5
+};
+enum { NUM_PARAMS = 19 };
+enum { HJ_PTS = 15, HJ_TABLE = 11390625 };
+enum { PHYS_BULLET_T = 0, PHYS_SIMPLE_T = 1 };
+enum { DSTB_NONE_T = 0, DSTB_EXTERNAL_T = 1, DSTB_UNIFORM_T = 2, DSTB_CONST_T = 3, DSTB_GUST_T = 4, DSTB_HJ_T = 5 };
+enum { LEVEL_FIXED_T = 0, LEVEL_BOLTZMANN_T = 1 };
+enum : uint32_t { TAG_STEP = 1, TAG_RESET = 2 };
+
+// Kernel parameter block, passed by value (kernarg segment -> scalar loads).
+struct KParams {
+    uint32_t N, gid_off, key0, key1;
+    int32_t agg, obs_rate, buf_size, use_latency, use_motor_dyn, max_steps, auto_reset, reset_dist;
+    int32_t dstb_mode, level_mode, num_levels, gust_dur, noise, dr, phys, held_persistent;
+    float time_step, mass, ixx, iyy, izz, ft0, ft1, K, A, B, hover_x, hover_action, ou_sigma;
+    float drag_xy, drag_z, g_world, g_agent, arm, prop_xy, prop_z, prop_mass, prop_inertia, prop_speed_gain;
+    float lin_damping, ang_damping, vmax;
+    float init_xyz[3], pos_lim, angle_lim, yaw_lim, vel_lim, rate_lim, yaw_rate_lim, action_std, motor_std;
+    float dr_lo[9], dr_hi[9];     // dt, m, Jx, Jy, Jz, k0, k1, mtc, t2w
+    float pos_std, pos_unif, vel_std, rot_std, rot_unif, pgd, sbgd, gyro_rw, gyro_ton, lpf_gain, lpf_ratio;
+    float pen_action, pen_angle, pen_spin, pen_term, pen_vel, pen_z, pen_arp, pen_dist;
+    float target_pos[3], target_rpy[3], target_rate[3];
+    float done_rp, done_rate_deg, done_zmin, cost_xy, cost_z, cost_rp, cost_vel, cost_rate;
+    float level_fixed, umax[3], gust_p, gust_max;
+    double umax_d[3], uni_hi[3];
+    const struct KTables* tab;   // device-resident lookup tables (dynamically indexed)
+    const float* V;              // HJ value tables [num_tables][15^6]
+};
+
+// Lookup tables indexed with per-env (divergent) indices: kept in device memory, not in the
+// kernarg block (a dynamically indexed by-value kernel argument is copied to scratch).
+struct KTables {
+    double level_cdf[32];
+    float level_values[32];
+    int32_t table_of_level[32];
+    double hj_grid[6][HJ_PTS];
+};
+
+struct StepIO {
+    float* sf;
+    int32_t* si;
+    const float* act;
+    const float* dstb;
+    float* obs;
+    float* rew;
+    uint8_t* done;
+    uint8_t* trunc;
+    float* cost;
+    float* level;
+    float* final_obs;
+};
+
+hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
+hipError_t launch_reset(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s);
+hipError_t launch_init(const KParams& P, float* sf, int32_t* si, hipStream_t s);
+hipError_t launch_hj(const KParams& P, const float* V, const float* states, uint32_t n, float level, float* dstb,
+                     float* uopt, hipStream_t s);
+
+}  // namespace cf2

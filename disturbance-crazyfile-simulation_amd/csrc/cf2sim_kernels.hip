@@ -1,0 +1,1058 @@
+// cf2sim_kernels.hip -- fused CDNA4 (gfx950) env-step / reset kernels for the batched
+// CrazyFlie hover environment.
+//
+// One lane = one env.  Env state is structure-of-arrays in HBM (field-major, DESIGN.md
+// "State layout"), so every field load/store of a wave is one contiguous 256-B transaction.
+// A step loads the state once, runs aggregate_phy_steps physics sub-steps plus the
+// observation / history / reward / done epilogue (and the auto-reset of finished envs) in
+// registers, and stores the state once: the kernel is HBM-bound by construction (no MFMA:
+// the work is per-env element-wise, not a contraction).
+//
+// What each piece restates (reference paths, phoenix_drone_simulation/ omitted):
+//   apply_action            envs/agents.py:259-298, envs/control.py:94-100, envs/utils.py:130-134
+//   force/torque assembly   envs/physics.py:213-250, envs/agents.py:300-337,517-533
+//   rigid-body step         bullet3 3.21 btMultiBody (third party; see oracle/cf2_oracle.c header)
+//   SimplePhysics           envs/physics.py:130-200
+//   update_information      envs/agents.py:434-453
+//   compute_observation     envs/hover_free.py:168-200, envs/sensors.py:75-134, envs/utils.py:102-105
+//   compute_history         envs/base.py:305-321
+//   reward / done / cost    envs/hover_free.py:124-235,449-461, envs/hover.py:102-202
+//   reset + DR              envs/base.py:241-298,420-464, envs/hover_free.py:237-289
+//   HJ disturbance          adversarial_generation/FasTrack_data/distur_gener.py:19-207,
+//                           adversarial_generation/odp/Grid/GridProcessing.py:52-71
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "cf2sim_internal.h"
+
+namespace cf2 {
+
+// ------------------------------------------------------------------------------------
+// Philox4x32-10 counter RNG (same stream as oracle/cf2_oracle.c)
+// ------------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                     uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    return U4{c0, c1, c2, c3};
+}
+
+struct Rng {
+    uint32_t k0, k1, ctr, gid, tag;
+    __device__ __forceinline__ U4 block(uint32_t b) const { return philox(b, ctr, gid, tag, k0, k1); }
+};
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
+
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+    const float u1 = ((float)(a >> 8) + 1.0f) * 5.9604644775390625e-08f;
+    const float u2 = (float)(b >> 8) * 5.9604644775390625e-08f;
+    const float r = sqrtf(-2.0f * logf(u1));
+    const float th = 6.283185307179586f * u2;
+    float s, c;
+    sincosf(th, &s, &c);
+    z0 = r * c;
+    z1 = r * s;
+}
+
+// N normals from consecutive blocks starting at b0 (pair k uses u32 2k, 2k+1)
+template <int N>
+__device__ __forceinline__ void normals(const Rng& g, uint32_t b0, float (&z)[N]) {
+#pragma unroll
+    for (int blk = 0; blk < (N + 3) / 4; ++blk) {
+        const U4 u = g.block(b0 + blk);
+        float a0, a1, a2, a3;
+        box_muller(u.x, u.y, a0, a1);
+        if (4 * blk + 0 < N) z[4 * blk + 0] = a0;
+        if (4 * blk + 1 < N) z[4 * blk + 1] = a1;
+        if (4 * blk + 2 < N) {
+            box_muller(u.z, u.w, a2, a3);
+            z[4 * blk + 2] = a2;
+            if (4 * blk + 3 < N) z[4 * blk + 3] = a3;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// rotation helpers (PyBullet C-API semantics)
+// ------------------------------------------------------------------------------------
+struct M3 { float m[9]; };
+
+__device__ __forceinline__ M3 rotmat(const float q[4]) {
+    const float x = q[0], y = q[1], z = q[2], w = q[3];
+    const float d = x * x + y * y + z * z + w * w;
+    const float s = 2.0f / d;
+    const float xs = x * s, ys = y * s, zs = z * s;
+    const float wx = w * xs, wy = w * ys, wz = w * zs;
+    const float xx = x * xs, xy = x * ys, xz = x * zs;
+    const float yy = y * ys, yz = y * zs, zz = z * zs;
+    M3 r;
+    r.m[0] = 1.0f - (yy + zz); r.m[1] = xy - wz;          r.m[2] = xz + wy;
+    r.m[3] = xy + wz;          r.m[4] = 1.0f - (xx + zz); r.m[5] = yz - wx;
+    r.m[6] = xz - wy;          r.m[7] = yz + wx;          r.m[8] = 1.0f - (xx + yy);
+    return r;
+}
+__device__ __forceinline__ void mv(const M3& R, const float v[3], float o[3]) {
+    o[0] = R.m[0] * v[0] + R.m[1] * v[1] + R.m[2] * v[2];
+    o[1] = R.m[3] * v[0] + R.m[4] * v[1] + R.m[5] * v[2];
+    o[2] = R.m[6] * v[0] + R.m[7] * v[1] + R.m[8] * v[2];
+}
+__device__ __forceinline__ void mtv(const M3& R, const float v[3], float o[3]) {
+    o[0] = R.m[0] * v[0] + R.m[3] * v[1] + R.m[6] * v[2];
+    o[1] = R.m[1] * v[0] + R.m[4] * v[1] + R.m[7] * v[2];
+    o[2] = R.m[2] * v[0] + R.m[5] * v[1] + R.m[8] * v[2];
+}
+__device__ __forceinline__ float norm3(const float v[3]) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+// Makes a register value opaque to the optimiser.  Used before data-dependent selects among
+// Env fields: otherwise InstCombine turns select(c, load p, load q) chains into a load of a
+// select of pointers, SROA can no longer promote the Env struct and it lands in scratch.
+__device__ __forceinline__ float opaque(float x) { asm("" : "+v"(x)); return x; }
+
+__device__ __forceinline__ void quat_from_euler(const float e[3], float q[4]) {
+    const float phi = e[0] * 0.5f, the = e[1] * 0.5f, psi = e[2] * 0.5f;
+    float sp, cp, st, ct, ss, cs;
+    sincosf(phi, &sp, &cp);
+    sincosf(the, &st, &ct);
+    sincosf(psi, &ss, &cs);
+    const float x = sp * ct * cs - cp * st * ss;
+    const float y = cp * st * cs + sp * ct * ss;
+    const float z = cp * ct * ss - sp * st * cs;
+    const float w = cp * ct * cs + sp * st * ss;
+    const float len = sqrtf(x * x + y * y + z * z + w * w);
+    q[0] = x / len; q[1] = y / len; q[2] = z / len; q[3] = w / len;
+}
+__device__ __forceinline__ void euler_from_quat(const float q[4], float e[3]) {
+    const float sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
+    const float sarg = -2.0f * (q[0] * q[2] - q[3] * q[1]);
+    if (sarg <= -0.99999f) {
+        e[0] = 0.0f; e[1] = -0.5f * 3.141592653589793f; e[2] = 2.0f * atan2f(q[0], -q[1]);
+    } else if (sarg >= 0.99999f) {
+        e[0] = 0.0f; e[1] = 0.5f * 3.141592653589793f; e[2] = 2.0f * atan2f(-q[0], q[1]);
+    } else {
+        e[0] = atan2f(2.0f * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+        e[1] = asinf(sarg);
+        e[2] = atan2f(2.0f * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+    }
+}
+__device__ __forceinline__ void quat2euler(const float q[4], float e[3]) {
+    const float x = q[0], y = q[1], z = q[2], w = q[3];
+    const float t0 = 2.0f * (w * x + y * z);
+    const float t1 = 1.0f - 2.0f * (x * x + y * y);
+    e[0] = atan2f(t0, t1);
+    float t2 = 2.0f * (w * y - z * x);
+    t2 = t2 > 1.0f ? 1.0f : t2;
+    t2 = t2 < -1.0f ? -1.0f : t2;
+    e[1] = asinf(t2);
+    const float t3 = 2.0f * (w * z + x * y);
+    const float t4 = 1.0f - 2.0f * (y * y + z * z);
+    e[2] = atan2f(t3, t4);
+}
+
+// ------------------------------------------------------------------------------------
+// HJ value-table gather (7 taps: centre and +-1 along the three rate dims)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int grid_nearest(const double* pts, double s) {
+    int idx = 0;
+#pragma unroll
+    for (int k = 0; k < HJ_PTS; ++k) idx += pts[k] < s ? 1 : 0;   // searchsorted(side='left') on sorted pts
+    if (idx > 0 && (idx == HJ_PTS || fabs(s - pts[idx - 1]) < fabs(s - pts[idx]))) return idx - 1;
+    return idx;
+}
+__device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+// returns bit i set <=> dV/dx_{3+i} > 0 (opt disturbance = -dmax_i)
+__device__ __forceinline__ unsigned hj_signs(const KParams& P, const float* __restrict__ V, const double st[6]) {
+    int idx[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) idx[d] = grid_nearest(P.tab->hj_grid[d], st[d]);
+    const int stride[6] = {759375, 50625, 3375, 225, 15, 1};
+    int c = 0;
+#pragma unroll
+    for (int d = 0; d < 6; ++d) c += idx[d] * stride[d];
+    const float Vc = V[c];
+    unsigned bits = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int d = 3 + i;
+        const int s = stride[d];
+        float L, Rr;
+        if (idx[d] == 0) {
+            const float Vn = V[c + s];
+            const float lb = __fadd_rn(Vc, __fmul_rn(fabsf(__fsub_rn(Vn, Vc)), sgnf(Vc)));
+            L = __fsub_rn(Vc, lb); Rr = __fsub_rn(Vn, Vc);
+        } else if (idx[d] == HJ_PTS - 1) {
+            const float Vp = V[c - s];
+            const float rb = __fadd_rn(Vc, __fmul_rn(fabsf(__fsub_rn(Vc, Vp)), sgnf(Vc)));
+            L = __fsub_rn(Vc, Vp); Rr = __fsub_rn(rb, Vc);
+        } else {
+            const float Vp = V[c - s], Vn = V[c + s];
+            L = __fsub_rn(Vc, Vp); Rr = __fsub_rn(Vn, Vc);
+        }
+        bits |= (L > -Rr ? 1u : 0u) << i;
+    }
+    return bits;
+}
+
+// ------------------------------------------------------------------------------------
+// per-env register state
+// ------------------------------------------------------------------------------------
+struct Env {
+    float p[3], q[4], v[3], w[3];   // w: world angular velocity (bullet) / body rates (simple)
+    float rpy[3], wb[3];            // derived readback (drone.rpy, drone.rpy_dot)
+    float x[4], ou[4], abuf[4][4];
+    float bias[3], lpf[3], held[10];
+    float obs_prev[17];
+    float hact[2][4];
+    float dt, m, J[3], k0, k1, A[4], B[4], K[4];
+    float dstb[3], level;
+    int ep_step, aidx, halias0, halias1, la_view, level_idx, gust_left;
+    uint32_t rng;
+    float la[4];                    // drone.last_action
+};
+
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void load_env(const KParams& P, const float* __restrict__ sf,
+                                         const int32_t* __restrict__ si, uint32_t i, Env& E) {
+    const uint32_t N = P.N;
+#define LD(f) sf[(size_t)(f) * N + i]
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.p[k] = LD(F_POS + k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.q[k] = LD(F_QUAT + k);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.v[k] = LD(F_VEL + k);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.w[k] = LD(F_OMEGA + k);
+    if (PHYS == PHYS_SIMPLE_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.rpy[k] = LD(F_RPY + k);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.x[k] = LD(F_MOTOR + k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.ou[k] = LD(F_OU + k);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.abuf[r][k] = r < P.buf_size ? LD(F_ABUF + 4 * r + k) : 0.0f;
+    if (NOISE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.bias[k] = LD(F_BIAS + k);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.lpf[k] = LD(F_LPF + k);
+        if (P.held_persistent) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) E.held[k] = LD(F_HELD + k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) E.held[k] = 0.0f;
+        }
+    }
+    constexpr int OL = NOISE ? 13 : 17;
+#pragma unroll
+    for (int k = 0; k < OL; ++k) E.obs_prev[k] = LD(F_OBS_PREV + k);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.hact[s][k] = LD(F_HIST_ACT + 4 * s + k);
+    if (DR) {
+        E.dt = LD(F_PARAM + 0); E.m = LD(F_PARAM + 1);
+        E.J[0] = LD(F_PARAM + 2); E.J[1] = LD(F_PARAM + 3); E.J[2] = LD(F_PARAM + 4);
+        E.k0 = LD(F_PARAM + 5); E.k1 = LD(F_PARAM + 6);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { E.A[k] = LD(F_PARAM + 7 + k); E.B[k] = LD(F_PARAM + 11 + k); E.K[k] = LD(F_PARAM + 15 + k); }
+    } else {
+        E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
+        E.k0 = P.ft0; E.k1 = P.ft1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { E.A[k] = P.A; E.B[k] = P.B; E.K[k] = P.K; }
+    }
+    if (P.dstb_mode == DSTB_CONST_T || P.dstb_mode == DSTB_GUST_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.dstb[k] = LD(F_DSTB + k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.dstb[k] = 0.0f;
+    }
+    E.level = LD(F_LEVEL);
+#undef LD
+    E.ep_step = si[(size_t)I_EP_STEP * N + i];
+    E.rng = (uint32_t)si[(size_t)I_RNG * N + i];
+    const int fl = si[(size_t)I_FLAGS * N + i];
+    E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
+    E.level_idx = si[(size_t)I_LEVEL * N + i];
+    E.gust_left = P.dstb_mode == DSTB_GUST_T ? si[(size_t)I_GUST * N + i] : 0;
+}
+
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
+                                          uint32_t i, const Env& E, bool params_dirty) {
+    const uint32_t N = P.N;
+#define ST(f, val) sf[(size_t)(f) * N + i] = (val)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ST(F_POS + k, E.p[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ST(F_QUAT + k, E.q[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ST(F_VEL + k, E.v[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ST(F_OMEGA + k, E.w[k]);
+    if (PHYS == PHYS_SIMPLE_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ST(F_RPY + k, E.rpy[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ST(F_MOTOR + k, E.x[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ST(F_OU + k, E.ou[k]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) if (r < P.buf_size) ST(F_ABUF + 4 * r + k, E.abuf[r][k]);
+    if (NOISE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ST(F_BIAS + k, E.bias[k]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ST(F_LPF + k, E.lpf[k]);
+        if (P.held_persistent) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) ST(F_HELD + k, E.held[k]);
+        }
+    }
+    constexpr int OL = NOISE ? 13 : 17;
+#pragma unroll
+    for (int k = 0; k < OL; ++k) ST(F_OBS_PREV + k, E.obs_prev[k]);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ST(F_HIST_ACT + 4 * s + k, E.hact[s][k]);
+    if (DR && params_dirty) {
+        ST(F_PARAM + 0, E.dt); ST(F_PARAM + 1, E.m);
+        ST(F_PARAM + 2, E.J[0]); ST(F_PARAM + 3, E.J[1]); ST(F_PARAM + 4, E.J[2]);
+        ST(F_PARAM + 5, E.k0); ST(F_PARAM + 6, E.k1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { ST(F_PARAM + 7 + k, E.A[k]); ST(F_PARAM + 11 + k, E.B[k]); ST(F_PARAM + 15 + k, E.K[k]); }
+    }
+    if (P.dstb_mode == DSTB_CONST_T ? params_dirty : P.dstb_mode == DSTB_GUST_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ST(F_DSTB + k, E.dstb[k]);
+    }
+    if (params_dirty) ST(F_LEVEL, E.level);
+#undef ST
+    si[(size_t)I_EP_STEP * N + i] = E.ep_step;
+    si[(size_t)I_RNG * N + i] = (int32_t)E.rng;
+    si[(size_t)I_FLAGS * N + i] = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6);
+    if (params_dirty) si[(size_t)I_LEVEL * N + i] = E.level_idx;
+    if (P.dstb_mode == DSTB_GUST_T) si[(size_t)I_GUST * N + i] = E.gust_left;
+}
+
+// ------------------------------------------------------------------------------------
+// physics
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void apply_action(const KParams& P, Env& E, const float a[4], const float on[4],
+                                             float f[4], float& tz) {
+    float pwm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) E.la[j] = a[j];
+    E.la_view = 0;
+    if (P.use_latency) {
+        float del[4];
+        // dynamic ring index resolved with selects (no scratch)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float d = opaque(E.abuf[0][j]);
+#pragma unroll
+            for (int r = 1; r < 4; ++r) d = E.aidx == r ? opaque(E.abuf[r][j]) : d;
+            del[j] = d;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) E.abuf[r][j] = E.aidx == r ? a[j] : E.abuf[r][j];
+        E.aidx = E.aidx + 1 == P.buf_size ? 0 : E.aidx + 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pwm[j] = 30000.0f + clampf(del[j], -1.0f, 1.0f) * 30000.0f;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pwm[j] = 30000.0f + clampf(a[j], -1.0f, 1.0f) * 30000.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float xo = E.ou[j];
+        const float dx = 0.15f * (0.0f - xo) + P.ou_sigma * on[j];
+        E.ou[j] = xo + dx;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float tn = pwm[j] / 60000.0f;
+        float noisy;
+        if (P.use_motor_dyn) {
+            const float rot = sqrtf(tn);
+            E.x[j] = E.A[j] * E.x[j] + E.B[j] * rot;
+            noisy = (1.0f + E.ou[j]) * (E.x[j] * E.x[j]);
+        } else {
+            noisy = (1.0f + E.ou[j]) * tn;
+        }
+        f[j] = E.K[j] * clampf(noisy, 0.0f, 1.0f);
+    }
+    float t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j] = E.k1 * f[j] + E.k0;
+    tz = (-t[0] + t[1] - t[2] + t[3]);
+}
+
+__device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const float a[4], const float d[3],
+                                               const float on[4], bool first_after_reset) {
+    float xprev[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xprev[j] = E.x[j];
+    float f[4], tz;
+    apply_action(P, E, a, on, f, tz);
+    const M3 R = rotmat(E.q);
+    float ssum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float rpm = E.x[j] * E.x[j] * 25000.0f;
+        ssum += 2.0f * 3.141592653589793f * rpm / 60.0f;
+    }
+    const float dl[3] = {-1.0f * P.drag_xy * ssum * E.v[0], -1.0f * P.drag_xy * ssum * E.v[1], -1.0f * P.drag_z * ssum * E.v[2]};
+    float drag1[3], dragw[3];
+    mv(R, dl, drag1);
+    mv(R, drag1, dragw);
+    const float L = P.prop_xy;
+    float tb[3];
+    tb[0] = L * (-f[0] - f[1] + f[2] + f[3]) + d[0];
+    tb[1] = L * (-f[0] + f[1] + f[2] - f[3]) + d[1];
+    tb[2] = tz;
+    const float fsum = f[0] + f[1] + f[2] + f[3];
+    const float mp = P.prop_mass, Ip = P.prop_inertia, Lz = P.prop_z;
+    const float mtot = E.m + 4.0f * mp;
+    float Fw[3];
+    Fw[0] = R.m[2] * fsum + dragw[0];
+    Fw[1] = R.m[5] * fsum + dragw[1];
+    Fw[2] = R.m[8] * fsum + dragw[2] - P.g_world * mtot;
+    float wb[3], vb[3];
+    mtv(R, E.w, wb);
+    mtv(R, E.v, vb);
+    const float wn = norm3(wb), vn = norm3(vb);
+    float Ic[3];
+    Ic[0] = E.J[0] + 4.0f * Ip + 4.0f * mp * (L * L + Lz * Lz);
+    Ic[1] = E.J[1] + 4.0f * Ip + 4.0f * mp * (L * L + Lz * Lz);
+    Ic[2] = E.J[2] + 4.0f * Ip + 4.0f * mp * (L * L + L * L);
+    const float kq = P.prop_speed_gain;
+    const float sp_old = first_after_reset ? 0.0f : kq * (-xprev[0] + xprev[1] - xprev[2] + xprev[3]);
+    const float sp_new = kq * (-E.x[0] + E.x[1] - E.x[2] + E.x[3]);
+    const float h_old = Ip * sp_old;
+    const float Iw[3] = {Ic[0] * wb[0], Ic[1] * wb[1], Ic[2] * wb[2] + h_old};
+    const float gyro[3] = {wb[1] * Iw[2] - wb[2] * Iw[1], wb[2] * Iw[0] - wb[0] * Iw[2], wb[0] * Iw[1] - wb[1] * Iw[0]};
+    const float dampa = P.ang_damping * (1.0f + wn);
+    const float tdamp[3] = {E.J[0] * wb[0] * dampa, E.J[1] * wb[1] * dampa, E.J[2] * wb[2] * dampa};
+    float pd[3] = {0.0f, 0.0f, 0.0f};
+    {
+        const float ax[4] = {-1.0f, 1.0f, -1.0f, 1.0f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float qd = first_after_reset ? 0.0f : kq * xprev[j];
+            const float wp[3] = {wb[0], wb[1], wb[2] + ax[j] * qd};
+            const float k = Ip * P.ang_damping * (1.0f + norm3(wp));
+            pd[0] += k * wp[0]; pd[1] += k * wp[1]; pd[2] += k * wp[2];
+        }
+    }
+    const float dt = E.dt;
+    float wdot_b[3];
+    wdot_b[0] = (tb[0] - gyro[0] - tdamp[0] - pd[0]) / Ic[0];
+    wdot_b[1] = (tb[1] - gyro[1] - tdamp[1] - pd[1]) / Ic[1];
+    wdot_b[2] = (tb[2] - gyro[2] - tdamp[2] - pd[2] - Ip * (sp_new - sp_old) / dt) / Ic[2];
+    const float dampl = P.lin_damping * (1.0f + vn) * E.m / mtot;
+    float vdot_w[3], wdot_w[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) vdot_w[k] = Fw[k] / mtot - dampl * E.v[k];
+    mv(R, wdot_b, wdot_w);
+    const float vmax = P.vmax;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        E.w[k] = clampf(E.w[k] + wdot_w[k] * dt, -vmax, vmax);
+        E.v[k] = clampf(E.v[k] + vdot_w[k] * dt, -vmax, vmax);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.p[k] += dt * E.v[k];
+    {
+        float ang = norm3(E.w);
+        if (ang * dt > 0.7853981633974483f) ang = 0.7853981633974483f / dt;
+        float s;
+        if (ang < 0.001f) s = 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang;
+        else s = sinf(0.5f * ang * dt) / ang;
+        const float axs[3] = {E.w[0] * s, E.w[1] * s, E.w[2] * s};
+        const float cw = cosf(0.5f * ang * dt);
+        const float qx = E.q[0], qy = E.q[1], qz = E.q[2], qw = E.q[3];
+        const float nx = cw * qx + axs[0] * qw + axs[1] * qz - axs[2] * qy;
+        const float ny = cw * qy + axs[1] * qw + axs[2] * qx - axs[0] * qz;
+        const float nz = cw * qz + axs[2] * qw + axs[0] * qy - axs[1] * qx;
+        const float nw = cw * qw - axs[0] * qx - axs[1] * qy - axs[2] * qz;
+        const float len = sqrtf(nx * nx + ny * ny + nz * nz + nw * nw);
+        E.q[0] = nx / len; E.q[1] = ny / len; E.q[2] = nz / len; E.q[3] = nw / len;
+    }
+    // update_information
+    euler_from_quat(E.q, E.rpy);
+    const M3 Rn = rotmat(E.q);
+    mtv(Rn, E.w, E.wb);
+}
+
+__device__ __forceinline__ void simple_substep(const KParams& P, Env& E, const float a[4], const float on[4]) {
+    float f[4], tz;
+    apply_action(P, E, a, on, f, tz);
+    const M3 R = rotmat(E.q);
+    const float fsum = f[0] + f[1] + f[2] + f[3];
+    const float Fw[3] = {R.m[2] * fsum - 0.0f * E.m, R.m[5] * fsum - 0.0f * E.m, R.m[8] * fsum - P.g_world * E.m};
+    const float tx = (-f[0] - f[1] + f[2] + f[3]) * P.arm / sqrtf(2.0f);
+    const float ty = (-f[0] + f[1] + f[2] - f[3]) * P.arm / sqrtf(2.0f);
+    float* w = E.wb;
+    const float Jw[3] = {E.J[0] * w[0], E.J[1] * w[1], E.J[2] * w[2]};
+    const float cr[3] = {w[1] * Jw[2] - w[2] * Jw[1], w[2] * Jw[0] - w[0] * Jw[2], w[0] * Jw[1] - w[1] * Jw[0]};
+    const float t[3] = {tx - cr[0], ty - cr[1], tz - cr[2]};
+    const float wdd[3] = {(1.0f / E.J[0]) * t[0], (1.0f / E.J[1]) * t[1], (1.0f / E.J[2]) * t[2]};
+    const float acc[3] = {Fw[0] / E.m, Fw[1] / E.m, Fw[2] / E.m};
+    const float dt = E.dt;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.v[k] += dt * acc[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.wb[k] += dt * wdd[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.p[k] += dt * E.v[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.rpy[k] += dt * E.wb[k];
+    quat_from_euler(E.rpy, E.q);
+    if (E.p[2] < 0.0f) E.p[2] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.w[k] = E.wb[k];   // simple mode stores body rates in F_OMEGA
+}
+
+// ------------------------------------------------------------------------------------
+// observation / history / reward
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void omega_noise(const KParams& P, Env& E, const float* n, float om[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.bias[k] = P.pgd * E.bias[k] + P.sbgd * n[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) om[k] = E.wb[k] + E.bias[k] + P.gyro_rw * n[3 + k] + P.gyro_ton * n[6 + k];
+}
+
+template <bool NOISE>
+__device__ __forceinline__ void compute_observation(const KParams& P, Env& E, const Rng& g, uint32_t base,
+                                                    int iteration, float* obs) {
+    if (!NOISE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) obs[k] = E.p[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) obs[3 + k] = E.q[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) obs[7 + k] = E.v[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) obs[10 + k] = E.wb[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) obs[13 + k] = E.la[k];
+        return;
+    }
+    float om[3];
+    if (iteration % P.obs_rate == 0) {
+        float n[18];
+        normals<18>(g, base, n);
+        const U4 ua = g.block(base + 4), ub = g.block(base + 5);
+        const uint32_t up[3] = {ua.z, ua.w, ub.x}, ur[3] = {ub.y, ub.z, ub.w};
+        float pos[3], vel[3], rot[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float uo = -P.pos_unif + (P.pos_unif - -P.pos_unif) * u01(up[k]);
+            pos[k] = E.p[k] + (P.pos_std * n[k] + uo);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vel[k] = E.v[k] + P.vel_std * n[3 + k] + 0.0f;
+        omega_noise(P, E, n + 6, om);
+        const float lo[3] = {-3.141592653589793f, -1.5707963267948966f, -3.141592653589793f};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float uo = -P.rot_unif + (P.rot_unif - -P.rot_unif) * u01(ur[k]);
+            const float th = P.rot_std * n[15 + k] + uo;
+            rot[k] = clampf(E.rpy[k] + th, lo[k], -lo[k]);
+        }
+        float qn[4];
+        quat_from_euler(rot, qn);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.held[k] = pos[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.held[3 + k] = qn[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.held[7 + k] = vel[k];
+    } else {
+        float n[9];
+        normals<9>(g, base, n);
+        omega_noise(P, E, n, om);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.lpf[k] = (1.0f - P.lpf_ratio) * E.lpf[k] + P.lpf_gain * P.lpf_ratio * om[k];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) obs[k] = E.held[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) obs[10 + k] = E.lpf[k];
+}
+
+__device__ __forceinline__ bool compute_done(const KParams& P, const Env& E) {
+    const bool rp = fabsf(E.rpy[0]) > P.done_rp || fabsf(E.rpy[1]) > P.done_rp;
+    bool rt = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rt |= (180.0f * fabsf(E.wb[k]) / 3.141592653589793f) > P.done_rate_deg;
+    return rp || rt || (E.p[2] < P.done_zmin);
+}
+
+__device__ __forceinline__ float compute_reward(const KParams& P, const Env& E, const float a[4], bool done) {
+    float na[4], ad[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { na[k] = 0.5f * (clampf(a[k], -1.0f, 1.0f) + 1.0f); ad[k] = a[k] - E.la[k]; }
+    const float nna = sqrtf(na[0] * na[0] + na[1] * na[1] + na[2] * na[2] + na[3] * na[3]);
+    const float nad = sqrtf(ad[0] * ad[0] + ad[1] * ad[1] + ad[2] * ad[2] + ad[3] * ad[3]);
+    float dr[3], dw[3], dp[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        dr[k] = E.rpy[k] - P.target_rpy[k];
+        dw[k] = E.wb[k] - P.target_rate[k];
+        dp[k] = E.p[k] - P.target_pos[k];
+    }
+    float pen = 0.0f;
+    pen += P.pen_angle * norm3(dr);
+    pen += P.pen_arp * nad;
+    pen += P.pen_spin * norm3(dw);
+    pen += P.pen_vel * norm3(E.v);
+    pen += P.pen_action * nna;
+    pen += done ? P.pen_term : 0.0f;
+    const float zd = P.pen_z * fabsf(E.p[2] - P.target_pos[2]);
+    const float dist = P.pen_dist * norm3(dp);
+    return -pen - zd - dist;
+}
+
+__device__ __forceinline__ float compute_cost(const KParams& P, const Env& E) {
+    float c = 0.0f;
+    if (fabsf(E.p[0]) > P.cost_xy || fabsf(E.p[1]) > P.cost_xy || E.p[2] > P.cost_z) c = 1.0f;
+    if (fabsf(E.rpy[0]) > P.cost_rp || fabsf(E.rpy[1]) > P.cost_rp) c = 1.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) if (fabsf(E.wb[k]) > P.cost_vel) c = 1.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) if (fabsf(E.la[k]) > P.cost_rate) c = 1.0f;
+    return c;
+}
+
+__device__ __forceinline__ void abuf_last(const KParams& P, const Env& E, float o[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float v = opaque(E.abuf[0][j]);
+#pragma unroll
+        for (int r = 1; r < 4; ++r) v = (P.buf_size - 1) == r ? opaque(E.abuf[r][j]) : v;
+        o[j] = v;
+    }
+}
+
+// compute_history: writes out[obs_dim] = [obs_prev, A0, obs_next, A1]
+template <bool NOISE>
+__device__ __forceinline__ void compute_history(const KParams& P, Env& E, const float* on, float* out) {
+    constexpr int OL = NOISE ? 13 : 17;
+    float last[4];
+    abuf_last(P, E, last);
+    int o = 0;
+#pragma unroll
+    for (int k = 0; k < OL; ++k) out[o++] = E.obs_prev[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[o++] = E.halias0 ? last[k] : E.hact[0][k];
+#pragma unroll
+    for (int k = 0; k < OL; ++k) out[o++] = on[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[o++] = E.halias1 ? last[k] : E.hact[1][k];
+#pragma unroll
+    for (int k = 0; k < OL; ++k) E.obs_prev[k] = on[k];
+    E.halias0 = E.halias1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.hact[0][k] = E.hact[1][k];
+    E.halias1 = E.la_view;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.hact[1][k] = E.la[k];
+}
+
+__device__ __forceinline__ int boltzmann_index(const KParams& P, float u) {
+    int i = 0;
+    for (int k = 0; k < P.num_levels - 1; ++k) i += ((double)u < P.tab->level_cdf[k]) ? 0 : 1;
+    // cdf is non-decreasing: count of entries <= u == searchsorted(side='right')
+    return i;
+}
+
+// ------------------------------------------------------------------------------------
+// reset (base.py:420-464 + task_specific_reset + apply_domain_randomization)
+// ------------------------------------------------------------------------------------
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void reset_env(const KParams& P, Env& E, uint32_t gid, float* out) {
+    Rng g{P.key0, P.key1, E.rng, gid, TAG_RESET};
+    const U4 b0 = g.block(0), b1 = g.block(1), b2 = g.block(2), b3 = g.block(3);
+    const uint32_t u[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
+                            b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
+    const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
+    E.ep_step = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) E.x[j] = 0.0f;
+    E.aidx = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) E.abuf[r][j] = 0.0f;
+    float pos[3] = {P.init_xyz[0], P.init_xyz[1], P.init_xyz[2]};
+    float quat[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    float vel[3] = {0.0f, 0.0f, 0.0f}, rate[3] = {0.0f, 0.0f, 0.0f};
+    if (P.reset_dist) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pos[k] += -P.pos_lim + (P.pos_lim - -P.pos_lim) * u01(u[k]);
+        float rpy[3];
+        rpy[0] = -P.angle_lim + (P.angle_lim - -P.angle_lim) * u01(u[4]);
+        rpy[1] = -P.angle_lim + (P.angle_lim - -P.angle_lim) * u01(u[5]);
+        rpy[2] = -P.yaw_lim + (P.yaw_lim - -P.yaw_lim) * u01(u[3]);
+        quat_from_euler(rpy, quat);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vel[k] = vel[k] + (-P.vel_lim + (P.vel_lim - -P.vel_lim) * u01(u[8 + k]));
+        rate[0] = rate[0] + (-P.rate_lim + (P.rate_lim - -P.rate_lim) * u01(u[11]));
+        rate[1] = rate[1] + (-P.rate_lim + (P.rate_lim - -P.rate_lim) * u01(u[12]));
+        rate[2] = -P.yaw_rate_lim + (P.yaw_rate_lim - -P.yaw_rate_lim) * u01(u[7]);
+        float nx[4];
+        normals<4>(g, 4, nx);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) E.x[j] = P.hover_x + P.motor_std * nx[j];
+        float nb[16];
+        normals<16>(g, 5, nb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                E.abuf[r][j] = r < P.buf_size ? clampf(P.hover_action + P.action_std * nb[4 * r + j], -1.0f, 1.0f) : 0.0f;
+    }
+    abuf_last(P, E, E.la);
+    E.la_view = 1;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { E.p[k] = pos[k]; E.v[k] = vel[k]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.q[k] = quat[k];
+    const M3 R0 = rotmat(quat);
+    float ww[3];
+    mtv(R0, rate, ww);
+    // domain randomization
+    E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
+    E.k0 = P.ft0; E.k1 = P.ft1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { E.A[j] = P.A; E.B[j] = P.B; E.K[j] = P.K; }
+    if (DR) {
+        const U4 d0 = g.block(9), d1 = g.block(10), d2 = g.block(11), d3 = g.block(12);
+        const uint32_t d[16] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w,
+                                d2.x, d2.y, d2.z, d2.w, d3.x, d3.y, d3.z, d3.w};
+#define DRAW(b, ui) (P.dr_lo[b] + (P.dr_hi[b] - P.dr_lo[b]) * u01(d[ui]))
+        E.dt = DRAW(0, 0); E.m = DRAW(1, 1);
+        E.J[0] = DRAW(2, 2); E.J[1] = DRAW(3, 3); E.J[2] = DRAW(4, 4);
+        E.k0 = DRAW(5, 5); E.k1 = DRAW(6, 6);
+        if (P.use_motor_dyn) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float mtc = DRAW(7, 7 + j);
+                const float t2w = DRAW(8, 11 + j);
+                const float T = mtc < E.dt ? E.dt : mtc;
+                E.A[j] = 1.0f - E.dt / T;
+                E.B[j] = E.dt / T;
+                E.K[j] = 0.028f * P.g_agent * t2w / 4.0f;
+            }
+        }
+#undef DRAW
+    }
+    {
+        const U4 w = g.block(13);
+        if (P.dstb_mode == DSTB_CONST_T) {
+            const uint32_t wu[3] = {w.x, w.y, w.z};
+#pragma unroll
+            for (int k = 0; k < 3; ++k) E.dstb[k] = (-1.0f + 2.0f * u01(wu[k])) * P.umax[k] * E.level;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) E.dstb[k] = 0.0f;
+        }
+        E.gust_left = 0;
+    }
+    if (NOISE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.lpf[k] = stale[k];
+    }
+    if (PHYS == PHYS_BULLET_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.w[k] = ww[k];
+        euler_from_quat(E.q, E.rpy);
+        mtv(R0, E.w, E.wb);      // R(q) of the reset quaternion
+    } else {
+        euler_from_quat(E.q, E.rpy);
+        mtv(R0, ww, E.wb);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.w[k] = E.wb[k];
+    }
+    float o0[17], o1[17];
+    compute_observation<NOISE>(P, E, g, 32, 0, o0);
+    constexpr int OL = NOISE ? 13 : 17;
+#pragma unroll
+    for (int k = 0; k < OL; ++k) E.obs_prev[k] = o0[k];
+    E.halias0 = E.halias1 = 1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.hact[s][k] = E.la[k];
+    compute_observation<NOISE>(P, E, g, 40, 0, o1);
+    compute_history<NOISE>(P, E, o1, out);
+    if (P.level_mode == LEVEL_BOLTZMANN_T) {
+        E.level_idx = boltzmann_index(P, u01(u[13]));
+        E.level = P.tab->level_values[E.level_idx];
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------
+template <bool NOISE>
+__device__ __forceinline__ void write_obs(float* __restrict__ dst, uint32_t i, const float* o) {
+    constexpr int OD = NOISE ? 34 : 42;
+    float2* d2 = reinterpret_cast<float2*>(dst + (size_t)i * OD);
+#pragma unroll
+    for (int k = 0; k < OD / 2; ++k) d2[k] = make_float2(o[2 * k], o[2 * k + 1]);
+}
+
+template <bool NOISE, bool DR, int PHYS>
+__global__ void __launch_bounds__(256) step_kernel(KParams P, StepIO io) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.N) return;
+    constexpr int OL = NOISE ? 13 : 17;
+    constexpr int OD = 2 * (OL + 4);
+    Env E;
+    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E);
+    const uint32_t gid = P.gid_off + i;
+    const float4 a4 = reinterpret_cast<const float4*>(io.act)[i];
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+    const Rng g{P.key0, P.key1, E.rng, gid, TAG_STEP};
+    if (PHYS == PHYS_BULLET_T) {
+        euler_from_quat(E.q, E.rpy);
+        const M3 R = rotmat(E.q);
+        mtv(R, E.w, E.wb);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.wb[k] = E.w[k];
+    }
+    const float level_used = E.level;
+    // disturbance (once per env-step, held for all sub-steps)
+    float d[3] = {0.0f, 0.0f, 0.0f};
+    switch (P.dstb_mode) {
+    case DSTB_EXTERNAL_T:
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d[k] = io.dstb[(size_t)i * 3 + k];
+        break;
+    case DSTB_UNIFORM_T: {
+        const U4 u = g.block(0);
+        const uint32_t uu[3] = {u.x, u.y, u.z};
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            d[k] = (float)(-P.uni_hi[k] + (P.uni_hi[k] - -P.uni_hi[k]) * (double)u01(uu[k]));
+        break;
+    }
+    case DSTB_CONST_T:
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d[k] = E.dstb[k];
+        break;
+    case DSTB_GUST_T: {
+        const U4 u = g.block(0);
+        if (E.gust_left == 0 && u01(u.x) < P.gust_p) {
+            E.gust_left = P.gust_dur;
+            const float mag = P.gust_max * u01(u.y);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) E.dstb[k] = ((u.z >> k) & 1u ? -1.0f : 1.0f) * mag * P.umax[k];
+        }
+        if (E.gust_left > 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) d[k] = E.dstb[k];
+            E.gust_left -= 1;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) E.dstb[k] = 0.0f;
+        }
+        break;
+    }
+    case DSTB_HJ_T: {
+        const int t = P.level_mode == LEVEL_FIXED_T ? P.tab->table_of_level[0] : P.tab->table_of_level[E.level_idx & 31];
+        if (t >= 0 && P.V != nullptr) {
+            float e[3];
+            quat2euler(E.q, e);
+            const double st[6] = {(double)e[0], (double)e[1], (double)e[2], (double)E.wb[0], (double)E.wb[1], (double)E.wb[2]};
+            const unsigned bits = hj_signs(P, P.V + (size_t)t * HJ_TABLE, st);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float dm = (float)((double)E.level * (double)P.umax_d[k]);
+                d[k] = (bits >> k) & 1u ? -dm : dm;
+            }
+        }
+        break;
+    }
+    default: break;
+    }
+    for (int s = 0; s < P.agg; ++s) {
+        float on[4];
+        normals<4>(g, 1 + s, on);
+        if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0);
+        else simple_substep(P, E, a, on);
+        float dummy[17];
+        compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy);
+    }
+    float onx[17], o[OD];
+    compute_observation<NOISE>(P, E, g, 8 + 8 * P.agg, (E.ep_step + 1) * P.agg, onx);
+    compute_history<NOISE>(P, E, onx, o);
+    const bool term = compute_done(P, E);
+    const float r = compute_reward(P, E, a, term);
+    const float cost = compute_cost(P, E);
+    E.ep_step += 1;
+    const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
+    const bool done = term || trunc;
+    io.rew[i] = r;
+    io.done[i] = (uint8_t)done;
+    if (io.trunc) io.trunc[i] = (uint8_t)trunc;
+    if (io.cost) io.cost[i] = cost;
+    if (io.level) io.level[i] = level_used;
+    bool params_dirty = false;
+    if (done && P.auto_reset) {
+        if (io.final_obs) write_obs<NOISE>(io.final_obs, i, o);
+        reset_env<NOISE, DR, PHYS>(P, E, gid, o);
+        params_dirty = true;
+    }
+    E.rng += 1;
+    write_obs<NOISE>(io.obs, i, o);
+    store_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, params_dirty);
+}
+
+template <bool NOISE, bool DR, int PHYS>
+__global__ void __launch_bounds__(256) reset_kernel(KParams P, float* __restrict__ sf, int32_t* __restrict__ si,
+                                                    const uint8_t* __restrict__ mask, float* __restrict__ obs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.N) return;
+    if (mask && !mask[i]) return;
+    constexpr int OD = NOISE ? 34 : 42;
+    Env E;
+    load_env<NOISE, DR, PHYS>(P, sf, si, i, E);
+    if (PHYS == PHYS_BULLET_T) {
+        const M3 R = rotmat(E.q);
+        mtv(R, E.w, E.wb);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.wb[k] = E.w[k];
+    }
+    float o[OD];
+    reset_env<NOISE, DR, PHYS>(P, E, P.gid_off + i, o);
+    E.rng += 1;
+    if (obs) write_obs<NOISE>(obs, i, o);
+    store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
+}
+
+// initial (pre-reset) state: AgentBase defaults, nominal params
+__global__ void init_kernel(KParams P, float* __restrict__ sf, int32_t* __restrict__ si) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.N) return;
+    const uint32_t N = P.N;
+    for (int f = 0; f < NF; ++f) sf[(size_t)f * N + i] = 0.0f;
+    sf[(size_t)(F_POS + 2) * N + i] = 1.0f;
+    sf[(size_t)(F_QUAT + 3) * N + i] = 1.0f;
+    sf[(size_t)(F_PARAM + 0) * N + i] = P.time_step;
+    sf[(size_t)(F_PARAM + 1) * N + i] = P.mass;
+    sf[(size_t)(F_PARAM + 2) * N + i] = P.ixx;
+    sf[(size_t)(F_PARAM + 3) * N + i] = P.iyy;
+    sf[(size_t)(F_PARAM + 4) * N + i] = P.izz;
+    sf[(size_t)(F_PARAM + 5) * N + i] = P.ft0;
+    sf[(size_t)(F_PARAM + 6) * N + i] = P.ft1;
+    for (int k = 0; k < 4; ++k) {
+        sf[(size_t)(F_PARAM + 7 + k) * N + i] = P.A;
+        sf[(size_t)(F_PARAM + 11 + k) * N + i] = P.B;
+        sf[(size_t)(F_PARAM + 15 + k) * N + i] = P.K;
+    }
+    sf[(size_t)F_LEVEL * N + i] = P.level_fixed;
+    for (int f = 0; f < NI; ++f) si[(size_t)f * N + i] = 0;
+    if (P.level_mode == LEVEL_BOLTZMANN_T) {
+        // construction-time Boltzmann() draw (hover_free.py:488), rng counter 0xFFFFFFFF
+        const Rng g{P.key0, P.key1, 0xFFFFFFFFu, P.gid_off + i, TAG_RESET};
+        const U4 u = g.block(0);
+        const int li = boltzmann_index(P, u01(u.x));
+        si[(size_t)I_LEVEL * N + i] = li;
+        sf[(size_t)F_LEVEL * N + i] = P.tab->level_values[li];
+    }
+}
+
+__global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* __restrict__ states, uint32_t n,
+                          float level, float* __restrict__ dstb, float* __restrict__ uopt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double st[6];
+#pragma unroll
+    for (int d = 0; d < 6; ++d) st[d] = (double)states[(size_t)i * 6 + d];
+    const unsigned bits = hj_signs(P, V, st);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double um = P.umax_d[k];
+        const double dm = (double)level * um;
+        dstb[(size_t)i * 3 + k] = (float)((bits >> k) & 1u ? -dm : dm);
+        if (uopt) uopt[(size_t)i * 3 + k] = (float)((bits >> k) & 1u ? -um : um);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// host-side launch table
+// ------------------------------------------------------------------------------------
+template <bool NOISE, bool DR, int PHYS>
+static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
+    const dim3 grid((P.N + 255) / 256), block(256);
+    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS>), grid, block, 0, s, P, io);
+    return hipGetLastError();
+}
+template <bool NOISE, bool DR, int PHYS>
+static hipError_t launch_reset_t(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s) {
+    const dim3 grid((P.N + 255) / 256), block(256);
+    hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS>), grid, block, 0, s, P, sf, si, mask, obs);
+    return hipGetLastError();
+}
+
+#define CF2_DISPATCH(FN, ...)                                                                          \
+    do {                                                                                               \
+        const int key = (P.noise ? 4 : 0) | (P.dr ? 2 : 0) | (P.phys == PHYS_SIMPLE_T ? 1 : 0);           \
+        switch (key) {                                                                                 \
+        case 0: return FN<false, false, PHYS_BULLET_T>(__VA_ARGS__);                                   \
+        case 1: return FN<false, false, PHYS_SIMPLE_T>(__VA_ARGS__);                                   \
+        case 2: return FN<false, true, PHYS_BULLET_T>(__VA_ARGS__);                                    \
+        case 3: return FN<false, true, PHYS_SIMPLE_T>(__VA_ARGS__);                                    \
+        case 4: return FN<true, false, PHYS_BULLET_T>(__VA_ARGS__);                                    \
+        case 5: return FN<true, false, PHYS_SIMPLE_T>(__VA_ARGS__);                                    \
+        case 6: return FN<true, true, PHYS_BULLET_T>(__VA_ARGS__);                                     \
+        default: return FN<true, true, PHYS_SIMPLE_T>(__VA_ARGS__);                                    \
+        }                                                                                              \
+    } while (0)
+
+hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
+hipError_t launch_reset(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s) {
+    CF2_DISPATCH(launch_reset_t, P, sf, si, mask, obs, s);
+}
+hipError_t launch_init(const KParams& P, float* sf, int32_t* si, hipStream_t s) {
+    const dim3 grid((P.N + 255) / 256), block(256);
+    hipLaunchKernelGGL(init_kernel, grid, block, 0, s, P, sf, si);
+    return hipGetLastError();
+}
+hipError_t launch_hj(const KParams& P, const float* V, const float* states, uint32_t n, float level, float* dstb,
+                     float* uopt, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const dim3 grid((n + 255) / 256), block(256);
+    hipLaunchKernelGGL(hj_kernel, grid, block, 0, s, P, V, states, n, level, dstb, uopt);
+    return hipGetLastError();
+}
+
+}  // namespace cf2

@@ -1,0 +1,211 @@
+/*
+ * cf2sim.h -- C ABI of the MI355X-native batched CrazyFlie hover environment.
+ *
+ * One context owns N independent hover environments whose state lives in HBM as
+ * structure-of-arrays.  Every entry point is asynchronous on the caller's HIP stream;
+ * every I/O buffer is a caller-owned DEVICE pointer.  Return value: 0 on success or a
+ * negative cf2_status; the library never aborts the process.
+ *
+ * Reference interfaces replaced (paths relative to the reference repository root,
+ * phoenix_drone_simulation/ omitted):
+ *   cf2_reset  <- DroneBaseEnv.reset                         envs/base.py:420-464
+ *                 + task_specific_reset                       envs/hover_free.py:237-289, envs/hover.py:204-256
+ *                 + apply_domain_randomization                envs/base.py:241-298
+ *                 + RandomHJ level redraw (Boltzmann)         envs/hover_free.py:492-536, envs/utils.py:27-39
+ *   cf2_step   <- DroneBaseEnv.step and its adversary overrides
+ *                                                             envs/base.py:466-507, envs/hover_free.py:391-444,
+ *                                                             :778-835, :950-1007; envs/hover.py:649-702, ...
+ *                 (one call = aggregate_phy_steps x PybulletPhysicsWithAdversary.step_forward
+ *                  envs/physics.py:213-250 / PyBulletPhysics.step_forward :91-124 /
+ *                  SimplePhysics.step_forward :130-200, then compute_history/reward/info/done,
+ *                  then gym TimeLimit(max_episode_steps) and auto-reset)
+ *   cf2_hj_disturbance <- distur_gener                        adversarial_generation/FasTrack_data/distur_gener.py:19-183
+ *                         (+ Grid.get_index                   adversarial_generation/odp/Grid/GridProcessing.py:52-71)
+ *   cf2_get_state / cf2_set_state: SoA snapshot (the reference never checkpoints env state;
+ *                 used for parity tests and checkpoint/resume of rollouts).
+ */
+#ifndef CF2SIM_H
+#define CF2SIM_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CF2SIM_ABI_VERSION 1
+
+typedef enum cf2_status {
+    CF2_OK = 0,
+    CF2_ERR_INVALID_ARG = -1,   /* null pointer, bad enum, inconsistent sizes */
+    CF2_ERR_OUT_OF_MEMORY = -2, /* hipMalloc failed */
+    CF2_ERR_HIP = -3,           /* a HIP runtime call failed (see cf2_last_hip_error) */
+    CF2_ERR_UNSUPPORTED = -4,   /* configuration outside what the kernels implement */
+    CF2_ERR_NO_TABLE = -5       /* HJ disturbance requested but no value table bound */
+} cf2_status;
+
+/* physics plugin (envs/physics.py) */
+enum { CF2_PHYS_BULLET = 0,   /* PyBulletPhysics / PybulletPhysicsWithAdversary: rigid-body restatement of the
+                                 btMultiBody step (bullet3 3.21) the reference delegates to stepSimulation() */
+       CF2_PHYS_SIMPLE = 1 }; /* SimplePhysics: explicit Euler on rpy (envs/physics.py:130-200) */
+
+/* task (reward / done / reset flavour) */
+enum { CF2_TASK_HOVER = 0,       /* DroneHoverBaseEnv  envs/hover.py:16-256 */
+       CF2_TASK_HOVER_FREE = 1 };/* DroneHoverFreeEnv  envs/hover_free.py:17-289 */
+
+/* disturbance source (the dstb argument of PybulletPhysicsWithAdversary.step_forward) */
+enum { CF2_DSTB_NONE = 0,      /* dstb = (0,0,0)                       hover_free.py:814 */
+       CF2_DSTB_EXTERNAL = 1,  /* caller passes dstb[N,3] each step     (test / custom adversary hook) */
+       CF2_DSTB_UNIFORM = 2,   /* dstb_space.sample() each env-step    hover_free.py:986, hover.py:1244 */
+       CF2_DSTB_CONST = 3,     /* per-episode constant torque ("constant wind", BASELINE config 2) */
+       CF2_DSTB_GUST = 4,      /* Philox-driven torque bursts (BASELINE config 4, build-defined) */
+       CF2_DSTB_HJ = 5 };      /* HJ bang-bang disturbance from a 15^6 value table  distur_gener.py:19-183 */
+
+/* how the per-episode disturbance level is chosen (HJ / const / gust magnitudes) */
+enum { CF2_LEVEL_FIXED = 0,      /* env.disturbance_level constant, e.g. 1.5 (hover_free.py:319) */
+       CF2_LEVEL_BOLTZMANN = 1 };/* Boltzmann() redraw at the end of every reset (hover_free.py:536) */
+
+#define CF2_MAX_ENVS_PER_CTX  (1u << 27)
+#define CF2_HJ_PTS 15               /* grid points per dimension, distur_gener.py:179 */
+#define CF2_NUM_LEVELS_MAX 32
+
+typedef struct cf2_config {
+    /* ---- sizes / plumbing ---- */
+    uint32_t num_envs;             /* envs owned by this context (this rank's shard)             */
+    uint32_t env_id_offset;        /* global id of env 0 (rank shard offset): RNG keys use global ids */
+    uint64_t seed;                 /* Philox4x32-10 key                                            */
+
+    /* ---- env flavour ---- */
+    int32_t physics;               /* CF2_PHYS_*                                                   */
+    int32_t task;                  /* CF2_TASK_*                                                   */
+    int32_t disturbance;           /* CF2_DSTB_*                                                   */
+    int32_t level_mode;            /* CF2_LEVEL_*                                                  */
+    int32_t aggregate_phy_steps;   /* physics sub-steps per env-step (2)       base.py:35          */
+    int32_t obs_rate;              /* sim_freq // observation_frequency (2)    base.py:106          */
+    int32_t buf_size;              /* latency ring length int(latency//dt) (2) agents.py:180        */
+    int32_t use_latency;           /* agents.py:165                                                */
+    int32_t use_motor_dynamics;    /* agents.py:196                                                */
+    int32_t max_episode_steps;     /* gym TimeLimit (500)  __init__.py; 0 = none                    */
+    int32_t auto_reset;            /* reset envs on done/truncation inside cf2_step                 */
+    int32_t enable_reset_distribution; /* base.py:38                                                */
+    int32_t observation_noise_on;  /* observation_noise > 0                    hover_free.py:170    */
+    int32_t domain_randomization_on; /* domain_randomization > 0               base.py:261          */
+    double  domain_randomization;  /* DR factor (0.10)                                              */
+    double  motor_thrust_noise;    /* OU sigma = 0.2 * this                    agents.py:206        */
+
+    /* ---- time ---- */
+    double sim_freq;               /* Hz (200 bullet, 100 simple)                                  */
+    double time_step;              /* 1/sim_freq (nominal; DR redraws per env)                      */
+
+    /* ---- robot constants (URDF + agents.py:142-206) ---- */
+    double mass, arm, thrust2weight, ixx, iyy, izz;
+    double drag_xy, drag_z;
+    double gravity_agent;          /* 9.81  agents.py:145 (K formula)          */
+    double gravity_world;          /* 9.81  bc.setGravity base.py:192 / SimplePhysics G physics.py:16 */
+    double motor_time_constant;    /* 0.080 */
+    double ft0, ft1;               /* FORCE_TORQUE_FACTOR_0/1  agents.py:142-143 */
+    double K, A, B;                /* nominal MAX_THRUST, 1 - Ts/T, Ts/T */
+    double hover_x, hover_action;  /* sqrt(1/t2w), 2/t2w - 1 */
+    double prop_mass, prop_inertia;/* cf21x_bullet.urdf m1..m4_link: 1e-9 kg, 1e-9 kg m^2 */
+    double prop_xy, prop_z;        /* prop joint origins (+-0.028, +-0.028, 0.0108) */
+    double prop_speed_gain;        /* setJointMotorControl2 targetVelocity = x*100  agents.py:327 */
+    double lin_damping, ang_damping;   /* btMultiBody default 0.04 / 0.04 */
+    double max_coord_velocity;     /* btMultiBody m_maxCoordinateVelocity 100 */
+
+    /* ---- initial state / reset distribution (hover_free.py:237-289) ---- */
+    double init_xyz[3];
+    double reset_pos_lim, reset_angle_lim, reset_yaw_lim, reset_vel_lim, reset_rate_lim, reset_yaw_rate_lim;
+    double action_init_std, motor_init_std;   /* 0.02, 0.02 */
+
+    /* ---- sensor noise (envs/sensors.py:17-134) & gyro LPF (base.py:107) ---- */
+    double pos_norm_std, pos_unif_range, vel_norm_std, vel_unif_range;
+    double rot_norm_std, rot_unif_range;
+    double gyro_noise_density, gyro_random_walk, gyro_bias_corr_time, gyro_turn_on_bias_sigma;
+    double lpf_gain, lpf_ratio;    /* K, T_s/T */
+
+    /* ---- reward / done / cost (hover.py:102-202, hover_free.py:124-235,449-461) ---- */
+    double penalty_action, penalty_angle, penalty_spin, penalty_terminal, penalty_velocity, penalty_z;
+    double penalty_arp;            /* self.ARP */
+    double penalty_dist;           /* 1 for DroneHoverBaseEnv (-dist term), 0 for free */
+    double target_pos[3], target_rpy[3], target_rate[3];
+    double done_rp_limit;          /* rad: deg2rad(60) or deg2rad(75) */
+    double done_rate_limit_deg;    /* 300 or 1000 */
+    double done_z_min;             /* 0.2 */
+    double cost_xy_lim, cost_z_lim, cost_rp_lim, cost_vel_lim, cost_rate_lim;
+
+    /* ---- disturbance ---- */
+    double dstb_level;             /* fixed level (CF2_LEVEL_FIXED) */
+    double dstb_umax[3];           /* 5.3e-3, 5.3e-3, 1.43e-4   distur_gener.py:152 */
+    double dstb_uniform_hi[3];     /* 1e-3, 1e-3, 1e-4          hover_free.py:315 */
+    double gust_onset_prob, gust_max_level;   /* 0.01, 1.5 */
+    int32_t gust_duration;         /* 20 env-steps */
+    int32_t num_levels;            /* Boltzmann support size (21) */
+    double level_values[CF2_NUM_LEVELS_MAX];  /* np.around(energies, 1) */
+    double level_cdf[CF2_NUM_LEVELS_MAX];     /* normalised cumsum(p), numpy choice()  */
+    double hj_grid_min[6];         /* per-dim lower bounds (Grid.min)                */
+    double hj_grid_dx[6];          /* Grid.dx                                       */
+    double hj_grid_points[6][CF2_HJ_PTS]; /* np.linspace node values (Grid.grid_points) */
+} cf2_config;
+
+/* SoA layout descriptor returned by cf2_layout(): state_f[field*num_envs + env],
+ * state_i[field*num_envs + env]. Field meaning is documented in DESIGN.md. */
+typedef struct cf2_layout {
+    uint32_t num_envs;
+    uint32_t num_float_fields;
+    uint32_t num_int_fields;
+    uint32_t obs_dim;              /* 34 with observation noise, 42 without */
+    uint32_t obs_len;              /* 13 or 17 */
+    uint32_t f_pos, f_quat, f_vel, f_omega, f_rpy, f_motor, f_ou, f_abuf, f_bias, f_lpf, f_held,
+             f_obs_prev, f_hist_act, f_param, f_dstb;
+    uint32_t i_ep_step, i_rng, i_flags, i_level, i_gust;
+    uint32_t num_params;           /* per-env DR parameters (19) */
+} cf2_layout;
+
+typedef struct cf2_ctx cf2_ctx;
+
+int  cf2_abi_version(void);
+size_t cf2_config_sizeof(void);     /* lets FFI callers check their struct mirror */
+const char* cf2_status_string(int status);
+int  cf2_last_hip_error(void);
+
+int  cf2_create(const cf2_config* cfg, cf2_ctx** out_ctx);
+int  cf2_destroy(cf2_ctx* ctx);
+int  cf2_layout_get(const cf2_ctx* ctx, cf2_layout* out);
+
+/* Bind HJ value tables: V_dev = [num_tables][15^6] float32 C-order [roll,pitch,yaw,p,q,r]
+ * (the on-disk fastrack_{level}_15x15.npy format).  table_level_index maps Boltzmann level
+ * index -> table row (or -1 = no table, dstb 0).  Caller owns V_dev for the ctx lifetime. */
+int  cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables,
+                        const int32_t* table_of_level /* host, num_levels entries */);
+
+/* Reset envs whose mask byte is non-zero (mask_dev NULL = all), write their obs rows. */
+int  cf2_reset(cf2_ctx* ctx, const uint8_t* mask_dev, float* obs_dev, void* stream);
+
+/* One env-step for all envs.  act_dev [N,4]; dstb_dev [N,3] (only for CF2_DSTB_EXTERNAL, else NULL);
+ * obs_dev [N,obs_dim]; rew_dev [N]; done_dev [N] (terminal OR truncated, gym 4-tuple semantics);
+ * trunc_dev [N] (TimeLimit truncation, may be NULL); cost_dev [N] (may be NULL);
+ * level_dev [N] disturbance level of the finished step (may be NULL);
+ * final_obs_dev [N,obs_dim] pre-reset observation of envs that auto-reset this step (may be NULL). */
+int  cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev,
+              float* obs_dev, float* rew_dev, uint8_t* done_dev, uint8_t* trunc_dev,
+              float* cost_dev, float* level_dev, float* final_obs_dev, void* stream);
+
+/* K consecutive env-steps with actions act_dev[k] = act_dev + k*N*4 (rollout mode); outputs
+ * are those of the last step.  Equivalent to K cf2_step calls; one launch per step. */
+int  cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems,
+                 float* obs_dev, float* rew_dev, uint8_t* done_dev, void* stream);
+
+/* Whole-state snapshot (device buffers sized by cf2_layout). */
+int  cf2_get_state(const cf2_ctx* ctx, float* state_f_dev, int32_t* state_i_dev, void* stream);
+int  cf2_set_state(cf2_ctx* ctx, const float* state_f_dev, const int32_t* state_i_dev, void* stream);
+
+/* Stand-alone batched distur_gener: states_dev [n,6] = [roll,pitch,yaw,p,q,r] (float32),
+ * V_dev one 15^6 table, out dstb_dev [n,3] = opt_d, out uopt_dev [n,3] = opt_u (may be NULL). */
+int  cf2_hj_disturbance(const cf2_config* cfg, const float* V_dev, const float* states_dev,
+                        uint32_t n, float level, float* dstb_dev, float* uopt_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CF2SIM_H */
