@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the batched CrazyFlie hover env-step on MI355X.
+
+Metric (BASELINE.json): env-steps/s for the whole node at 262 144 parallel envs, plus the
+achieved HBM GB/s of the step kernel against the chip's peak.
+
+Workload (BASELINE.json configs[3], the config the metric is quoted on; it fits one GPU):
+DroneHoverBulletFreeEnvWithGust -- the reference's free-hover task (envs/hover_free.py) with
+its default sensor noise, 10 % domain randomisation, motor-thrust noise, 15 ms latency and
+TimeLimit(500) auto-reset, plus Philox-driven torque gusts.  One step = one env-step of every
+env = 2 physics sub-steps at dt = 5 ms.  Actions: uniform(-1, 1) f32 drawn once into a ring of
+device slabs, so every step reads a fresh [N, 4] action tensor from HBM.
+
+Multi-GPU: one process per GPU (torchrun); envs are independent, each rank owns
+--envs-per-gpu envs with its own global id range (no collective in the data path; weak
+scaling).  --gather-obs adds an RCCL all-gather of the observation slab per step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+ENV_ID = "DroneHoverBulletFreeEnvWithGust-v0"
+
+
+def algorithmic_bytes_per_env_step(cfg, outputs=("obs", "rew", "done")) -> int:
+    """Bytes one env-step must move between HBM and the chip (state read + write once, action
+    in, outputs out) for this configuration; per-episode writes (reset, DR params) excluded.
+    Mirrors the SoA fields the step kernel touches (DESIGN.md 'Algorithmic bytes')."""
+    noise, dr = bool(cfg.observation_noise_on), bool(cfg.domain_randomization_on)
+    ol = 13 if noise else 17
+    B = int(cfg.buf_size)
+    held = (cfg.aggregate_phy_steps % cfg.obs_rate) != 0
+    gust_or_const = cfg.disturbance in (3, 4)
+    level = cfg.disturbance in (3, 5) or cfg.level_mode == 1
+    persist_f = 13 + 8 + 4 * B + (6 if noise else 0) + (10 if noise and held else 0) + ol + 8
+    if cfg.physics == 1:
+        persist_f += 3
+    rd_f = persist_f + (19 if dr else 0) + (3 if gust_or_const else 0) + (1 if level else 0)
+    wr_f = persist_f + (3 if cfg.disturbance == 4 else 0)
+    rd_i = 3 + (1 if level else 0) + (1 if cfg.disturbance == 4 else 0)
+    wr_i = 3 + (1 if cfg.disturbance == 4 else 0)
+    b = 4 * (rd_f + wr_f + rd_i + wr_i) + 16
+    if cfg.disturbance == 1:
+        b += 12
+    od = 2 * (ol + 4)
+    per_out = {"obs": 4 * od, "rew": 4, "done": 1, "trunc": 1, "cost": 4, "level": 4}
+    return b + sum(per_out[o] for o in outputs)
+
+
+def cpu_baseline(n_envs=2048, steps=300, seed=0):
+    """Time the CPU restatement (oracle/, scalar C, one core) on a bounded sample of the same
+    workload.  Reported baseline only, not the target."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    from cf2sim.config import build_config
+    cfg = build_config(ENV_ID, n_envs, seed=seed)
+    env = orc.OracleEnv(cfg, precision="f64")
+    env.reset()
+    rng = np.random.default_rng(seed)
+    acts = rng.uniform(-1, 1, size=(8, n_envs, 4)).astype(np.float32)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        env.step(acts[k % 8])
+    dt = time.perf_counter() - t0
+    env.close()
+    return {"value": n_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/cf2_oracle.c fp64, {n_envs} envs x {steps} env-steps of {ENV_ID} "
+                      f"(gust, noise, DR), 1 thread, {dt:.1f} s"}
+
+
+def load_traffic(workload_key: str):
+    """Per-launch HBM bytes of the step kernel from rocprofv3 PMC passes (tools/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", "step_kernel_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == workload_key:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs-per-gpu", type=int, default=262144)
+    ap.add_argument("--env-id", default=ENV_ID)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of obs every step")
+    ap.add_argument("--graph", action="store_true", help="capture the timed steps in a hipGraph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-envs", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=1500)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+
+    n = args.envs_per_gpu
+    env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=rank * n, device=dev)
+    env.reset()
+    ring = 8
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    acts = torch.rand(ring, n, 4, device=dev, generator=g) * 2 - 1
+    gathered = None
+
+    def one_step(k):
+        env.step_raw(acts[k % ring].data_ptr())
+        if args.gather_obs and world > 1:
+            dist.all_gather_into_tensor(gathered, env.obs)
+
+    if args.gather_obs and world > 1:
+        gathered = torch.empty(world * n, env.obs_dim, device=dev)
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize()
+
+    graph = None
+    if args.graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph, stream=s):
+                for k in range(args.steps):
+                    one_step(k)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps between barrier + synchronize ----
+    stream = torch.cuda.current_stream()
+    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev_start.record(stream)
+    if graph is not None:
+        graph.replay()
+    else:
+        for k in range(args.steps):
+            one_step(k)
+    ev_end.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # average step-kernel duration over the timed region, HIP events on the launch stream
+    kern_ms = ev_start.elapsed_time(ev_end) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if args.gather_obs and world > 1:
+        # the timed region also holds the all-gathers: time the step kernel alone here
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for k in range(20):
+            ev[k][0].record(stream)
+            env.step_raw(acts[k % ring].data_ptr())
+            ev[k][1].record(stream)
+        torch.cuda.synchronize()
+        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / 20
+
+    total_env_steps = n * args.steps * world
+    value = total_env_steps / elapsed
+    bytes_per = algorithmic_bytes_per_env_step(env.cfg)
+    achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
+    workload_key = f"{args.env_id}:N={n}"
+    traffic = load_traffic(workload_key)
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_envs, args.cpu_steps)
+        line = {
+            "metric": "env-steps/sec (whole node) at 262k parallel envs; achieved HBM GB/s vs peak",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: uniform(-1,1) actions, Philox-seeded resets/noise/gusts",
+            "config": {"workload": f"{args.env_id} (C4 gust, reference default noise/DR/latency, "
+                                   f"TimeLimit 500 + auto-reset), {n} envs per GPU",
+                       "envs_per_gpu": n, "global_envs": n * world, "aggregate_phy_steps": 2,
+                       "parallelism": f"env-shard x{world}", "gather_obs": bool(args.gather_obs),
+                       "graph": bool(args.graph)},
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "algorithmic_bytes_per_env_step": bytes_per,
+                         "kernel_ms_per_launch": kern_ms},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -78,6 +78,8 @@ static void fill_params(const cf2_config* c, KParams& P) {
     P.dr = c->domain_randomization_on;
     P.phys = c->physics;
     P.held_persistent = (c->aggregate_phy_steps % c->obs_rate) != 0;
+    P.need_level = c->disturbance == CF2_DSTB_HJ || c->disturbance == CF2_DSTB_CONST ||
+                   c->level_mode == CF2_LEVEL_BOLTZMANN;
     P.time_step = (float)c->time_step;
     P.mass = (float)c->mass;
     P.ixx = (float)c->ixx; P.iyy = (float)c->iyy; P.izz = (float)c->izz;

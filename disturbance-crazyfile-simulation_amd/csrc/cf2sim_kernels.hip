@@ -220,7 +220,7 @@ struct Env {
 
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ void load_env(const KParams& P, const float* __restrict__ sf,
-                                         const int32_t* __restrict__ si, uint32_t i, Env& E) {
+                                         const int32_t* __restrict__ si, uint32_t i, Env& E, bool need_level = true) {
     const uint32_t N = P.N;
 #define LD(f) sf[(size_t)(f) * N + i]
 #pragma unroll
@@ -282,13 +282,13 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
 #pragma unroll
         for (int k = 0; k < 3; ++k) E.dstb[k] = 0.0f;
     }
-    E.level = LD(F_LEVEL);
+    E.level = need_level ? LD(F_LEVEL) : P.level_fixed;
 #undef LD
     E.ep_step = si[(size_t)I_EP_STEP * N + i];
     E.rng = (uint32_t)si[(size_t)I_RNG * N + i];
     const int fl = si[(size_t)I_FLAGS * N + i];
     E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
-    E.level_idx = si[(size_t)I_LEVEL * N + i];
+    E.level_idx = need_level ? si[(size_t)I_LEVEL * N + i] : 0;
     E.gust_left = P.dstb_mode == DSTB_GUST_T ? si[(size_t)I_GUST * N + i] : 0;
 }
 
@@ -834,7 +834,7 @@ __global__ void __launch_bounds__(256) step_kernel(KParams P, StepIO io) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     Env E;
-    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E);
+    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, P.need_level || io.level != nullptr);
     const uint32_t gid = P.gid_off + i;
     const float4 a4 = reinterpret_cast<const float4*>(io.act)[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};

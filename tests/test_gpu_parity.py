@@ -1,0 +1,205 @@
+"""Parity of the HIP kernels (through the C ABI) against the CPU restatement (oracle/).
+
+Tolerances (stated per test):
+* vs the fp32 restatement (same operation order, -ffp-contract=off): differences come only
+  from the transcendental library (ocml vs glibc, <= 1-2 ulp) -> 2e-4 abs on observations over
+  120 env-steps with noise, 1e-4 on state;
+* vs the fp64 restatement: fp32 rounding of the whole trajectory -> 5e-3 abs on observations
+  over 120 env-steps (BASELINE.json's "1e-4 rel" is met on the noise-free state, test below);
+* integer/boolean outputs (done, truncation, episode counters, RNG counters): exact, except
+  envs whose trajectory crosses a termination threshold within fp32 rounding.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from cf2sim.config import build_config
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", {}),
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(observation_noise=0, domain_randomization=-1,
+                                                         motor_thrust_noise=0)),
+    ("DroneHoverSimpleEnv-v0", {}),
+    ("DroneHoverBulletEnvWithRandomAdversary-v0", {}),
+    ("DroneHoverBulletFreeEnvWithGust-v0", {}),
+    ("DroneHoverBulletFreeEnvWithConstWind-v0", {}),
+    ("DroneHoverBulletEnv-v0", dict(observation_noise=0)),
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(aggregate_phy_steps=1)),   # held obs persists
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(latency=0.02)),           # ring of 4
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(latency=0.0)),            # no latency
+]
+
+
+def _actions(rng, n):
+    return (rng.uniform(-1, 1, size=(n, 4)) * 0.25 + 0.1111).astype(np.float32)
+
+
+def _run_pair(env_id, kw, n, T, prec, seed=3, stop_at_done=False):
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env = BatchedCrazyflieEnv(env_id, n, seed=seed, want_final_obs=True, **kw)
+    ref = O.OracleEnv(build_config(env_id, n, seed=seed, **kw), precision=prec)
+    go = env.reset().cpu().numpy()
+    ro = ref.reset()
+    errs = [np.abs(go - ro).max()]
+    rng = np.random.default_rng(seed + 1)
+    done_mismatch = 0
+    rew_err = 0.0
+    for t in range(T):
+        a = _actions(rng, n)
+        g_o, g_r, g_d, g_i = env.step(torch.from_numpy(a).cuda())
+        r_o, r_r, r_d, r_i = ref.step(a, want_final=True)
+        g_o, g_d = g_o.cpu().numpy(), g_d.cpu().numpy().astype(bool)
+        done_mismatch += int((g_d != r_d).sum())
+        errs.append(np.abs(g_o - r_o).max())
+        rew_err = max(rew_err, float(np.abs(g_r.cpu().numpy() - r_r).max()))
+        fin = g_i["final_obs"].cpu().numpy()
+        m = r_d & g_d
+        if m.any():
+            errs[-1] = max(errs[-1], np.abs(fin[m] - r_i["final_obs"][m]).max())
+        np.testing.assert_array_equal(g_i["truncated"].cpu().numpy().astype(bool) & ~(g_d != r_d), r_i["truncated"] & ~(g_d != r_d))
+    gsf, gsi = env.get_state()
+    rsf, rsi = ref.get_state()
+    env.close()
+    ref.close()
+    return np.array(errs), done_mismatch, rew_err, (gsf.cpu().numpy(), gsi.cpu().numpy()), (rsf, rsi)
+
+
+@pytest.mark.parametrize("env_id,kw", CASES)
+def test_kernel_matches_fp32_restatement(gpu, env_id, kw):
+    n, T = 512, 120
+    errs, dmis, rew_err, (gsf, gsi), (rsf, rsi) = _run_pair(env_id, kw, n, T, "f32")
+    assert errs[0] < 1e-5, "reset observation"
+    assert errs.max() < 2e-4, f"obs max err {errs.max()}"
+    assert dmis == 0
+    assert rew_err < 2e-3 * 1000 / 1000 + 1e-3
+    np.testing.assert_array_equal(gsi[0], rsi[0])   # episode steps
+    np.testing.assert_array_equal(gsi[1], rsi[1])   # RNG counters
+    fields = list(range(0, 13)) + list(range(16, 24)) + list(range(56, 81))
+    assert np.abs(gsf[fields] - rsf[fields]).max() < 1e-4
+
+
+@pytest.mark.parametrize("env_id,kw", CASES[:3])
+def test_kernel_tracks_fp64_restatement(gpu, env_id, kw):
+    errs, dmis, rew_err, (gsf, gsi), (rsf, rsi) = _run_pair(env_id, kw, 512, 120, "f64")
+    assert errs.max() < 5e-3
+    assert dmis <= 2
+
+
+def test_noise_free_state_within_1e4_relative_over_240_steps(gpu):
+    """BASELINE.json target: state within 1e-4 rel over 240 steps (here vs the fp64 restatement,
+    hover-like actions, no noise, no DR; relative to max(|x|, 1))."""
+    env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
+    kw = dict(observation_noise=0, domain_randomization=-1, motor_thrust_noise=0, max_episode_steps=0)
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    n = 256
+    env = BatchedCrazyflieEnv(env_id, n, seed=11, **kw)
+    ref = O.OracleEnv(build_config(env_id, n, seed=11, **kw), "f64")
+    env.reset(); ref.reset()
+    rng = np.random.default_rng(5)
+    alive = np.ones(n, bool)
+    for t in range(240):
+        a = (rng.uniform(-1, 1, (n, 4)) * 0.05 + 0.1111).astype(np.float32)
+        _, _, gd, _ = env.step(torch.from_numpy(a).cuda())
+        _, _, rd, _ = ref.step(a)
+        alive &= ~rd
+    g = env.get_state()[0].cpu().numpy()[:13]
+    r = ref.get_state()[0][:13]
+    rel = np.abs(g - r) / np.maximum(np.abs(r), 1.0)
+    assert rel[:, alive].max() < 1e-4, rel[:, alive].max()
+    assert alive.mean() > 0.5
+
+
+def test_reset_mask_and_state_round_trip(gpu):
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
+    n = 300
+    env = BatchedCrazyflieEnv(env_id, n, seed=21)
+    ref = O.OracleEnv(build_config(env_id, n, seed=21), "f32")
+    env.reset(); ref.reset()
+    rng = np.random.default_rng(0)
+    for t in range(5):
+        a = _actions(rng, n)
+        env.step(torch.from_numpy(a).cuda()); ref.step(a)
+    mask = (np.arange(n) % 3 == 0).astype(np.uint8)
+    go = env.reset(torch.from_numpy(mask).cuda()).cpu().numpy()
+    ro = ref.reset(mask)
+    m = mask.astype(bool)
+    assert np.abs(go[m] - ro[m]).max() < 1e-5
+    sf, si = env.get_state()
+    env2 = BatchedCrazyflieEnv(env_id, n, seed=21)
+    env2.set_state(sf, si)
+    a = torch.from_numpy(_actions(rng, n)).cuda()
+    o1 = env.step(a)[0].clone()
+    o2 = env2.step(a)[0].clone()
+    assert torch.equal(o1, o2)
+
+
+def test_time_limit_truncation_on_gpu(gpu):
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    kw = dict(observation_noise=0, domain_randomization=-1, motor_thrust_noise=0, enable_reset_distribution=False,
+              max_episode_steps=7)
+    env = BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithoutAdversary-v0", 64, seed=0, **kw)
+    env.reset()
+    a = torch.full((64, 4), 0.1111111, device="cuda")
+    for k in range(7):
+        o, r, d, info = env.step(a)
+    assert bool(d.all()) and bool(info["truncated"].all())
+    sf, si = env.get_state()
+    assert int(si[0].max()) == 0
+
+
+def _synthetic_tables(levels=(0.0, 1.5), seed=0):
+    """Smooth random HJ-like value tables over the 15^6 grid (float32, C-order)."""
+    rng = np.random.default_rng(seed)
+    axes = [np.linspace(-1, 1, 15) for _ in range(6)]
+    out = []
+    for li, _ in enumerate(levels):
+        c = rng.normal(size=6)
+        g = [a.reshape([-1 if i == d else 1 for i in range(6)]) for d, a in enumerate(axes)]
+        V = sum(c[d] * g[d] ** (1 + (d % 2)) for d in range(6)) + 0.1 * np.sin(3 * g[3] + 2 * g[4] - g[5])
+        V = V + 0.01 * rng.normal(size=(15,) * 6)
+        out.append(V.astype(np.float32))
+    return np.stack(out)
+
+
+def test_hj_disturbance_batched_matches_restatement(gpu):
+    from cf2sim.vec_env import hj_disturbance
+    c = build_config("DroneHoverBulletFreeEnvWithAdversary-v0", 1)
+    V = _synthetic_tables((1.5,))[0]
+    rng = np.random.default_rng(2)
+    n = 20000
+    s = np.concatenate([rng.uniform(-1.6, 1.6, (n, 3)), rng.uniform(-4, 4, (n, 3))], 1).astype(np.float32)
+    # grid nodes and mid-points exercise the tie rule and the boundary rows
+    from cf2sim.config import hj_grid
+    _, _, pts = hj_grid()
+    s[:200, 3] = pts[3][rng.integers(0, 15, 200)]
+    s[200:400, 4] = 0.5 * (pts[4][:-1] + pts[4][1:])[rng.integers(0, 14, 200)]
+    u, d = hj_disturbance(torch.from_numpy(V).cuda(), torch.from_numpy(s).cuda(), 1.5, c)
+    rd, ru, _ = O.hj(c, V, s.astype(np.float64), 1.5)
+    np.testing.assert_array_equal(d.cpu().numpy(), rd.astype(np.float32))
+    np.testing.assert_array_equal(u.cpu().numpy(), ru.astype(np.float32))
+
+
+@pytest.mark.parametrize("env_id", ["DroneHoverBulletFreeEnvWithAdversary-v0",
+                                    "DroneHoverBulletFreeEnvWithRandomHJAdversary-v0"])
+def test_hj_adversary_env_matches_restatement(gpu, env_id):
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    c = build_config(env_id, 256, seed=4)
+    levels = 21
+    V = _synthetic_tables(tuple(range(3)), seed=1)
+    table_of_level = [l % 3 for l in range(levels)]
+    env = BatchedCrazyflieEnv(env_id, 256, seed=4)
+    env.bind_hj_tables(torch.from_numpy(V).cuda(), table_of_level)
+    ref = O.OracleEnv(c, "f32")
+    ref.bind_tables(V, table_of_level)
+    env.reset(); ref.reset()
+    rng = np.random.default_rng(9)
+    for t in range(60):
+        a = _actions(rng, 256)
+        go, gr, gd, gi = env.step(torch.from_numpy(a).cuda())
+        ro, rr, rd, ri = ref.step(a)
+        assert np.abs(go.cpu().numpy() - ro).max() < 5e-4
+        np.testing.assert_allclose(gi["disturbance_level"].cpu().numpy(), ri["level"], atol=1e-6)
