@@ -721,7 +721,7 @@ static void reset_env(orc_ctx* X, int i, REAL* obs) {
     /* obs = compute_observation(); histories filled with it; compute_history() */
     REAL o0[17], o1[17];
     compute_observation(X, E, &g, 32, o0);
-    for (int k = 0; k < 17; ++k) E->obs_prev[k] = o0[k];
+    for (int k = 0; k < obs_len(c); ++k) E->obs_prev[k] = o0[k];
     E->halias[0] = E->halias[1] = 1;
     for (int s = 0; s < 2; ++s) for (int k = 0; k < 4; ++k) E->hact[s][k] = E->last_action[k];
     compute_observation(X, E, &g, 40, o1);
