@@ -16,7 +16,7 @@ import torch  # noqa: F401  (loads the process' HIP runtime before libcf2sim)
 from .config import CF2Config
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libcf2sim.so")
+LIB_PATH = os.environ.get("CF2SIM_LIB") or os.path.join(PKG_DIR, "libcf2sim.so")   # override: A/B builds
 REPO_INCLUDE = os.path.abspath(os.path.join(PKG_DIR, "..", "..", "include", "cf2sim.h"))
 
 # every symbol include/cf2sim.h declares (checked by tests/test_abi.py)

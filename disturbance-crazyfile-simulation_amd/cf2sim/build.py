@@ -11,9 +11,11 @@ INC_DIR = os.path.abspath(os.path.join(PKG_DIR, "..", "..", "include"))
 LIB = os.path.join(PKG_DIR, "libcf2sim.so")
 SOURCES = ["cf2sim_kernels.hip", "cf2sim_api.cpp"]
 HEADERS = ["cf2sim_internal.h"]
-# -ffp-contract=off keeps the fp32 operation order of the kernels identical to the fp32 build
-# of the CPU restatement (oracle/), so parity is checked at rounding level, not just tolerance.
-FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off", "-Wall"]
+# The env-step is fp32 throughout.  FMA contraction, approximate division/sqrt (v_rcp / v_sqrt,
+# ~1 ulp) and the hardware sin/cos/log are allowed: the kernel is compared against the fp32 and
+# fp64 CPU restatements with stated tolerances (tests/test_gpu_parity.py), not bitwise.
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=fast",
+         "-fgpu-approx-transcendentals", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Wall"]
 
 
 def _hipcc() -> str:

@@ -35,11 +35,12 @@ __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
                                      uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }    // key schedule is wave-uniform: SALU
+        // one v_mad_u64_u32 per product yields both halves
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     }
     return U4{c0, c1, c2, c3};
 }
@@ -51,15 +52,14 @@ struct Rng {
 
 __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
 
+// Box-Muller on the hardware transcendental unit: v_log_f32 is log2, v_sin/v_cos_f32 take
+// their argument in revolutions, so sin(2 pi u2) needs no range reduction at all.
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
     const float u1 = ((float)(a >> 8) + 1.0f) * 5.9604644775390625e-08f;
     const float u2 = (float)(b >> 8) * 5.9604644775390625e-08f;
-    const float r = sqrtf(-2.0f * logf(u1));
-    const float th = 6.283185307179586f * u2;
-    float s, c;
-    sincosf(th, &s, &c);
-    z0 = r * c;
-    z1 = r * s;
+    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2(u1)
+    z0 = r * __builtin_amdgcn_cosf(u2);
+    z1 = r * __builtin_amdgcn_sinf(u2);
 }
 
 // N normals from consecutive blocks starting at b0 (pair k uses u32 2k, 2k+1)
@@ -218,9 +218,24 @@ struct Env {
     float la[4];                    // drone.last_action
 };
 
+// o_{k-1} and the action history are consumed only by compute_history at the end of a step:
+// the step kernel loads them after the physics loop so they do not occupy registers across it.
+template <bool NOISE>
+__device__ __forceinline__ void load_hist(const KParams& P, const float* __restrict__ sf, uint32_t i, Env& E) {
+    const uint32_t N = P.N;
+    constexpr int OL = NOISE ? 13 : 17;
+#pragma unroll
+    for (int k = 0; k < OL; ++k) E.obs_prev[k] = sf[(size_t)(F_OBS_PREV + k) * N + i];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.hact[s][k] = sf[(size_t)(F_HIST_ACT + 4 * s + k) * N + i];
+}
+
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ void load_env(const KParams& P, const float* __restrict__ sf,
-                                         const int32_t* __restrict__ si, uint32_t i, Env& E, bool need_level = true) {
+                                         const int32_t* __restrict__ si, uint32_t i, Env& E, bool need_level = true,
+                                         bool with_hist = true) {
     const uint32_t N = P.N;
 #define LD(f) sf[(size_t)(f) * N + i]
 #pragma unroll
@@ -256,13 +271,7 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
             for (int k = 0; k < 10; ++k) E.held[k] = 0.0f;
         }
     }
-    constexpr int OL = NOISE ? 13 : 17;
-#pragma unroll
-    for (int k = 0; k < OL; ++k) E.obs_prev[k] = LD(F_OBS_PREV + k);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) E.hact[s][k] = LD(F_HIST_ACT + 4 * s + k);
+    if (with_hist) load_hist<NOISE>(P, sf, i, E);
     if (DR) {
         E.dt = LD(F_PARAM + 0); E.m = LD(F_PARAM + 1);
         E.J[0] = LD(F_PARAM + 2); E.J[1] = LD(F_PARAM + 3); E.J[2] = LD(F_PARAM + 4);
@@ -292,9 +301,9 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
     E.gust_left = P.dstb_mode == DSTB_GUST_T ? si[(size_t)I_GUST * N + i] : 0;
 }
 
+// state the physics sub-steps update (stored as soon as the last sub-step is done)
 template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
-                                          uint32_t i, const Env& E, bool params_dirty) {
+__device__ __forceinline__ void store_core(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
     const uint32_t N = P.N;
 #define ST(f, val) sf[(size_t)(f) * N + i] = (val)
 #pragma unroll
@@ -327,13 +336,43 @@ __device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ 
             for (int k = 0; k < 10; ++k) ST(F_HELD + k, E.held[k]);
         }
     }
+    if (P.dstb_mode == DSTB_GUST_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ST(F_DSTB + k, E.dstb[k]);
+    }
+#undef ST
+}
+
+template <bool NOISE>
+__device__ __forceinline__ void store_hist(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
+    const uint32_t N = P.N;
     constexpr int OL = NOISE ? 13 : 17;
 #pragma unroll
-    for (int k = 0; k < OL; ++k) ST(F_OBS_PREV + k, E.obs_prev[k]);
+    for (int k = 0; k < OL; ++k) sf[(size_t)(F_OBS_PREV + k) * N + i] = E.obs_prev[k];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ST(F_HIST_ACT + 4 * s + k, E.hact[s][k]);
+        for (int k = 0; k < 4; ++k) sf[(size_t)(F_HIST_ACT + 4 * s + k) * N + i] = E.hact[s][k];
+}
+
+__device__ __forceinline__ void store_ints(const KParams& P, int32_t* __restrict__ si, uint32_t i, const Env& E,
+                                           bool with_level) {
+    const uint32_t N = P.N;
+    si[(size_t)I_EP_STEP * N + i] = E.ep_step;
+    si[(size_t)I_RNG * N + i] = (int32_t)E.rng;
+    si[(size_t)I_FLAGS * N + i] = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6);
+    if (with_level) si[(size_t)I_LEVEL * N + i] = E.level_idx;
+    if (P.dstb_mode == DSTB_GUST_T) si[(size_t)I_GUST * N + i] = E.gust_left;
+}
+
+// whole state (reset paths): core + history + per-episode parameters + counters
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
+                                          uint32_t i, const Env& E, bool params_dirty) {
+    const uint32_t N = P.N;
+    store_core<NOISE, DR, PHYS>(P, sf, i, E);
+    store_hist<NOISE>(P, sf, i, E);
+#define ST(f, val) sf[(size_t)(f) * N + i] = (val)
     if (DR && params_dirty) {
         ST(F_PARAM + 0, E.dt); ST(F_PARAM + 1, E.m);
         ST(F_PARAM + 2, E.J[0]); ST(F_PARAM + 3, E.J[1]); ST(F_PARAM + 4, E.J[2]);
@@ -341,17 +380,13 @@ __device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 4; ++k) { ST(F_PARAM + 7 + k, E.A[k]); ST(F_PARAM + 11 + k, E.B[k]); ST(F_PARAM + 15 + k, E.K[k]); }
     }
-    if (P.dstb_mode == DSTB_CONST_T ? params_dirty : P.dstb_mode == DSTB_GUST_T) {
+    if (P.dstb_mode == DSTB_CONST_T && params_dirty) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) ST(F_DSTB + k, E.dstb[k]);
     }
     if (params_dirty) ST(F_LEVEL, E.level);
 #undef ST
-    si[(size_t)I_EP_STEP * N + i] = E.ep_step;
-    si[(size_t)I_RNG * N + i] = (int32_t)E.rng;
-    si[(size_t)I_FLAGS * N + i] = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6);
-    if (params_dirty) si[(size_t)I_LEVEL * N + i] = E.level_idx;
-    if (P.dstb_mode == DSTB_GUST_T) si[(size_t)I_GUST * N + i] = E.gust_left;
+    store_ints(P, si, i, E, params_dirty);
 }
 
 // ------------------------------------------------------------------------------------
@@ -828,13 +863,16 @@ __device__ __forceinline__ void write_obs(float* __restrict__ dst, uint32_t i, c
 }
 
 template <bool NOISE, bool DR, int PHYS>
-__global__ void __launch_bounds__(256) step_kernel(KParams P, StepIO io) {
+#ifndef CF2_STEP_MIN_WAVES
+#define CF2_STEP_MIN_WAVES 2   // waves per SIMD the register allocator must leave room for
+#endif
+__global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P, StepIO io) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     Env E;
-    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, P.need_level || io.level != nullptr);
+    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
     const uint32_t gid = P.gid_off + i;
     const float4 a4 = reinterpret_cast<const float4*>(io.act)[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -910,9 +948,11 @@ __global__ void __launch_bounds__(256) step_kernel(KParams P, StepIO io) {
         float dummy[17];
         compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy);
     }
-    float onx[17], o[OD];
+    float onx[17];
     compute_observation<NOISE>(P, E, g, 8 + 8 * P.agg, (E.ep_step + 1) * P.agg, onx);
-    compute_history<NOISE>(P, E, onx, o);
+    // the physics state is final now (an auto-reset below overwrites it): store it early so
+    // its registers free up before the epilogue
+    store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
     const bool term = compute_done(P, E);
     const float r = compute_reward(P, E, a, term);
     const float cost = compute_cost(P, E);
@@ -924,15 +964,36 @@ __global__ void __launch_bounds__(256) step_kernel(KParams P, StepIO io) {
     if (io.trunc) io.trunc[i] = (uint8_t)trunc;
     if (io.cost) io.cost[i] = cost;
     if (io.level) io.level[i] = level_used;
-    bool params_dirty = false;
-    if (done && P.auto_reset) {
-        if (io.final_obs) write_obs<NOISE>(io.final_obs, i, o);
-        reset_env<NOISE, DR, PHYS>(P, E, gid, o);
-        params_dirty = true;
+    const bool do_reset = done && P.auto_reset;
+    load_hist<NOISE>(P, io.sf, i, E);
+    {
+        float o[OD];
+        compute_history<NOISE>(P, E, onx, o);
+        float* dst = do_reset ? io.final_obs : io.obs;   // a reset env returns its reset obs
+        if (dst) write_obs<NOISE>(dst, i, o);
     }
-    E.rng += 1;
+    if (!do_reset) {
+        store_hist<NOISE>(P, io.sf, i, E);
+        E.rng += 1;
+        store_ints(P, io.si, i, E, false);
+        return;
+    }
+    // vector-env auto-reset (rare): a fresh Env carrying only what reset reads from the old one
+    Env R;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) R.wb[k] = E.wb[k];    // stale drone.rpy_dot seeds the gyro LPF
+#pragma unroll
+    for (int k = 0; k < 3; ++k) R.bias[k] = E.bias[k]; // SensorNoise.gyro_bias is never reset
+#pragma unroll
+    for (int k = 0; k < 4; ++k) R.ou[k] = E.ou[k];     // nor is the OU thrust-noise state
+    R.rng = E.rng;
+    R.level = E.level;
+    R.level_idx = E.level_idx;
+    float o[OD];
+    reset_env<NOISE, DR, PHYS>(P, R, gid, o);
+    R.rng += 1;
     write_obs<NOISE>(io.obs, i, o);
-    store_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, params_dirty);
+    store_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, R, true);
 }
 
 template <bool NOISE, bool DR, int PHYS>
