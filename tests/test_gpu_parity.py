@@ -82,7 +82,8 @@ def test_kernel_matches_fp32_restatement(gpu, env_id, kw):
     ol = 13 if kw.get("observation_noise", 1) > 0 else 17
     fields = list(range(0, 13)) + list(range(16, 24)) + list(range(56, 56 + ol)) + list(range(73, 81))
     fe = (np.abs(gsf[fields] - rsf[fields]) / (1 + np.abs(rsf[fields]))).max(1)
-    assert fe.max() < 1e-4, {f: float(e) for f, e in zip(fields, fe) if e >= 1e-5}
+    top = sorted(zip(fe.tolist(), fields), reverse=True)[:4]
+    assert fe.max() < 1e-4, "state field errors (err, field): " + repr(top)
 
 
 @pytest.mark.parametrize("env_id,kw", CASES[:3])
