@@ -103,7 +103,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=4096)
     ap.add_argument("--cpu-steps", type=int, default=1500)
+    ap.add_argument("--env-kw", default="{}", help="JSON env kwargs (ablations), e.g. '{\"observation_noise\": 0}'")
     args = ap.parse_args()
+    env_kw = json.loads(args.env_kw)
 
     import torch
     import torch.distributed as dist
@@ -119,7 +121,7 @@ def main():
     from cf2sim.vec_env import BatchedCrazyflieEnv
 
     n = args.envs_per_gpu
-    env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=rank * n, device=dev)
+    env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=rank * n, device=dev, **env_kw)
     env.reset()
     ring = 8
     g = torch.Generator(device=dev)
