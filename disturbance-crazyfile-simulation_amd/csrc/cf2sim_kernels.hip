@@ -218,26 +218,51 @@ struct Env {
     float la[4];                    // drone.last_action
 };
 
+// ------------------------------------------------------------------------------------
+// SoA field access through buffer descriptors: one 32-bit VGPR offset (env * 4) serves every
+// field; the per-field base (field * N * 4) is a wave-uniform SGPR soffset.  With plain 64-bit
+// global addresses each field's address would occupy two VGPRs from its load to its store.
+// ------------------------------------------------------------------------------------
+struct SoA {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t stride, voff;
+    __device__ __forceinline__ SoA(const void* base, uint32_t N, uint32_t nfields, uint32_t i)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(N * 4u * nfields), 0x00020000)),
+          stride(N * 4u), voff(i * 4u) {}
+    __device__ __forceinline__ float ld(int f) const {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(f * stride), 0));
+    }
+    __device__ __forceinline__ void st(int f, float v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)(f * stride), 0);
+    }
+    __device__ __forceinline__ int ldi(int f) const {
+        return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(f * stride), 0);
+    }
+    __device__ __forceinline__ void sti(int f, int v) const {
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, (int)voff, (int)(f * stride), 0);
+    }
+};
+
 // o_{k-1} and the action history are consumed only by compute_history at the end of a step:
 // the step kernel loads them after the physics loop so they do not occupy registers across it.
 template <bool NOISE>
 __device__ __forceinline__ void load_hist(const KParams& P, const float* __restrict__ sf, uint32_t i, Env& E) {
-    const uint32_t N = P.N;
+    const SoA S(sf, P.N, NF, i);
     constexpr int OL = NOISE ? 13 : 17;
 #pragma unroll
-    for (int k = 0; k < OL; ++k) E.obs_prev[k] = sf[(size_t)(F_OBS_PREV + k) * N + i];
+    for (int k = 0; k < OL; ++k) E.obs_prev[k] = S.ld(F_OBS_PREV + k);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) E.hact[s][k] = sf[(size_t)(F_HIST_ACT + 4 * s + k) * N + i];
+        for (int k = 0; k < 4; ++k) E.hact[s][k] = S.ld(F_HIST_ACT + 4 * s + k);
 }
 
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ void load_env(const KParams& P, const float* __restrict__ sf,
                                          const int32_t* __restrict__ si, uint32_t i, Env& E, bool need_level = true,
                                          bool with_hist = true) {
-    const uint32_t N = P.N;
-#define LD(f) sf[(size_t)(f) * N + i]
+    const SoA S(sf, P.N, NF, i), SI(si, P.N, NI, i);
+#define LD(f) S.ld(f)
 #pragma unroll
     for (int k = 0; k < 3; ++k) E.p[k] = LD(F_POS + k);
 #pragma unroll
@@ -293,19 +318,19 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
     }
     E.level = need_level ? LD(F_LEVEL) : P.level_fixed;
 #undef LD
-    E.ep_step = si[(size_t)I_EP_STEP * N + i];
-    E.rng = (uint32_t)si[(size_t)I_RNG * N + i];
-    const int fl = si[(size_t)I_FLAGS * N + i];
+    E.ep_step = SI.ldi(I_EP_STEP);
+    E.rng = (uint32_t)SI.ldi(I_RNG);
+    const int fl = SI.ldi(I_FLAGS);
     E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
-    E.level_idx = need_level ? si[(size_t)I_LEVEL * N + i] : 0;
-    E.gust_left = P.dstb_mode == DSTB_GUST_T ? si[(size_t)I_GUST * N + i] : 0;
+    E.level_idx = need_level ? SI.ldi(I_LEVEL) : 0;
+    E.gust_left = P.dstb_mode == DSTB_GUST_T ? SI.ldi(I_GUST) : 0;
 }
 
 // state the physics sub-steps update (stored as soon as the last sub-step is done)
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
-    const uint32_t N = P.N;
-#define ST(f, val) sf[(size_t)(f) * N + i] = (val)
+    const SoA S(sf, P.N, NF, i);
+#define ST(f, val) S.st(f, val)
 #pragma unroll
     for (int k = 0; k < 3; ++k) ST(F_POS + k, E.p[k]);
 #pragma unroll
@@ -345,34 +370,34 @@ __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__
 
 template <bool NOISE>
 __device__ __forceinline__ void store_hist(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
-    const uint32_t N = P.N;
+    const SoA S(sf, P.N, NF, i);
     constexpr int OL = NOISE ? 13 : 17;
 #pragma unroll
-    for (int k = 0; k < OL; ++k) sf[(size_t)(F_OBS_PREV + k) * N + i] = E.obs_prev[k];
+    for (int k = 0; k < OL; ++k) S.st(F_OBS_PREV + k, E.obs_prev[k]);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) sf[(size_t)(F_HIST_ACT + 4 * s + k) * N + i] = E.hact[s][k];
+        for (int k = 0; k < 4; ++k) S.st(F_HIST_ACT + 4 * s + k, E.hact[s][k]);
 }
 
 __device__ __forceinline__ void store_ints(const KParams& P, int32_t* __restrict__ si, uint32_t i, const Env& E,
                                            bool with_level) {
-    const uint32_t N = P.N;
-    si[(size_t)I_EP_STEP * N + i] = E.ep_step;
-    si[(size_t)I_RNG * N + i] = (int32_t)E.rng;
-    si[(size_t)I_FLAGS * N + i] = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6);
-    if (with_level) si[(size_t)I_LEVEL * N + i] = E.level_idx;
-    if (P.dstb_mode == DSTB_GUST_T) si[(size_t)I_GUST * N + i] = E.gust_left;
+    const SoA SI(si, P.N, NI, i);
+    SI.sti(I_EP_STEP, E.ep_step);
+    SI.sti(I_RNG, (int32_t)E.rng);
+    SI.sti(I_FLAGS, (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6));
+    if (with_level) SI.sti(I_LEVEL, E.level_idx);
+    if (P.dstb_mode == DSTB_GUST_T) SI.sti(I_GUST, E.gust_left);
 }
 
 // whole state (reset paths): core + history + per-episode parameters + counters
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
                                           uint32_t i, const Env& E, bool params_dirty) {
-    const uint32_t N = P.N;
+    const SoA S(sf, P.N, NF, i);
     store_core<NOISE, DR, PHYS>(P, sf, i, E);
     store_hist<NOISE>(P, sf, i, E);
-#define ST(f, val) sf[(size_t)(f) * N + i] = (val)
+#define ST(f, val) S.st(f, val)
     if (DR && params_dirty) {
         ST(F_PARAM + 0, E.dt); ST(F_PARAM + 1, E.m);
         ST(F_PARAM + 2, E.J[0]); ST(F_PARAM + 3, E.J[1]); ST(F_PARAM + 4, E.J[2]);
