@@ -1,0 +1,147 @@
+"""Pin the CPU restatement (oracle/) on golden vectors produced by running the REFERENCE's own
+Python (tests/golden/make_golden.py; fixtures are data, the reference is not read here).
+
+What each fixture pins (reference file:line):
+* aa_*   CrazyFlieAgent.apply_action + PWM.act + OUNoise (agents.py:259-298, control.py:94-100,
+         utils.py:111-134), OU draws recorded
+* sn_*   SensorNoise.add_noise / add_noise_to_omega (sensors.py:75-134), draws recorded
+* q_*    get_quaternion_from_euler (utils.py:58-82), quat2euler (distur_gener.py:186-207)
+* boltz  Boltzmann() probabilities (utils.py:27-39)
+* hj     distur_gener() incl. Grid.get_index and the boundary rules (distur_gener.py:19-183,
+         GridProcessing.py:52-71) on an exactly reproducible synthetic value table
+* env    whole env-steps of DroneHoverBulletFreeEnvWithoutAdversary / DroneHoverBulletEnv /
+         DroneHoverBulletEnvWithoutAdversary / DroneHoverSimpleEnv driven by the reference's
+         real-flight PWM logs: apply_action, latency ring, drag, force/torque assembly,
+         update_information, compute_observation/history (with the action-buffer alias),
+         reward/done/info are the reference's code; SimplePhysics is the reference's code; the
+         Bullet integrator inside the fake physics server is a numpy restatement (PyBullet is
+         not installable here: parity of that one piece vs PyBullet is unpinned).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from cf2sim.config import boltzmann_table, build_config
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def test_apply_action_matches_reference():
+    g = load("golden_components.npz")
+    c = build_config("DroneHoverBulletEnv-v0", 1)
+    f, tz, x = O.apply_action(c, g["aa_actions"], g["aa_ou_normals"], g["aa_init_x"], g["aa_init_buf"])
+    np.testing.assert_allclose(f, g["aa_forces"], rtol=1e-13, atol=1e-16)
+    np.testing.assert_allclose(tz, g["aa_tz"], rtol=1e-12, atol=1e-16)
+    np.testing.assert_allclose(x, g["aa_x"], rtol=1e-14)
+
+
+def test_sensor_noise_matches_reference():
+    g = load("golden_components.npz")
+    c = build_config("DroneHoverBulletFreeEnvWithoutAdversary-v0", 1)
+    ins, draws, outs = g["sn_in"], g["sn_draws"], g["sn_out"]
+    for k in range(len(ins)):
+        pos, vel, rot, om, bias = ins[k][0:3], ins[k][3:6], ins[k][6:9], ins[k][9:12], ins[k][12:15]
+        p, v, r, o, b = O.add_noise(c, pos, vel, rot, om, draws[k][:18], draws[k][18:24], bias)
+        np.testing.assert_allclose(np.concatenate([p, v, r, o, b]), outs[k], rtol=1e-14, atol=1e-15)
+
+
+def test_quaternion_conversions_match_reference():
+    g = load("golden_components.npz")
+    for rpy, q in zip(g["q_rpy"], g["q_utils"]):
+        np.testing.assert_allclose(O.quat_from_euler(rpy), q / np.linalg.norm(q), atol=1e-15)
+    for q, e in zip(g["q_quats"], g["q_quat2euler"]):
+        np.testing.assert_allclose(O.quat2euler(q), e, atol=1e-14)
+
+
+def test_boltzmann_probabilities_match_reference():
+    g = load("golden_components.npz")
+    values, cdf = boltzmann_table()
+    np.testing.assert_allclose(values, np.around(g["boltz_energies"], 1))
+    p = g["boltz_p"]
+    np.testing.assert_allclose(np.diff(np.concatenate([[0.0], cdf])), p / p.sum(), rtol=1e-12)
+
+
+def synthetic_value_table():
+    i = np.indices((15,) * 6, dtype=np.int64)
+    bowl = (i[3] - 7) ** 2 + (i[4] - 7) ** 2 + 2 * (i[5] - 7) ** 2 + (i[0] - 7) - (i[1] - 7)
+    lin = np.arange(15 ** 6, dtype=np.uint64).reshape((15,) * 6)
+    h = ((lin * np.uint64(2654435761)) >> np.uint64(13)) & np.uint64(255)
+    return (bowl.astype(np.float32) + (h.astype(np.float32) - np.float32(128)) / np.float32(64)).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def V():
+    return synthetic_value_table()
+
+
+@pytest.mark.parametrize("level", [0.0, 1.5, 3.0])
+def test_hj_disturbance_matches_reference(V, level):
+    g = load("golden_hj.npz")
+    c = build_config("DroneHoverBulletFreeEnvWithAdversary-v0", 1)
+    d, u, idx = O.hj(c, V, g["states"], level)
+    ref = g[f"ud_{level}"]
+    np.testing.assert_array_equal(u, ref[:, :3])
+    np.testing.assert_array_equal(d, ref[:, 3:])
+
+
+ENV_IDS = {"DroneHoverBulletFreeEnvWithoutAdversary": "DroneHoverBulletFreeEnvWithoutAdversary-v0",
+           "DroneHoverBulletEnv": "DroneHoverBulletEnv-v0",
+           "DroneHoverBulletEnvWithoutAdversary": "DroneHoverBulletEnvWithoutAdversary-v0",
+           "DroneHoverSimpleEnv": "DroneHoverSimpleEnv-v0"}
+
+
+def oracle_from_golden(g, key, env_id, precision="f64"):
+    """Oracle env whose state is the reference env's state right after its reset()."""
+    c = build_config(env_id, 1, observation_noise=0, domain_randomization=-1, motor_thrust_noise=0,
+                     max_episode_steps=0, auto_reset=False)
+    env = O.OracleEnv(c, precision)
+    sf, si = env.get_state()
+    sf[:] = 0
+    simple = "Simple" in key
+    obs0 = g[key + "__obs0"]
+    if simple:
+        sf[0:3, 0] = g[key + "__init_xyz"]; sf[3:7, 0] = g[key + "__init_quat"]; sf[7:10, 0] = g[key + "__init_xyz_dot"]
+        sf[10:13, 0] = g[key + "__init_rpy_dot"]; sf[13:16, 0] = g[key + "__init_rpy"]
+    else:
+        sf[0:3, 0] = g[key + "__init_p"]; sf[3:7, 0] = g[key + "__init_q"]; sf[7:10, 0] = g[key + "__init_v"]
+        sf[10:13, 0] = g[key + "__init_w"]
+    sf[16:20, 0] = g[key + "__init_x"]
+    abuf = g[key + "__init_abuf"]
+    for r in range(abuf.shape[0]):
+        sf[24 + 4 * r:28 + 4 * r, 0] = abuf[r]
+    sf[56:73, 0] = obs0[21:38]                       # o_0 of the reset history
+    sf[73:77, 0] = obs0[17:21]; sf[77:81, 0] = obs0[38:42]
+    sf[81, 0] = c.time_step; sf[82, 0] = c.mass; sf[83:86, 0] = (c.ixx, c.iyy, c.izz)
+    sf[86, 0] = c.ft0; sf[87, 0] = c.ft1
+    sf[88:92, 0] = c.A; sf[92:96, 0] = c.B; sf[96:100, 0] = c.K
+    si[:] = 0
+    si[2, 0] = (1 << 4) | (1 << 5) | (1 << 6)      # both history entries alias action_buffer[-1]
+    env.set_state(sf, si)
+    return env
+
+
+def golden_keys():
+    g = load("golden_env_trajectories.npz")
+    return sorted({k.split("__")[0] + "__" + k.split("__")[1] for k in g.files})
+
+
+@pytest.mark.parametrize("key", golden_keys())
+def test_env_steps_match_reference(key):
+    g = load("golden_env_trajectories.npz")
+    env = oracle_from_golden(g, key, ENV_IDS[key.split("__")[0]])
+    acts, obs, rew, done, cost = (g[key + s] for s in ("__actions", "__obs", "__rew", "__done", "__cost"))
+    assert len(acts) >= 10
+    for t in range(len(acts)):
+        o, r, d, info = env.step(acts[t:t + 1])
+        err = np.abs(o[0] - obs[t]) / (1 + np.abs(obs[t]))
+        assert err.max() < 1e-9, (t, err.max(), np.argmax(err))
+        assert abs(r[0] - rew[t]) <= 1e-9 * (1 + abs(rew[t])), (t, r[0], rew[t])
+        assert bool(d[0]) == bool(done[t]), t
+        assert info["cost"][0] == cost[t], t
+    env.close()
