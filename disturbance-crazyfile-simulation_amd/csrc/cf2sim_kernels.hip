@@ -47,7 +47,14 @@ __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
 
 struct Rng {
     uint32_t k0, k1, ctr, gid, tag;
-    __device__ __forceinline__ U4 block(uint32_t b) const { return philox(b, ctr, gid, tag, k0, k1); }
+    __device__ __forceinline__ U4 block(uint32_t b) const {
+        // launder the key so its 10-round schedule is rebuilt per block on the SALU instead of
+        // being CSE'd into 20 SGPRs live across the kernel (spilled to VGPR lanes, re-read with
+        // one VALU v_readlane each)
+        uint32_t a = k0, c = k1;
+        asm volatile("" : "+s"(a), "+s"(c));
+        return philox(b, ctr, gid, tag, a, c);
+    }
 };
 
 __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
@@ -229,17 +236,24 @@ struct SoA {
     __device__ __forceinline__ SoA(const void* base, uint32_t N, uint32_t nfields, uint32_t i)
         : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(N * 4u * nfields), 0x00020000)),
           stride(N * 4u), voff(i * 4u) {}
+    // field * stride is recomputed per access (one s_mul_i32): a CSE'd per-field offset would be
+    // one more SGPR live from the load phase to the store phase, and the ~100 of them spill
+    __device__ __forceinline__ int fo(int f) const {
+        uint32_t s = stride;
+        asm volatile("" : "+s"(s));
+        return (int)((uint32_t)f * s);
+    }
     __device__ __forceinline__ float ld(int f) const {
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(f * stride), 0));
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, fo(f), 0));
     }
     __device__ __forceinline__ void st(int f, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, (int)(f * stride), 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, fo(f), 0);
     }
     __device__ __forceinline__ int ldi(int f) const {
-        return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)(f * stride), 0);
+        return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, fo(f), 0);
     }
     __device__ __forceinline__ void sti(int f, int v) const {
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, (int)voff, (int)(f * stride), 0);
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, (int)voff, fo(f), 0);
     }
 };
 
@@ -891,13 +905,10 @@ __device__ __forceinline__ void write_obs(float* __restrict__ dst, uint32_t i, c
     for (int k = 0; k < OD / 2; ++k) d2[k] = make_float2(o[2 * k], o[2 * k + 1]);
 }
 
+// One env-step of env i (aggregate_phy_steps physics sub-steps, observation, reward, done);
+// returns whether the env finished and must be auto-reset.
 template <bool NOISE, bool DR, int PHYS>
-#ifndef CF2_STEP_MIN_WAVES
-#define CF2_STEP_MIN_WAVES 2   // waves per SIMD the register allocator must leave room for
-#endif
-__global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P, StepIO io) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.N) return;
+__device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     Env E;
@@ -1001,28 +1012,84 @@ __global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P
         float* dst = do_reset ? io.final_obs : io.obs;   // a reset env returns its reset obs
         if (dst) write_obs<NOISE>(dst, i, o);
     }
-    if (!do_reset) {
-        store_hist<NOISE>(P, io.sf, i, E);
-        E.rng += 1;
-        store_ints(P, io.si, i, E, false);
-        return;
+    store_hist<NOISE>(P, io.sf, i, E);
+    E.rng += 1;
+    store_ints(P, io.si, i, E, false);
+    return do_reset;
+}
+
+// Reset one env in place: reads only what a reset consumes from the finished episode (the
+// stale body rates for the gyro LPF, the never-reset gyro bias and OU state, the RNG counter
+// and the disturbance level), writes the reset observation row and the whole state.
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
+                                          uint32_t i, float* __restrict__ obs, uint32_t rng_ctr) {
+    constexpr int OD = NOISE ? 34 : 42;
+    const SoA S(sf, P.N, NF, i), SI(si, P.N, NI, i);
+    Env E;
+    float q[4], w[3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = S.ld(F_QUAT + k);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = S.ld(F_OMEGA + k);
+    if (PHYS == PHYS_BULLET_T) {
+        const M3 R = rotmat(q);
+        mtv(R, w, E.wb);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.wb[k] = w[k];
     }
-    // vector-env auto-reset (rare): a fresh Env carrying only what reset reads from the old one
-    Env R;
+    if (NOISE) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) R.wb[k] = E.wb[k];    // stale drone.rpy_dot seeds the gyro LPF
+        for (int k = 0; k < 3; ++k) E.bias[k] = S.ld(F_BIAS + k);
+    }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) R.bias[k] = E.bias[k]; // SensorNoise.gyro_bias is never reset
-#pragma unroll
-    for (int k = 0; k < 4; ++k) R.ou[k] = E.ou[k];     // nor is the OU thrust-noise state
-    R.rng = E.rng;
-    R.level = E.level;
-    R.level_idx = E.level_idx;
+    for (int k = 0; k < 4; ++k) E.ou[k] = S.ld(F_OU + k);
+    E.rng = rng_ctr;
+    E.level = S.ld(F_LEVEL);
+    E.level_idx = SI.ldi(I_LEVEL);
     float o[OD];
-    reset_env<NOISE, DR, PHYS>(P, R, gid, o);
-    R.rng += 1;
-    write_obs<NOISE>(io.obs, i, o);
-    store_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, R, true);
+    reset_env<NOISE, DR, PHYS>(P, E, P.gid_off + i, o);
+    E.rng = rng_ctr + 1;
+    if (obs) write_obs<NOISE>(obs, i, o);
+    store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
+}
+
+#ifndef CF2_STEP_MIN_WAVES
+#define CF2_STEP_MIN_WAVES 2   // waves per SIMD the register allocator must leave room for
+#endif
+// Step kernel: one lane per env.  Auto-reset is compacted per block: with random actions a few
+// % of envs finish per step, so nearly every wave would hold one and run the whole reset path
+// divergently.  Finished envs are listed in LDS and reset by the fewest waves after a block
+// barrier; their state rows were just written by this block and are still in L2, so the reset's
+// scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
+// 4-byte field access for them).
+template <bool NOISE, bool DR, int PHYS>
+__global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P, StepIO io) {
+    __shared__ uint32_t s_list[256];
+    __shared__ uint32_t s_cnt;
+    if (P.auto_reset && threadIdx.x == 0) s_cnt = 0;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool do_reset = false;
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i);
+    if (!P.auto_reset) return;
+    __syncthreads();     // s_cnt initialised (and a fence for the state rows written above)
+    const uint64_t m = __ballot(do_reset);
+    if (m) {
+        const int lane = (int)(threadIdx.x & 63);
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        if (do_reset) s_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+    }
+    __syncthreads();
+    const uint32_t cnt = s_cnt;
+    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+        const uint32_t j = s_list[k];
+        const uint32_t ctr = (uint32_t)io.si[(size_t)I_RNG * P.N + j] - 1u;   // the finished step's counter
+        reset_one<NOISE, DR, PHYS>(P, io.sf, io.si, j, io.obs, ctr);
+    }
 }
 
 template <bool NOISE, bool DR, int PHYS>
@@ -1031,21 +1098,7 @@ __global__ void __launch_bounds__(256) reset_kernel(KParams P, float* __restrict
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     if (mask && !mask[i]) return;
-    constexpr int OD = NOISE ? 34 : 42;
-    Env E;
-    load_env<NOISE, DR, PHYS>(P, sf, si, i, E);
-    if (PHYS == PHYS_BULLET_T) {
-        const M3 R = rotmat(E.q);
-        mtv(R, E.w, E.wb);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.wb[k] = E.w[k];
-    }
-    float o[OD];
-    reset_env<NOISE, DR, PHYS>(P, E, P.gid_off + i, o);
-    E.rng += 1;
-    if (obs) write_obs<NOISE>(obs, i, o);
-    store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
+    reset_one<NOISE, DR, PHYS>(P, sf, si, i, obs, (uint32_t)si[(size_t)I_RNG * P.N + i]);
 }
 
 // initial (pre-reset) state: AgentBase defaults, nominal params

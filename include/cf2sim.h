@@ -66,7 +66,9 @@ enum { CF2_DSTB_NONE = 0,      /* dstb = (0,0,0)                       hover_fre
 enum { CF2_LEVEL_FIXED = 0,      /* env.disturbance_level constant, e.g. 1.5 (hover_free.py:319) */
        CF2_LEVEL_BOLTZMANN = 1 };/* Boltzmann() redraw at the end of every reset (hover_free.py:536) */
 
-#define CF2_MAX_ENVS_PER_CTX  (1u << 27)
+/* 8 Mi envs per context: the state SoA (104 x 4 B x N) must stay addressable by one 32-bit
+   buffer-descriptor range; shard larger populations over several contexts / GPUs. */
+#define CF2_MAX_ENVS_PER_CTX  (1u << 23)
 #define CF2_HJ_PTS 15               /* grid points per dimension, distur_gener.py:179 */
 #define CF2_NUM_LEVELS_MAX 32
 
