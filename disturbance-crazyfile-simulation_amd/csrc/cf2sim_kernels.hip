@@ -87,15 +87,36 @@ __device__ __forceinline__ void normals(const Rng& g, uint32_t b0, float (&z)[N]
     }
 }
 
+// Normals LO..HI-1 of the sequence normals<N>(g, b0, .) would produce, drawing only the Philox
+// blocks and Box-Muller pairs that cover them (the stream positions of all other draws are
+// unchanged, so skipping dead draws is invisible to everything else).
+template <int LO, int HI>
+__device__ __forceinline__ void normals_range(const Rng& g, uint32_t b0, float* z) {
+#pragma unroll
+    for (int blk = LO / 4; blk < (HI + 3) / 4; ++blk) {
+        const U4 u = g.block(b0 + blk);
+        float a[4];
+        if (4 * blk + 1 >= LO && 4 * blk < HI) box_muller(u.x, u.y, a[0], a[1]);
+        if (4 * blk + 3 >= LO && 4 * blk + 2 < HI) box_muller(u.z, u.w, a[2], a[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (4 * blk + k >= LO && 4 * blk + k < HI) z[4 * blk + k] = a[k];
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // rotation helpers (PyBullet C-API semantics)
 // ------------------------------------------------------------------------------------
+// v_rcp_f32 / v_rsq_f32 (1 ulp) for well-scaled operands (no denormal pre-scaling)
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+
 struct M3 { float m[9]; };
 
 __device__ __forceinline__ M3 rotmat(const float q[4]) {
     const float x = q[0], y = q[1], z = q[2], w = q[3];
     const float d = x * x + y * y + z * z + w * w;
-    const float s = 2.0f / d;
+    const float s = 2.0f * rcp(d);
     const float xs = x * s, ys = y * s, zs = z * s;
     const float wx = w * xs, wy = w * ys, wz = w * zs;
     const float xx = x * xs, xy = x * ys, xz = x * zs;
@@ -123,30 +144,65 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) { return x 
 // select of pointers, SROA can no longer promote the Env struct and it lands in scratch.
 __device__ __forceinline__ float opaque(float x) { asm("" : "+v"(x)); return x; }
 
+// ---- short-range elementary functions (VALU polynomials instead of the ocml library paths,
+// whose general range reduction costs ~100 instructions each).  Errors are a few fp32 ulp.
+// sin and cos of x: Cody-Waite reduction by pi/2 (3-part constant, exact for |x| < ~1e4), then
+// degree-11/12 Taylor polynomials on [-pi/4, pi/4] (truncation < 2e-9)
+__device__ __forceinline__ void sincos_fast(float x, float& s, float& c) {
+    const float k = __builtin_rintf(x * 0.63661977236758134f);
+    float r = __builtin_fmaf(k, -1.5707963705062866f, x);
+    r = __builtin_fmaf(k, 4.3711388286737929e-08f, r);
+    r = __builtin_fmaf(k, 1.7151245100059206e-15f, r);
+    const float r2 = r * r;
+    const float sr = r * (1.0f + r2 * (-1.6666667e-1f + r2 * (8.3333333e-3f + r2 * (-1.9841270e-4f + r2 * (2.7557319e-6f - r2 * 2.5052108e-8f)))));
+    const float cr = 1.0f + r2 * (-0.5f + r2 * (4.1666668e-2f + r2 * (-1.3888889e-3f + r2 * (2.4801587e-5f + r2 * (-2.7557319e-7f + r2 * 2.0876757e-9f)))));
+    const int q = (int)k & 3;
+    const float ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+}
+// atan2 (Cephes atanf kernel on the reduced ratio min/max in [0, 1], reduced again about 1)
+__device__ __forceinline__ float atan2_fast(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    float t = mx > 0.0f ? mn * rcp(mx) : 0.0f;
+    const bool red = t > 0.41421356237309503f;
+    const float z = red ? (t - 1.0f) * rcp(t + 1.0f) : t;
+    const float z2 = z * z;
+    float r = (((8.05374449538e-2f * z2 - 1.38776856032e-1f) * z2 + 1.99777106478e-1f) * z2 - 3.33329491539e-1f) * z2 * z + z;
+    r = red ? r + 0.78539816339744831f : r;
+    r = ay > ax ? 1.5707963267948966f - r : r;
+    r = x < 0.0f ? 3.1415926535897932f - r : r;
+    return __builtin_copysignf(r, y);
+}
+__device__ __forceinline__ float asin_fast(float x) {
+    return atan2_fast(x, __builtin_sqrtf(fmaxf(0.0f, (1.0f - x) * (1.0f + x))));
+}
+
 __device__ __forceinline__ void quat_from_euler(const float e[3], float q[4]) {
     const float phi = e[0] * 0.5f, the = e[1] * 0.5f, psi = e[2] * 0.5f;
     float sp, cp, st, ct, ss, cs;
-    sincosf(phi, &sp, &cp);
-    sincosf(the, &st, &ct);
-    sincosf(psi, &ss, &cs);
+    sincos_fast(phi, sp, cp);
+    sincos_fast(the, st, ct);
+    sincos_fast(psi, ss, cs);
     const float x = sp * ct * cs - cp * st * ss;
     const float y = cp * st * cs + sp * ct * ss;
     const float z = cp * ct * ss - sp * st * cs;
     const float w = cp * ct * cs + sp * st * ss;
-    const float len = sqrtf(x * x + y * y + z * z + w * w);
-    q[0] = x / len; q[1] = y / len; q[2] = z / len; q[3] = w / len;
+    const float il = rsq(x * x + y * y + z * z + w * w);
+    q[0] = x * il; q[1] = y * il; q[2] = z * il; q[3] = w * il;
 }
 __device__ __forceinline__ void euler_from_quat(const float q[4], float e[3]) {
     const float sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
     const float sarg = -2.0f * (q[0] * q[2] - q[3] * q[1]);
     if (sarg <= -0.99999f) {
-        e[0] = 0.0f; e[1] = -0.5f * 3.141592653589793f; e[2] = 2.0f * atan2f(q[0], -q[1]);
+        e[0] = 0.0f; e[1] = -0.5f * 3.141592653589793f; e[2] = 2.0f * atan2_fast(q[0], -q[1]);
     } else if (sarg >= 0.99999f) {
-        e[0] = 0.0f; e[1] = 0.5f * 3.141592653589793f; e[2] = 2.0f * atan2f(-q[0], q[1]);
+        e[0] = 0.0f; e[1] = 0.5f * 3.141592653589793f; e[2] = 2.0f * atan2_fast(-q[0], q[1]);
     } else {
-        e[0] = atan2f(2.0f * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
-        e[1] = asinf(sarg);
-        e[2] = atan2f(2.0f * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+        e[0] = atan2_fast(2.0f * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+        e[1] = asin_fast(sarg);
+        e[2] = atan2_fast(2.0f * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
     }
 }
 __device__ __forceinline__ void quat2euler(const float q[4], float e[3]) {
@@ -542,13 +598,14 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
     }
     const float dt = E.dt;
     float wdot_b[3];
-    wdot_b[0] = (tb[0] - gyro[0] - tdamp[0] - pd[0]) / Ic[0];
-    wdot_b[1] = (tb[1] - gyro[1] - tdamp[1] - pd[1]) / Ic[1];
-    wdot_b[2] = (tb[2] - gyro[2] - tdamp[2] - pd[2] - Ip * (sp_new - sp_old) / dt) / Ic[2];
-    const float dampl = P.lin_damping * (1.0f + vn) * E.m / mtot;
+    wdot_b[0] = (tb[0] - gyro[0] - tdamp[0] - pd[0]) * rcp(Ic[0]);
+    wdot_b[1] = (tb[1] - gyro[1] - tdamp[1] - pd[1]) * rcp(Ic[1]);
+    wdot_b[2] = (tb[2] - gyro[2] - tdamp[2] - pd[2] - Ip * (sp_new - sp_old) * rcp(dt)) * rcp(Ic[2]);
+    const float imtot = rcp(mtot);
+    const float dampl = P.lin_damping * (1.0f + vn) * E.m * imtot;
     float vdot_w[3], wdot_w[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) vdot_w[k] = Fw[k] / mtot - dampl * E.v[k];
+    for (int k = 0; k < 3; ++k) vdot_w[k] = Fw[k] * imtot - dampl * E.v[k];
     mv(R, wdot_b, wdot_w);
     const float vmax = P.vmax;
 #pragma unroll
@@ -560,7 +617,7 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
     for (int k = 0; k < 3; ++k) E.p[k] += dt * E.v[k];
     {
         float ang = norm3(E.w);
-        if (ang * dt > 0.7853981633974483f) ang = 0.7853981633974483f / dt;
+        if (ang * dt > 0.7853981633974483f) ang = 0.7853981633974483f * rcp(dt);
         // half-angle h = ang*dt/2 <= pi/8 after the clamp: odd/even Taylor polynomials are exact to
         // fp32 there (truncation < 3e-13), cheaper and more accurate than the hardware sin/cos
         const float h = 0.5f * ang * dt, h2 = h * h;
@@ -568,15 +625,15 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
         const float cw = 1.0f + h2 * (-0.5f + h2 * (4.1666668e-2f + h2 * (-1.3888889e-3f + h2 * (2.4801587e-5f - h2 * 2.7557319e-7f))));
         float s;
         if (ang < 0.001f) s = 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang;
-        else s = sin_h / ang;
+        else s = sin_h * rcp(ang);
         const float axs[3] = {E.w[0] * s, E.w[1] * s, E.w[2] * s};
         const float qx = E.q[0], qy = E.q[1], qz = E.q[2], qw = E.q[3];
         const float nx = cw * qx + axs[0] * qw + axs[1] * qz - axs[2] * qy;
         const float ny = cw * qy + axs[1] * qw + axs[2] * qx - axs[0] * qz;
         const float nz = cw * qz + axs[2] * qw + axs[0] * qy - axs[1] * qx;
         const float nw = cw * qw - axs[0] * qx - axs[1] * qy - axs[2] * qz;
-        const float len = sqrtf(nx * nx + ny * ny + nz * nz + nw * nw);
-        E.q[0] = nx / len; E.q[1] = ny / len; E.q[2] = nz / len; E.q[3] = nw / len;
+        const float il = rsq(nx * nx + ny * ny + nz * nz + nw * nw);
+        E.q[0] = nx * il; E.q[1] = ny * il; E.q[2] = nz * il; E.q[3] = nw * il;
     }
     // update_information
     euler_from_quat(E.q, E.rpy);
@@ -596,8 +653,9 @@ __device__ __forceinline__ void simple_substep(const KParams& P, Env& E, const f
     const float Jw[3] = {E.J[0] * w[0], E.J[1] * w[1], E.J[2] * w[2]};
     const float cr[3] = {w[1] * Jw[2] - w[2] * Jw[1], w[2] * Jw[0] - w[0] * Jw[2], w[0] * Jw[1] - w[1] * Jw[0]};
     const float t[3] = {tx - cr[0], ty - cr[1], tz - cr[2]};
-    const float wdd[3] = {(1.0f / E.J[0]) * t[0], (1.0f / E.J[1]) * t[1], (1.0f / E.J[2]) * t[2]};
-    const float acc[3] = {Fw[0] / E.m, Fw[1] / E.m, Fw[2] / E.m};
+    const float wdd[3] = {rcp(E.J[0]) * t[0], rcp(E.J[1]) * t[1], rcp(E.J[2]) * t[2]};
+    const float im = rcp(E.m);
+    const float acc[3] = {Fw[0] * im, Fw[1] * im, Fw[2] * im};
     const float dt = E.dt;
 #pragma unroll
     for (int k = 0; k < 3; ++k) E.v[k] += dt * acc[k];
@@ -623,9 +681,12 @@ __device__ __forceinline__ void omega_noise(const KParams& P, Env& E, const floa
     for (int k = 0; k < 3; ++k) om[k] = E.wb[k] + E.bias[k] + P.gyro_rw * n[3 + k] + P.gyro_ton * n[6 + k];
 }
 
+// need_held = false: the held measurement of this call is dead (it is overwritten by a later
+// full measurement before any observation is emitted), so a full measurement only advances the
+// gyro (bias walk + LPF) and draws just the gyro normals n[6..15) of its stream positions.
 template <bool NOISE>
 __device__ __forceinline__ void compute_observation(const KParams& P, Env& E, const Rng& g, uint32_t base,
-                                                    int iteration, float* obs) {
+                                                    int iteration, float* obs, bool need_held = true) {
     if (!NOISE) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) obs[k] = E.p[k];
@@ -640,7 +701,12 @@ __device__ __forceinline__ void compute_observation(const KParams& P, Env& E, co
         return;
     }
     float om[3];
-    if (iteration % P.obs_rate == 0) {
+    const bool full = (uint32_t)iteration % (uint32_t)P.obs_rate == 0u;
+    if (full && !need_held) {
+        float n[18];
+        normals_range<6, 15>(g, base, n);
+        omega_noise(P, E, n + 6, om);
+    } else if (full) {
         float n[18];
         normals<18>(g, base, n);
         const U4 ua = g.block(base + 4), ub = g.block(base + 5);
@@ -905,6 +971,19 @@ __device__ __forceinline__ void write_obs(float* __restrict__ dst, uint32_t i, c
     for (int k = 0; k < OD / 2; ++k) d2[k] = make_float2(o[2 * k], o[2 * k + 1]);
 }
 
+// Compile-time view of the env-step shape.  SPEC 1 is the reference default for the Bullet envs
+// (aggregate_phy_steps 2, obs_rate 2, buf_size 2, latency + motor dynamics on): the shape fields
+// of a local KParams copy become constants, so the sub-step loop unrolls, the sensor-call parity
+// and the latency-ring index resolve statically and the dead sub-step draws drop out.
+template <int SPEC>
+__device__ __forceinline__ KParams shape_view(const KParams& P) {
+    KParams Q = P;
+    if (SPEC == 1) {
+        Q.agg = 2; Q.obs_rate = 2; Q.buf_size = 2; Q.use_latency = 1; Q.use_motor_dyn = 1; Q.held_persistent = 0;
+    }
+    return Q;
+}
+
 // One env-step of env i (aggregate_phy_steps physics sub-steps, observation, reward, done);
 // returns whether the env finished and must be auto-reset.
 template <bool NOISE, bool DR, int PHYS>
@@ -986,7 +1065,9 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
         if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0);
         else simple_substep(P, E, a, on);
         float dummy[17];
-        compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy);
+        // a sub-step's held measurement reaches an observation only if the final measurement
+        // of the env-step is not a full one (aggregate_phy_steps % obs_rate != 0)
+        compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy, P.held_persistent != 0);
     }
     float onx[17];
     compute_observation<NOISE>(P, E, g, 8 + 8 * P.agg, (E.ep_step + 1) * P.agg, onx);
@@ -1064,8 +1145,9 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
 // barrier; their state rows were just written by this block and are still in L2, so the reset's
 // scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
 // 4-byte field access for them).
-template <bool NOISE, bool DR, int PHYS>
-__global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P, StepIO io) {
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
+    const KParams P = shape_view<SPEC>(P0);
     __shared__ uint32_t s_list[256];
     __shared__ uint32_t s_cnt;
     if (P.auto_reset && threadIdx.x == 0) s_cnt = 0;
@@ -1092,9 +1174,10 @@ __global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P
     }
 }
 
-template <bool NOISE, bool DR, int PHYS>
-__global__ void __launch_bounds__(256) reset_kernel(KParams P, float* __restrict__ sf, int32_t* __restrict__ si,
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(256) reset_kernel(KParams P0, float* __restrict__ sf, int32_t* __restrict__ si,
                                                     const uint8_t* __restrict__ mask, float* __restrict__ obs) {
+    const KParams P = shape_view<SPEC>(P0);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     if (mask && !mask[i]) return;
@@ -1153,31 +1236,45 @@ __global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* _
 // ------------------------------------------------------------------------------------
 // host-side launch table
 // ------------------------------------------------------------------------------------
-template <bool NOISE, bool DR, int PHYS>
+template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
-    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS>), grid, block, 0, s, P, io);
+    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, io);
     return hipGetLastError();
 }
-template <bool NOISE, bool DR, int PHYS>
+template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_reset_t(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
-    hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS>), grid, block, 0, s, P, sf, si, mask, obs);
+    hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, sf, si, mask, obs);
     return hipGetLastError();
+}
+
+// SPEC 1 when the config has the reference-default Bullet env-step shape (see shape_view)
+static inline bool spec_default_shape(const KParams& P) {
+    return P.phys == PHYS_BULLET_T && P.agg == 2 && P.obs_rate == 2 && P.buf_size == 2 && P.use_latency &&
+           P.use_motor_dyn;
 }
 
 #define CF2_DISPATCH(FN, ...)                                                                          \
     do {                                                                                               \
         const int key = (P.noise ? 4 : 0) | (P.dr ? 2 : 0) | (P.phys == PHYS_SIMPLE_T ? 1 : 0);           \
+        if (spec_default_shape(P)) {                                                                   \
+            switch (key) {                                                                             \
+            case 0: return FN<false, false, PHYS_BULLET_T, 1>(__VA_ARGS__);                            \
+            case 2: return FN<false, true, PHYS_BULLET_T, 1>(__VA_ARGS__);                             \
+            case 4: return FN<true, false, PHYS_BULLET_T, 1>(__VA_ARGS__);                             \
+            default: return FN<true, true, PHYS_BULLET_T, 1>(__VA_ARGS__);                             \
+            }                                                                                          \
+        }                                                                                              \
         switch (key) {                                                                                 \
-        case 0: return FN<false, false, PHYS_BULLET_T>(__VA_ARGS__);                                   \
-        case 1: return FN<false, false, PHYS_SIMPLE_T>(__VA_ARGS__);                                   \
-        case 2: return FN<false, true, PHYS_BULLET_T>(__VA_ARGS__);                                    \
-        case 3: return FN<false, true, PHYS_SIMPLE_T>(__VA_ARGS__);                                    \
-        case 4: return FN<true, false, PHYS_BULLET_T>(__VA_ARGS__);                                    \
-        case 5: return FN<true, false, PHYS_SIMPLE_T>(__VA_ARGS__);                                    \
-        case 6: return FN<true, true, PHYS_BULLET_T>(__VA_ARGS__);                                     \
-        default: return FN<true, true, PHYS_SIMPLE_T>(__VA_ARGS__);                                    \
+        case 0: return FN<false, false, PHYS_BULLET_T, 0>(__VA_ARGS__);                                \
+        case 1: return FN<false, false, PHYS_SIMPLE_T, 0>(__VA_ARGS__);                                \
+        case 2: return FN<false, true, PHYS_BULLET_T, 0>(__VA_ARGS__);                                 \
+        case 3: return FN<false, true, PHYS_SIMPLE_T, 0>(__VA_ARGS__);                                 \
+        case 4: return FN<true, false, PHYS_BULLET_T, 0>(__VA_ARGS__);                                 \
+        case 5: return FN<true, false, PHYS_SIMPLE_T, 0>(__VA_ARGS__);                                 \
+        case 6: return FN<true, true, PHYS_BULLET_T, 0>(__VA_ARGS__);                                  \
+        default: return FN<true, true, PHYS_SIMPLE_T, 0>(__VA_ARGS__);                                 \
         }                                                                                              \
     } while (0)
 
