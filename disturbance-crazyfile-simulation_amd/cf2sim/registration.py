@@ -1,0 +1,129 @@
+"""Single-env gym-style adapter over the batched HIP env, with the reference's env ids.
+
+The reference registers its hover envs with gym (phoenix_drone_simulation/__init__.py:8-109,
+``max_episode_steps=500``) and callers do ``env = gym.make(id); obs = env.reset();
+obs, r, done, info = env.step(a)`` (tests/test_envs.py:96-123, algs/iwpg/iwpg.py:372-410).
+``make(id)`` returns an object with that API, backed by a 1-env ``BatchedCrazyflieEnv``:
+
+* ``reset() -> np.ndarray[obs_dim]`` float64 (the reference builds obs with numpy float64 ops)
+* ``step(a) -> (obs, float r, bool done, dict info)``, ``info`` = compute_info() keys
+  (``cost``, ``disturbance_level``) plus ``TimeLimit.truncated`` when gym's TimeLimit(500) ends
+  the episode (gym 0.19 TimeLimit semantics: done = terminal or truncated; no auto-reset)
+* ``observation_space`` Box(-1000, 1000, (34,), float32) / (42,) without noise, ``action_space``
+  Box(-1, 1, (4,), float32) (envs/base.py:139-148); ``metadata`` as envs/base.py:24
+* ``seed(s)`` re-seeds the Philox stream (the reference re-seeds numpy's global RNG)
+
+The physics plugin is chosen by name like the reference's ``physics=`` string
+(envs/base.py:223-231): 'PybulletPhysicsWithAdversary', 'PyBulletPhysics' (the Bullet
+restatement), 'SimplePhysics' (physics.py:127-200) and 'HipBatchedPhysics' (whatever the env id
+uses, run by the fused HIP kernel).  Unknown names fail like the reference's assert.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .config import ENV_SPECS, PHYS_BULLET, PHYS_SIMPLE, REFERENCE_IDS, spec_for_id
+
+PHYSICS_PLUGINS = {
+    "PybulletPhysicsWithAdversary": PHYS_BULLET,   # envs/physics.py:202
+    "PyBulletPhysics": PHYS_BULLET,                # envs/physics.py:79
+    "SimplePhysics": PHYS_SIMPLE,                  # envs/physics.py:127
+    "HipBatchedPhysics": None,                     # the env id's own physics, fused HIP kernel
+}
+
+
+class HipBatchedPhysics:
+    """Name-level stand-in for the reference's physics classes (envs/physics.py): the physics of
+    this framework is not a separate object but the fused env-step kernel, so selecting it by
+    name only picks the Bullet or Simple restatement the kernel runs."""
+    name = "HipBatchedPhysics"
+
+    @staticmethod
+    def resolve(physics: str | None, default: int) -> int:
+        if physics is None:
+            return default
+        if physics not in PHYSICS_PLUGINS:
+            raise AssertionError(f"Physics={physics} not found.")   # envs/base.py:224-225
+        p = PHYSICS_PLUGINS[physics]
+        return default if p is None else p
+
+
+# registered ids + the framework's extension ids (C2 const wind, C4 gust) of BASELINE.json
+registry = {s.registered_id: s for s in ENV_SPECS.values() if s.registered_id}
+
+
+class CrazyflieEnv:
+    metadata = {"render.modes": ["human", "rgb_array"]}   # envs/base.py:24
+    reward_range = (-float("inf"), float("inf"))
+
+    def __init__(self, env_id: str, seed: int = 0, device=None, physics: str | None = None, **env_kwargs):
+        from .vec_env import BatchedCrazyflieEnv
+        self.spec = spec_for_id(env_id)
+        self.env_id = env_id
+        self._kwargs = dict(env_kwargs)
+        self._device = device
+        self._physics = HipBatchedPhysics.resolve(physics, self.spec.physics)
+        self.max_episode_steps = int(self._kwargs.pop("max_episode_steps", 500))
+        self._cls = BatchedCrazyflieEnv
+        self._seed = int(seed)
+        self._make()
+
+    def _make(self):
+        from dataclasses import replace
+        spec = replace(self.spec, physics=self._physics)
+        # TimeLimit is applied here (as gym's wrapper does), the kernel only sees terminal states
+        self._env = self._cls(spec.registered_id or self.env_id, 1, seed=self._seed, device=self._device,
+                              auto_reset=False, max_episode_steps=0, _spec=spec, **self._kwargs)
+        self.observation_space = self._env.observation_space
+        self.action_space = self._env.action_space
+        self._t = 0
+        self._needs_reset = True
+
+    @property
+    def disturbance_level(self) -> float:        # read by iwpg.py:408
+        return float(self._env.level[0].item())
+
+    def seed(self, seed=None):
+        self._seed = int(seed) if seed is not None else 0
+        self._env.close()
+        self._make()
+        return [self._seed]
+
+    def reset(self) -> np.ndarray:
+        obs = self._env.reset()
+        self._t = 0
+        self._needs_reset = False
+        return obs[0].double().cpu().numpy()
+
+    def step(self, action):
+        import torch
+        if self._needs_reset:
+            raise RuntimeError("call reset() before step() (gym TimeLimit semantics)")
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, 4), device=self._env.device)
+        obs, rew, done, info = self._env.step(a)
+        self._t += 1
+        terminal = bool(done[0].item())
+        info_out = {"cost": float(info["cost"][0].item()),
+                    "disturbance_level": float(info["disturbance_level"][0].item())}
+        truncated = self._t >= self.max_episode_steps > 0
+        if truncated and not terminal:
+            info_out["TimeLimit.truncated"] = True
+        d = terminal or truncated
+        if d:
+            self._needs_reset = True
+        return obs[0].double().cpu().numpy(), float(rew[0].item()), d, info_out
+
+    def render(self, mode="human"):
+        raise NotImplementedError("rendering is outside the accelerated path (DESIGN.md 'Out of scope')")
+
+    def close(self):
+        self._env.close()
+
+
+def make(env_id: str, **kwargs) -> CrazyflieEnv:
+    """``gym.make(env_id)`` equivalent for the hover ids (REFERENCE_IDS) and the extension ids."""
+    spec_for_id(env_id)   # raises KeyError / NotImplementedError for unknown / out-of-scope ids
+    return CrazyflieEnv(env_id, **kwargs)
+
+
+__all__ = ["make", "registry", "CrazyflieEnv", "HipBatchedPhysics", "PHYSICS_PLUGINS", "REFERENCE_IDS"]

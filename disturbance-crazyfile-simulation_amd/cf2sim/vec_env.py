@@ -25,14 +25,14 @@ from .spaces import make_box
 class BatchedCrazyflieEnv:
     def __init__(self, env_id: str, num_envs: int, seed: int = 0, device=None, env_id_offset: int = 0,
                  auto_reset: bool = True, want_final_obs: bool = False, config: CF2Config | None = None,
-                 **env_kwargs):
+                 _spec=None, **env_kwargs):
         if not torch.cuda.is_available():
             raise _native.CF2Error("BatchedCrazyflieEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.env_id = env_id
-        self.spec = spec_for_id(env_id) if config is None else None
+        self.spec = (_spec if _spec is not None else spec_for_id(env_id)) if config is None else None
         self.cfg = config if config is not None else build_config(
-            env_id, num_envs, seed=seed, env_id_offset=env_id_offset, auto_reset=auto_reset, **env_kwargs)
+            self.spec, num_envs, seed=seed, env_id_offset=env_id_offset, auto_reset=auto_reset, **env_kwargs)
         self.num_envs = int(self.cfg.num_envs)
         self.obs_dim = obs_dim(self.cfg)
         self.lib = _native.load()
@@ -138,12 +138,9 @@ class BatchedCrazyflieEnv:
 
     def gather_observations(self, group=None) -> torch.Tensor:
         """RCCL all-gather of every rank's obs slab (optional policy-side exchange; the physics
-        itself needs no collective).  Returns [world * N, obs_dim]."""
-        import torch.distributed as dist
-        world = dist.get_world_size(group)
-        out = torch.empty(world * self.num_envs, self.obs_dim, dtype=self.obs.dtype, device=self.device)
-        dist.all_gather_into_tensor(out, self.obs, group=group)
-        return out
+        itself needs no collective).  Returns [sum of N over ranks, obs_dim] in rank order."""
+        from .dist import gather_rows
+        return gather_rows(self.obs, group)
 
 
 def hj_disturbance(V: torch.Tensor, states: torch.Tensor, level: float, cfg: CF2Config | None = None):

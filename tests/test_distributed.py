@@ -1,0 +1,86 @@
+"""N>1 path on CPU (gloo, world_size 2): sharding by global env id is rank-count invariant and the
+observation gather reassembles the single-process result.  The per-env computation here is the
+CPU restatement (oracle/) because this container has no GPU; the HIP kernel keys its Philox
+stream by the same global env id, which tests/test_gpu_parity.py checks against the same
+restatement, and bench.py runs the identical sharding on GPUs over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cf2sim.dist import shard_range
+
+ENV_ID = "DroneHoverBulletFreeEnvWithGust-v0"
+N_TOTAL, T, SEED = 37, 25, 11          # ragged: 19 + 18
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _actions(t):
+    rng = np.random.default_rng(1000 + t)
+    return rng.uniform(-1, 1, size=(N_TOTAL, 4)).astype(np.float32)
+
+
+def _single_process():
+    import oracle as O
+    from cf2sim.config import build_config
+    env = O.OracleEnv(build_config(ENV_ID, N_TOTAL, seed=SEED), precision="f64")
+    obs = [env.reset()]
+    rew = []
+    for t in range(T):
+        o, r, d, _ = env.step(_actions(t))
+        obs.append(o)
+        rew.append(r)
+    env.close()
+    return np.stack(obs), np.stack(rew)
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "disturbance-crazyfile-simulation_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from cf2sim.config import build_config
+    from cf2sim.dist import gather_rows, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, cnt = shard_range(N_TOTAL, rank, world)
+    env = O.OracleEnv(build_config(ENV_ID, cnt, seed=SEED, env_id_offset=off), precision="f64")
+    obs = [gather_rows(torch.from_numpy(env.reset()))]
+    rew = []
+    for t in range(T):
+        o, r, d, _ = env.step(_actions(t)[off:off + cnt])
+        obs.append(gather_rows(torch.from_numpy(o)))
+        rew.append(gather_rows(torch.from_numpy(r)))
+    env.close()
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "dist.npz"), obs=torch.stack(obs).numpy(), rew=torch.stack(rew).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for n, w in [(37, 2), (262144, 8), (5, 8), (8, 8)]:
+        spans = [shard_range(n, r, w) for r in range(w)]
+        assert sum(c for _, c in spans) == n
+        assert all(spans[r][0] + spans[r][1] == spans[r + 1][0] for r in range(w - 1))
+        assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+
+
+def test_two_rank_gloo_matches_single_process(tmp_path):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / "dist.npz")
+    ref_obs, ref_rew = _single_process()
+    np.testing.assert_array_equal(got["obs"], ref_obs)
+    np.testing.assert_array_equal(got["rew"], ref_rew)
