@@ -65,6 +65,13 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&out, sizeof(float) * NF * N));
     CHECK(hipMalloc(&obs, sizeof(float) * 34 * N));
     CHECK(hipMemset(in, 0, sizeof(float) * NF * N));
+    if (argc > 2) {   // calibration mode for the PMC byte counters: one known-byte pattern, few launches
+        run<0, 84, 72, NF, 34>("SoA    R84 W72 +obs34 (calib)", in, out, obs, N, 0);
+        CHECK(hipFree(in));
+        CHECK(hipFree(out));
+        CHECK(hipFree(obs));
+        return 0;
+    }
     const int spins[] = {0, 256, 1024};
     for (int s : spins) {
         run<0, 84, 72, NF, 0>("SoA    R84 W72", in, out, obs, N, s);

@@ -1,0 +1,45 @@
+"""Turn the PMC passes of tools/pmc_traffic.sh into per-launch HBM bytes of the step kernel.
+
+Calibration: membench's SoA kernel (R84 W72 + obs34, N=262144) moves a known number of bytes
+with the step kernel's access width (4 B per lane, 256 B per wave instruction; obs rows as
+8-B stores at a 136-B stride).  bytes/counter ratios from it convert the step kernel's FETCH_SIZE /
+WRITE_SIZE (KiB) into bytes.  Writes profiles/step_kernel_traffic.json for bench.py."""
+import csv, glob, json, os, sys
+
+out = sys.argv[1]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def mean_counter(d, name, kern):
+    v = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kern in row.get("Kernel_Name", "") and row["Counter_Name"] == name:
+                v.append(float(row["Counter_Value"]))
+    if not v:
+        raise SystemExit(f"no {name} samples for {kern} in {d}")
+    return sum(v) / len(v)
+
+
+N = 262144
+calib_rd = N * 4 * 84
+calib_wr = N * 4 * (72 + 34)
+c_f = mean_counter(os.path.join(out, "calib_FETCH_SIZE"), "FETCH_SIZE", "kern") * 1024
+c_w = mean_counter(os.path.join(out, "calib_WRITE_SIZE"), "WRITE_SIZE", "kern") * 1024
+s_f = mean_counter(os.path.join(out, "step_FETCH_SIZE"), "FETCH_SIZE", "step_kernel") * 1024
+s_w = mean_counter(os.path.join(out, "step_WRITE_SIZE"), "WRITE_SIZE", "step_kernel") * 1024
+kr, kw = calib_rd / c_f, calib_wr / c_w
+res = {
+    "workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}",
+    "hbm_bytes_per_launch": s_f * kr + s_w * kw,
+    "read_bytes_per_launch": s_f * kr,
+    "write_bytes_per_launch": s_w * kw,
+    "raw_FETCH_SIZE_bytes": s_f, "raw_WRITE_SIZE_bytes": s_w,
+    "calibration": {"kernel": "tools/membench.hip SoA R84 W72 +obs34 (4 B/lane)", "known_read_bytes": calib_rd,
+                    "known_write_bytes": calib_wr, "FETCH_SIZE_bytes": c_f, "WRITE_SIZE_bytes": c_w,
+                    "read_factor": kr, "write_factor": kw},
+    "note": "FETCH_SIZE/WRITE_SIZE count L2 memory-side requests; Infinity-Cache hits are counted "
+            "(MI355X_MICROARCH.md HBM section), so this is L2->fabric traffic.",
+}
+json.dump(res, open(os.path.join(out, "step_kernel_traffic.json"), "w"), indent=1)
+print(json.dumps(res, indent=1))
