@@ -245,7 +245,7 @@ int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* o
     if (!ctx || !act_dev || !obs_dev || !rew_dev || !done_dev) return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL && !dstb_dev) return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
-    if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
+    if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
     if (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
     StepIO io{ctx->sf, ctx->si, act_dev, dstb_dev, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev,
               final_obs_dev};

@@ -984,16 +984,50 @@ __device__ __forceinline__ KParams shape_view(const KParams& P) {
     return Q;
 }
 
+// ---- phase timeline instrumentation (tools/timeline.py; -DCF2_TIMING builds only) ----
+#ifdef CF2_TIMING
+__device__ uint64_t* g_cf2_timing;   // [waves][16]: 0 hw id, 1 realtime start, 2 realtime end, 3.. memtime stamps
+__device__ __forceinline__ uint64_t* timing_row() {
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    return g_cf2_timing ? g_cf2_timing + (size_t)wave * 16 : nullptr;
+}
+#define TSTAMP(k)                                                                              \
+    do {                                                                                       \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                      \
+        uint64_t* r_ = timing_row();                                                           \
+        const int first_ = __ffsll((unsigned long long)__builtin_amdgcn_read_exec()) - 1;      \
+        if (r_ && (int)(threadIdx.x & 63) == first_) r_[3 + (k)] = t_;                         \
+    } while (0)
+#define TREADY(...) asm volatile("" ::__VA_ARGS__)
+#else
+#define TSTAMP(k) do { } while (0)
+#define TREADY(...) do { } while (0)
+#endif
+
 // One env-step of env i (aggregate_phy_steps physics sub-steps, observation, reward, done);
 // returns whether the env finished and must be auto-reset.
+// What an auto-reset consumes from the finished episode (handed to the resetting lane in LDS, so
+// the reset issues no global load behind the step's store burst)
+struct ResetSeed {
+    float wb[3], bias[3], ou[4], level;
+    int level_idx;
+    uint32_t ctr;
+};
+enum { SEED_WORDS = 13 };
+
 template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i) {
+__device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
+                                         ResetSeed& rs) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     Env E;
-    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
+    // every state load is issued up front: on gfx9 vmcnt also counts stores, so a load issued
+    // after the state stores would wait for the whole store burst to drain
+    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, P.need_level || io.level != nullptr, /*with_hist=*/true);
     const uint32_t gid = P.gid_off + i;
     const float4 a4 = reinterpret_cast<const float4*>(io.act)[i];
+    TREADY("v"(E.p[0]), "v"(E.obs_prev[OL - 1]), "v"(E.hact[1][3]), "v"(E.K[3]), "v"(a4.w), "v"(E.rng));
+    TSTAMP(1);   // every state load has landed
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
     const Rng g{P.key0, P.key1, E.rng, gid, TAG_STEP};
     if (PHYS == PHYS_BULLET_T) {
@@ -1059,6 +1093,7 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     }
     default: break;
     }
+#pragma unroll 4
     for (int s = 0; s < P.agg; ++s) {
         float on[4];
         normals<4>(g, 1 + s, on);
@@ -1070,6 +1105,8 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
         compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy, P.held_persistent != 0);
     }
     float onx[17];
+    TREADY("v"(E.q[3]), "v"(E.lpf[2]));
+    TSTAMP(2);   // physics sub-steps done
     compute_observation<NOISE>(P, E, g, 8 + 8 * P.agg, (E.ep_step + 1) * P.agg, onx);
     // the physics state is final now (an auto-reset below overwrites it): store it early so
     // its registers free up before the epilogue
@@ -1086,16 +1123,29 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     if (io.cost) io.cost[i] = cost;
     if (io.level) io.level[i] = level_used;
     const bool do_reset = done && P.auto_reset;
-    load_hist<NOISE>(P, io.sf, i, E);
     {
         float o[OD];
         compute_history<NOISE>(P, E, onx, o);
-        float* dst = do_reset ? io.final_obs : io.obs;   // a reset env returns its reset obs
-        if (dst) write_obs<NOISE>(dst, i, o);
+        // the block's obs rows are staged in LDS and written out coalesced by the kernel; a
+        // reset env's row is overwritten there by its reset observation
+#pragma unroll
+        for (int k = 0; k < OD; k += 2)
+            *reinterpret_cast<float2*>(obs_row + k) = make_float2(o[k], o[k + 1]);
+        if (do_reset && io.final_obs) write_obs<NOISE>(io.final_obs, i, o);
+    }
+    if (do_reset) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { rs.wb[k] = E.wb[k]; rs.bias[k] = NOISE ? E.bias[k] : 0.0f; }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rs.ou[k] = E.ou[k];
+        rs.level = E.level;
+        rs.level_idx = E.level_idx;
+        rs.ctr = E.rng;
     }
     store_hist<NOISE>(P, io.sf, i, E);
     E.rng += 1;
     store_ints(P, io.si, i, E, false);
+    TSTAMP(3);   // epilogue issued
     return do_reset;
 }
 
@@ -1136,6 +1186,31 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
     store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
 }
 
+// Auto-reset of env i from a seed handed over in LDS; the reset observation goes to obs_row (LDS).
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
+                                             uint32_t i, const ResetSeed& rs, float* __restrict__ obs_row) {
+    constexpr int OD = NOISE ? 34 : 42;
+    Env E;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { E.wb[k] = rs.wb[k]; E.bias[k] = rs.bias[k]; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) E.ou[k] = rs.ou[k];
+    E.level = rs.level;
+    E.level_idx = rs.level_idx;
+    E.rng = rs.ctr;
+    float o[OD];
+    TSTAMP(6);
+    reset_env<NOISE, DR, PHYS>(P, E, P.gid_off + i, o);
+    TREADY("v"(o[OD - 1]), "v"(E.p[0]), "v"(E.K[3]));
+    TSTAMP(7);   // reset state + observation computed
+    E.rng = rs.ctr + 1;
+#pragma unroll
+    for (int k = 0; k < OD; k += 2) *reinterpret_cast<float2*>(obs_row + k) = make_float2(o[k], o[k + 1]);
+    store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
+    TSTAMP(8);   // reset stores issued
+}
+
 #ifndef CF2_STEP_MIN_WAVES
 #define CF2_STEP_MIN_WAVES 2   // waves per SIMD the register allocator must leave room for
 #endif
@@ -1146,32 +1221,92 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
 // scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
 // 4-byte field access for them).
 template <bool NOISE, bool DR, int PHYS, int SPEC>
-__global__ void __launch_bounds__(256, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
+#ifndef CF2_STEP_BLOCK
+#define CF2_STEP_BLOCK 256     // envs per block = auto-reset compaction group
+#endif
+__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
     const KParams P = shape_view<SPEC>(P0);
-    __shared__ uint32_t s_list[256];
+#ifdef CF2_TIMING
+    if (uint64_t* r = timing_row()) {
+        if ((threadIdx.x & 63) == 0) {
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // XCC_ID
+            r[0] = ((uint64_t)xcc << 32) | hw;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[3] = __builtin_amdgcn_s_memtime();
+        }
+    }
+#endif
+    constexpr int OD = NOISE ? 34 : 42;
+    constexpr uint32_t B = CF2_STEP_BLOCK;
+    __shared__ __align__(16) float s_obs[B * OD];          // the block's obs rows, global layout
+    __shared__ uint32_t s_seed[SEED_WORDS][B];             // reset seeds by queue position
+    __shared__ uint32_t s_list[B];                         // queue: block-local env index
     __shared__ uint32_t s_cnt;
-    if (P.auto_reset && threadIdx.x == 0) s_cnt = 0;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (threadIdx.x == 0) s_cnt = 0;
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
     bool do_reset = false;
-    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i);
-    if (!P.auto_reset) return;
-    __syncthreads();     // s_cnt initialised (and a fence for the state rows written above)
-    const uint64_t m = __ballot(do_reset);
-    if (m) {
-        const int lane = (int)(threadIdx.x & 63);
-        const int leader = __ffsll((unsigned long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
-        base = __shfl(base, leader);
-        if (do_reset) s_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+    ResetSeed rs;
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs);
+    if (P.auto_reset) {
+        __syncthreads();     // s_cnt initialised
+        const uint64_t m = __ballot(do_reset);
+        if (m) {
+            const int lane = (int)(threadIdx.x & 63);
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t pos = 0;
+            if (lane == leader) pos = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+            pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (do_reset) {
+                s_list[pos] = tid;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    s_seed[k][pos] = __float_as_uint(rs.wb[k]);
+                    s_seed[3 + k][pos] = __float_as_uint(rs.bias[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) s_seed[6 + k][pos] = __float_as_uint(rs.ou[k]);
+                s_seed[10][pos] = __float_as_uint(rs.level);
+                s_seed[11][pos] = (uint32_t)rs.level_idx;
+                s_seed[12][pos] = rs.ctr;
+            }
+        }
+        __syncthreads();
+        TSTAMP(4);   // block barrier passed
+        const uint32_t cnt = s_cnt;
+        for (uint32_t k = tid; k < cnt; k += B) {
+            const uint32_t t = s_list[k];
+            ResetSeed q;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(s_seed[c][k]); q.bias[c] = __uint_as_float(s_seed[3 + c][k]); }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(s_seed[6 + c][k]);
+            q.level = __uint_as_float(s_seed[10][k]);
+            q.level_idx = (int)s_seed[11][k];
+            q.ctr = s_seed[12][k];
+            reset_seeded<NOISE, DR, PHYS>(P, io.sf, io.si, base + t, q, s_obs + t * OD);
+        }
     }
     __syncthreads();
-    const uint32_t cnt = s_cnt;
-    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
-        const uint32_t j = s_list[k];
-        const uint32_t ctr = (uint32_t)io.si[(size_t)I_RNG * P.N + j] - 1u;   // the finished step's counter
-        reset_one<NOISE, DR, PHYS>(P, io.sf, io.si, j, io.obs, ctr);
+    // coalesced write of the block's obs rows (contiguous in global memory)
+    {
+        const uint32_t nvalid = P.N - base < B ? P.N - base : B;
+        float* dst = io.obs + (size_t)base * OD;
+        if (nvalid == B && (B * OD) % 4 == 0) {
+            const float4* src4 = reinterpret_cast<const float4*>(s_obs);
+            float4* dst4 = reinterpret_cast<float4*>(dst);
+            for (uint32_t k = tid; k < B * OD / 4; k += B) dst4[k] = src4[k];
+        } else {
+            const float2* src2 = reinterpret_cast<const float2*>(s_obs);
+            float2* dst2 = reinterpret_cast<float2*>(dst);
+            for (uint32_t k = tid; k < nvalid * OD / 2; k += B) dst2[k] = src2[k];
+        }
     }
+#ifdef CF2_TIMING
+    TSTAMP(5);   // resets done
+    if (uint64_t* r = timing_row())
+        if ((threadIdx.x & 63) == 0) r[2] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
@@ -1238,7 +1373,7 @@ __global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* _
 // ------------------------------------------------------------------------------------
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
-    const dim3 grid((P.N + 255) / 256), block(256);
+    const dim3 grid((P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK), block(CF2_STEP_BLOCK);
     hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, io);
     return hipGetLastError();
 }
@@ -1278,6 +1413,11 @@ static inline bool spec_default_shape(const KParams& P) {
         }                                                                                              \
     } while (0)
 
+#ifdef CF2_TIMING
+extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cf2_timing), &dev, sizeof(dev));
+}
+#endif
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
 hipError_t launch_reset(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s) {
     CF2_DISPATCH(launch_reset_t, P, sf, si, mask, obs, s);

@@ -184,8 +184,8 @@ int  cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables,
 /* Reset envs whose mask byte is non-zero (mask_dev NULL = all), write their obs rows. */
 int  cf2_reset(cf2_ctx* ctx, const uint8_t* mask_dev, float* obs_dev, void* stream);
 
-/* One env-step for all envs.  act_dev [N,4]; dstb_dev [N,3] (only for CF2_DSTB_EXTERNAL, else NULL);
- * obs_dev [N,obs_dim]; rew_dev [N]; done_dev [N] (terminal OR truncated, gym 4-tuple semantics);
+/* One env-step for all envs.  act_dev [N,4] (16-B aligned); dstb_dev [N,3] (only for CF2_DSTB_EXTERNAL,
+ * else NULL); obs_dev [N,obs_dim] (16-B aligned); rew_dev [N]; done_dev [N] (terminal OR truncated, gym 4-tuple semantics);
  * trunc_dev [N] (TimeLimit truncation, may be NULL); cost_dev [N] (may be NULL);
  * level_dev [N] disturbance level of the finished step (may be NULL);
  * final_obs_dev [N,obs_dim] pre-reset observation of envs that auto-reset this step (may be NULL). */
