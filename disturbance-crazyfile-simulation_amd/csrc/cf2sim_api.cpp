@@ -18,8 +18,7 @@ struct cf2_ctx {
     KParams P;
     KTables T;
     KTables* tab_dev = nullptr;
-    float* sf = nullptr;
-    int32_t* si = nullptr;
+    float* sf = nullptr;           // internal AoSoA state, state_bytes(N)
     int device = 0;
 };
 
@@ -179,13 +178,11 @@ int cf2_create(const cf2_config* cfg, cf2_ctx** out_ctx) {
     e = hipMalloc((void**)&ctx->tab_dev, sizeof(KTables));
     if (e == hipSuccess) e = hipMemcpy(ctx->tab_dev, &ctx->T, sizeof(KTables), hipMemcpyHostToDevice);
     ctx->P.tab = ctx->tab_dev;
-    if (e == hipSuccess) e = hipMalloc((void**)&ctx->sf, sizeof(float) * NF * N);
-    if (e == hipSuccess) e = hipMalloc((void**)&ctx->si, sizeof(int32_t) * NI * N);
-    if (e == hipSuccess) e = launch_init(ctx->P, ctx->sf, ctx->si, 0);
+    if (e == hipSuccess) e = hipMalloc((void**)&ctx->sf, state_bytes((uint32_t)N));
+    if (e == hipSuccess) e = launch_init(ctx->P, ctx->sf, 0);
     if (e == hipSuccess) e = hipStreamSynchronize(0);
     if (e != hipSuccess) {
         (void)hipFree(ctx->sf);
-        (void)hipFree(ctx->si);
         (void)hipFree(ctx->tab_dev);
         delete ctx;
         return hip_fail(e);
@@ -197,11 +194,9 @@ int cf2_create(const cf2_config* cfg, cf2_ctx** out_ctx) {
 int cf2_destroy(cf2_ctx* ctx) {
     if (!ctx) return CF2_ERR_INVALID_ARG;
     hipError_t e1 = hipFree(ctx->sf);
-    hipError_t e2 = hipFree(ctx->si);
     (void)hipFree(ctx->tab_dev);
     delete ctx;
     if (e1 != hipSuccess) return hip_fail(e1);
-    if (e2 != hipSuccess) return hip_fail(e2);
     return CF2_OK;
 }
 
@@ -235,7 +230,7 @@ int cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables, const i
 
 int cf2_reset(cf2_ctx* ctx, const uint8_t* mask_dev, float* obs_dev, void* stream) {
     if (!ctx) return CF2_ERR_INVALID_ARG;
-    const hipError_t e = launch_reset(ctx->P, ctx->sf, ctx->si, mask_dev, obs_dev, (hipStream_t)stream);
+    const hipError_t e = launch_reset(ctx->P, ctx->sf, mask_dev, obs_dev, (hipStream_t)stream);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
@@ -247,7 +242,7 @@ int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* o
     if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
     if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
     if (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
-    StepIO io{ctx->sf, ctx->si, act_dev, dstb_dev, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev,
+    StepIO io{ctx->sf, act_dev, dstb_dev, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev,
               final_obs_dev};
     const hipError_t e = launch_step(ctx->P, io, (hipStream_t)stream);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
@@ -267,21 +262,13 @@ int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_ele
 
 int cf2_get_state(const cf2_ctx* ctx, float* state_f_dev, int32_t* state_i_dev, void* stream) {
     if (!ctx || !state_f_dev || !state_i_dev) return CF2_ERR_INVALID_ARG;
-    const size_t N = ctx->cfg.num_envs;
-    hipError_t e = hipMemcpyAsync(state_f_dev, ctx->sf, sizeof(float) * NF * N, hipMemcpyDeviceToDevice,
-                                  (hipStream_t)stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(state_i_dev, ctx->si, sizeof(int32_t) * NI * N, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    const hipError_t e = launch_state_convert(ctx->P, ctx->sf, state_f_dev, state_i_dev, 1, (hipStream_t)stream);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
-
 int cf2_set_state(cf2_ctx* ctx, const float* state_f_dev, const int32_t* state_i_dev, void* stream) {
     if (!ctx || !state_f_dev || !state_i_dev) return CF2_ERR_INVALID_ARG;
-    const size_t N = ctx->cfg.num_envs;
-    hipError_t e = hipMemcpyAsync(ctx->sf, state_f_dev, sizeof(float) * NF * N, hipMemcpyDeviceToDevice,
-                                  (hipStream_t)stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(ctx->si, state_i_dev, sizeof(int32_t) * NI * N, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    const hipError_t e = launch_state_convert(ctx->P, ctx->sf, const_cast<float*>(state_f_dev),
+                                              const_cast<int32_t*>(state_i_dev), 0, (hipStream_t)stream);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 

@@ -36,6 +36,34 @@ enum : int {
     NI = 5
 };
 enum { NUM_PARAMS = 19 };
+
+// ---- internal state layout (what the kernels read and write) ----
+// AoSoA of float4 groups: tiles of 64 envs (one wave); inside a tile, group g of lane l is the
+// 16 B at tile_base + g * 1024 + l * 16.  Every state access is a coalesced dwordx4 (1 KB per
+// wave instruction).  Int fields live in the same array as bit patterns.  Groups are arranged
+// so that a config touches whole groups: read-write state, read-only per-episode parameters and
+// optional fields never share a group.  The public snapshot format of cf2_get_state /
+// cf2_set_state stays the plain SoA above (F_* / I_* fields); conversion kernels map it.
+enum : int {
+    S_POS = 0, S_QUAT = 3, S_VEL = 7, S_OMEGA = 10,      // G0-G3 (always read + written)
+    S_EP = 13, S_RNG = 14, S_FLAGS = 15,                  //   ints in G3
+    S_MOTOR = 16,                                         // G4
+    S_OU = 20,                                            // G5
+    S_ABUF = 24,                                          // G6-G9, row r in G6+r
+    S_BIAS = 40, S_GUST = 43,                             // G10: gyro bias + gust_left (int)
+    S_LPF = 44,                                           // G11
+    S_RPY = 48,                                           // G12 (Simple physics)
+    S_DSTB = 52,                                          // G13
+    S_HACT = 56,                                          // G14-G15
+    S_OBSP = 64,                                          // G16-G20 (13 or 17 used)
+    S_HELD = 84,                                          // G21-G23 (held_persistent only)
+    S_PARAM = 96,                                         // G24-G28.z (19 DR params)
+    S_LEVEL = 115,                                        // G28.w
+    S_LEVEL_IDX = 116,                                    // G29.x (int)
+    NS = 120, NG = 30
+};
+__host__ __device__ constexpr uint32_t tiles_of(uint32_t n) { return (n + 63u) / 64u; }
+__host__ __device__ constexpr size_t state_bytes(uint32_t n) { return (size_t)tiles_of(n) * NG * 1024u; }
 enum { HJ_PTS = 15, HJ_TABLE = 11390625 };
 enum { PHYS_BULLET_T = 0, PHYS_SIMPLE_T = 1 };
 enum { DSTB_NONE_T = 0, DSTB_EXTERNAL_T = 1, DSTB_UNIFORM_T = 2, DSTB_CONST_T = 3, DSTB_GUST_T = 4, DSTB_HJ_T = 5 };
@@ -72,8 +100,7 @@ struct KTables {
 };
 
 struct StepIO {
-    float* sf;
-    int32_t* si;
+    float* sf;          // internal AoSoA state (state_bytes(N))
     const float* act;
     const float* dstb;
     float* obs;
@@ -86,8 +113,11 @@ struct StepIO {
 };
 
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
-hipError_t launch_reset(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s);
-hipError_t launch_init(const KParams& P, float* sf, int32_t* si, hipStream_t s);
+hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s);
+hipError_t launch_init(const KParams& P, float* sf, hipStream_t s);
+// public SoA snapshot <-> internal AoSoA (to_public = 1: internal -> state_f/state_i)
+hipError_t launch_state_convert(const KParams& P, float* sf, float* state_f, int32_t* state_i, int to_public,
+                                hipStream_t s);
 hipError_t launch_hj(const KParams& P, const float* V, const float* states, uint32_t n, float level, float* dstb,
                      float* uopt, hipStream_t s);
 

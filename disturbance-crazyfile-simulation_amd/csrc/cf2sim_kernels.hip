@@ -31,29 +31,53 @@ namespace cf2 {
 // ------------------------------------------------------------------------------------
 struct U4 { uint32_t x, y, z, w; };
 
-__device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                     uint32_t k0, uint32_t k1) {
+// Round keys k + r * (W0, W1), built once per kernel and held in VGPRs: as wave-uniform values
+// the compiler keeps them in SGPRs, where with the kernel's parameter block they spill (each
+// use then costs a v_readlane), and laundering them per block costs 18 SALU per block instead.
+struct Keys { uint32_t k0[10], k1[10]; };
+__device__ __forceinline__ Keys make_keys(uint32_t k0, uint32_t k1) {
+    Keys K;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }    // key schedule is wave-uniform: SALU
+        const uint32_t a = k0 + (uint32_t)r * 0x9E3779B9u, b = k1 + (uint32_t)r * 0xBB67AE85u;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(K.k0[r]) : "s"(a));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(K.k1[r]) : "s"(b));
+    }
+    return K;
+}
+
+__device__ __forceinline__ U4 philox(const Keys& K, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
         // one v_mad_u64_u32 per product yields both halves
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ K.k0[r], n2 = (uint32_t)(p0 >> 32) ^ c3 ^ K.k1[r];
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     }
     return U4{c0, c1, c2, c3};
 }
 
+// Random-word sources: Rng computes Philox blocks; TableRng reads blocks a whole block of
+// threads precomputed into LDS (auto-reset, see step_kernel).  Counter = (block, rng counter,
+// global env id, tag).
 struct Rng {
-    uint32_t k0, k1, ctr, gid, tag;
+    const Keys& K;
+    uint32_t ctr, gid, tag;
+    __device__ __forceinline__ U4 block(uint32_t b) const { return philox(K, b, ctr, gid, tag); }
+};
+
+// reset-time blocks (reset_env): 0-13 direct, sensor calls at 32-37 and 40-45
+enum { RESET_SLOTS = 26 };
+__host__ __device__ constexpr int reset_slot(uint32_t b) { return b < 14 ? (int)b : (b < 40 ? 14 + (int)b - 32 : 20 + (int)b - 40); }
+__host__ __device__ constexpr uint32_t reset_block_of_slot(int s) { return s < 14 ? (uint32_t)s : (s < 20 ? 32u + (uint32_t)(s - 14) : 40u + (uint32_t)(s - 20)); }
+
+struct TableRng {
+    const uint32_t* t;      // LDS: word w of slot s at t[(s * 4 + w) * stride]
+    uint32_t stride;
     __device__ __forceinline__ U4 block(uint32_t b) const {
-        // launder the key so its 10-round schedule is rebuilt per block on the SALU instead of
-        // being CSE'd into 20 SGPRs live across the kernel (spilled to VGPR lanes, re-read with
-        // one VALU v_readlane each)
-        uint32_t a = k0, c = k1;
-        asm volatile("" : "+s"(a), "+s"(c));
-        return philox(b, ctr, gid, tag, a, c);
+        const uint32_t* q = t + (size_t)reset_slot(b) * 4 * stride;
+        return U4{q[0], q[stride], q[2 * stride], q[3 * stride]};
     }
 };
 
@@ -70,8 +94,8 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, fl
 }
 
 // N normals from consecutive blocks starting at b0 (pair k uses u32 2k, 2k+1)
-template <int N>
-__device__ __forceinline__ void normals(const Rng& g, uint32_t b0, float (&z)[N]) {
+template <int N, class G>
+__device__ __forceinline__ void normals(const G& g, uint32_t b0, float (&z)[N]) {
 #pragma unroll
     for (int blk = 0; blk < (N + 3) / 4; ++blk) {
         const U4 u = g.block(b0 + blk);
@@ -90,8 +114,8 @@ __device__ __forceinline__ void normals(const Rng& g, uint32_t b0, float (&z)[N]
 // Normals LO..HI-1 of the sequence normals<N>(g, b0, .) would produce, drawing only the Philox
 // blocks and Box-Muller pairs that cover them (the stream positions of all other draws are
 // unchanged, so skipping dead draws is invisible to everything else).
-template <int LO, int HI>
-__device__ __forceinline__ void normals_range(const Rng& g, uint32_t b0, float* z) {
+template <int LO, int HI, class G>
+__device__ __forceinline__ void normals_range(const G& g, uint32_t b0, float* z) {
 #pragma unroll
     for (int blk = LO / 4; blk < (HI + 3) / 4; ++blk) {
         const U4 u = g.block(b0 + blk);
@@ -282,206 +306,190 @@ struct Env {
 };
 
 // ------------------------------------------------------------------------------------
-// SoA field access through buffer descriptors: one 32-bit VGPR offset (env * 4) serves every
-// field; the per-field base (field * N * 4) is a wave-uniform SGPR soffset.  With plain 64-bit
-// global addresses each field's address would occupy two VGPRs from its load to its store.
+// State access: AoSoA float4 groups through a buffer descriptor (cf2sim_internal.h, "internal
+// state layout").  One VGPR offset (tile base + lane * 16) serves every group; the group
+// offset g * 1024 is a constant the backend splits into the instruction's immediate offset
+// and a shared SGPR.  Every access is one coalesced dwordx4 per lane (1 KB per wave).
 // ------------------------------------------------------------------------------------
-struct SoA {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+struct F4 { float x, y, z, w; };
+__device__ __forceinline__ F4 f4(float x, float y, float z, float w) { return F4{x, y, z, w}; }
+__device__ __forceinline__ float ib(int v) { return __int_as_float(v); }       // int field -> slot bits
+__device__ __forceinline__ int bi(float v) { return __float_as_int(v); }
+
+struct Tile {
     __amdgpu_buffer_rsrc_t r;
-    uint32_t stride, voff;
-    __device__ __forceinline__ SoA(const void* base, uint32_t N, uint32_t nfields, uint32_t i)
-        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(N * 4u * nfields), 0x00020000)),
-          stride(N * 4u), voff(i * 4u) {}
-    // field * stride is recomputed per access (one s_mul_i32): a CSE'd per-field offset would be
-    // one more SGPR live from the load phase to the store phase, and the ~100 of them spill
-    __device__ __forceinline__ int fo(int f) const {
-        uint32_t s = stride;
-        asm volatile("" : "+s"(s));
-        return (int)((uint32_t)f * s);
+    uint32_t voff;
+    __device__ __forceinline__ Tile(const void* base, uint32_t N, uint32_t i)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(uint32_t)state_bytes(N), 0x00020000)),
+          voff((i >> 6) * (uint32_t)(NG * 1024) + (i & 63u) * 16u) {}
+    __device__ __forceinline__ F4 ld(int g) const {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + (uint32_t)g * 1024u), 0, 0);
+        return F4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
     }
-    __device__ __forceinline__ float ld(int f) const {
-        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, fo(f), 0));
-    }
-    __device__ __forceinline__ void st(int f, float v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, fo(f), 0);
-    }
-    __device__ __forceinline__ int ldi(int f) const {
-        return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, fo(f), 0);
-    }
-    __device__ __forceinline__ void sti(int f, int v) const {
-        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, (int)voff, fo(f), 0);
+    __device__ __forceinline__ void st(int g, F4 f) const {
+        const u32x4 v = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(voff + (uint32_t)g * 1024u), 0, 0);
     }
 };
 
-// o_{k-1} and the action history are consumed only by compute_history at the end of a step:
-// the step kernel loads them after the physics loop so they do not occupy registers across it.
+enum : int { G_CORE3 = 3, G_MOTOR = 4, G_OU = 5, G_ABUF = 6, G_BIAS = 10, G_LPF = 11, G_RPY = 12, G_DSTB = 13,
+             G_HACT = 14, G_OBSP = 16, G_HELD = 21, G_PARAM = 24, G_LEVEL_IDX = 29 };
+
+__device__ __forceinline__ bool gust_mode(const KParams& P) { return P.dstb_mode == DSTB_GUST_T; }
+__device__ __forceinline__ bool dstb_stored(const KParams& P) {
+    return P.dstb_mode == DSTB_CONST_T || P.dstb_mode == DSTB_GUST_T;
+}
+
 template <bool NOISE>
-__device__ __forceinline__ void load_hist(const KParams& P, const float* __restrict__ sf, uint32_t i, Env& E) {
-    const SoA S(sf, P.N, NF, i);
+__device__ __forceinline__ void load_hist(const Tile& T, Env& E) {
     constexpr int OL = NOISE ? 13 : 17;
+    const F4 h0 = T.ld(G_HACT), h1 = T.ld(G_HACT + 1);
+    E.hact[0][0] = h0.x; E.hact[0][1] = h0.y; E.hact[0][2] = h0.z; E.hact[0][3] = h0.w;
+    E.hact[1][0] = h1.x; E.hact[1][1] = h1.y; E.hact[1][2] = h1.z; E.hact[1][3] = h1.w;
 #pragma unroll
-    for (int k = 0; k < OL; ++k) E.obs_prev[k] = S.ld(F_OBS_PREV + k);
+    for (int g = 0; g < (OL + 3) / 4; ++g) {
+        const F4 o = T.ld(G_OBSP + g);
+        const float v[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) E.hact[s][k] = S.ld(F_HIST_ACT + 4 * s + k);
+        for (int k = 0; k < 4; ++k)
+            if (4 * g + k < OL) E.obs_prev[4 * g + k] = v[k];
+    }
 }
 
 template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void load_env(const KParams& P, const float* __restrict__ sf,
-                                         const int32_t* __restrict__ si, uint32_t i, Env& E, bool need_level = true,
-                                         bool with_hist = true) {
-    const SoA S(sf, P.N, NF, i), SI(si, P.N, NI, i);
-#define LD(f) S.ld(f)
+__device__ __forceinline__ void load_env(const KParams& P, const float* __restrict__ sf, uint32_t i, Env& E,
+                                         bool need_level = true, bool with_hist = true) {
+    const Tile T(sf, P.N, i);
+    const F4 g0 = T.ld(0), g1 = T.ld(1), g2 = T.ld(2), g3 = T.ld(3), gx = T.ld(G_MOTOR), go = T.ld(G_OU);
+    E.p[0] = g0.x; E.p[1] = g0.y; E.p[2] = g0.z; E.q[0] = g0.w;
+    E.q[1] = g1.x; E.q[2] = g1.y; E.q[3] = g1.z; E.v[0] = g1.w;
+    E.v[1] = g2.x; E.v[2] = g2.y; E.w[0] = g2.z; E.w[1] = g2.w;
+    E.w[2] = g3.x;
+    E.ep_step = bi(g3.y);
+    E.rng = (uint32_t)bi(g3.z);
+    const int fl = bi(g3.w);
+    E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
+    E.x[0] = gx.x; E.x[1] = gx.y; E.x[2] = gx.z; E.x[3] = gx.w;
+    E.ou[0] = go.x; E.ou[1] = go.y; E.ou[2] = go.z; E.ou[3] = go.w;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) E.p[k] = LD(F_POS + k);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) E.q[k] = LD(F_QUAT + k);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) E.v[k] = LD(F_VEL + k);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) E.w[k] = LD(F_OMEGA + k);
-    if (PHYS == PHYS_SIMPLE_T) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.rpy[k] = LD(F_RPY + k);
+    for (int r = 0; r < 4; ++r) {
+        F4 a = f4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (r < P.buf_size) a = T.ld(G_ABUF + r);
+        E.abuf[r][0] = a.x; E.abuf[r][1] = a.y; E.abuf[r][2] = a.z; E.abuf[r][3] = a.w;
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) E.x[k] = LD(F_MOTOR + k);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) E.ou[k] = LD(F_OU + k);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) E.abuf[r][k] = r < P.buf_size ? LD(F_ABUF + 4 * r + k) : 0.0f;
+    E.gust_left = 0;
+    if (NOISE || gust_mode(P)) {
+        const F4 b = T.ld(G_BIAS);
+        if (NOISE) { E.bias[0] = b.x; E.bias[1] = b.y; E.bias[2] = b.z; }
+        if (gust_mode(P)) E.gust_left = bi(b.w);
+    }
     if (NOISE) {
+        const F4 l = T.ld(G_LPF);
+        E.lpf[0] = l.x; E.lpf[1] = l.y; E.lpf[2] = l.z;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) E.bias[k] = LD(F_BIAS + k);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.lpf[k] = LD(F_LPF + k);
+        for (int k = 0; k < 10; ++k) E.held[k] = 0.0f;
         if (P.held_persistent) {
+            const F4 h0 = T.ld(G_HELD), h1 = T.ld(G_HELD + 1), h2 = T.ld(G_HELD + 2);
+            const float hv[12] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w, h2.x, h2.y, h2.z, h2.w};
 #pragma unroll
-            for (int k = 0; k < 10; ++k) E.held[k] = LD(F_HELD + k);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 10; ++k) E.held[k] = 0.0f;
+            for (int k = 0; k < 10; ++k) E.held[k] = hv[k];
         }
     }
-    if (with_hist) load_hist<NOISE>(P, sf, i, E);
+    if (PHYS == PHYS_SIMPLE_T) {
+        const F4 r = T.ld(G_RPY);
+        E.rpy[0] = r.x; E.rpy[1] = r.y; E.rpy[2] = r.z;
+    }
+    if (dstb_stored(P)) {
+        const F4 d = T.ld(G_DSTB);
+        E.dstb[0] = d.x; E.dstb[1] = d.y; E.dstb[2] = d.z;
+    } else {
+        E.dstb[0] = E.dstb[1] = E.dstb[2] = 0.0f;
+    }
+    if (with_hist) load_hist<NOISE>(T, E);
+    F4 lv = f4(0.0f, 0.0f, 0.0f, P.level_fixed);
     if (DR) {
-        E.dt = LD(F_PARAM + 0); E.m = LD(F_PARAM + 1);
-        E.J[0] = LD(F_PARAM + 2); E.J[1] = LD(F_PARAM + 3); E.J[2] = LD(F_PARAM + 4);
-        E.k0 = LD(F_PARAM + 5); E.k1 = LD(F_PARAM + 6);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { E.A[k] = LD(F_PARAM + 7 + k); E.B[k] = LD(F_PARAM + 11 + k); E.K[k] = LD(F_PARAM + 15 + k); }
+        const F4 p0 = T.ld(G_PARAM), p1 = T.ld(G_PARAM + 1), p2 = T.ld(G_PARAM + 2), p3 = T.ld(G_PARAM + 3);
+        lv = T.ld(G_PARAM + 4);
+        E.dt = p0.x; E.m = p0.y; E.J[0] = p0.z; E.J[1] = p0.w;
+        E.J[2] = p1.x; E.k0 = p1.y; E.k1 = p1.z; E.A[0] = p1.w;
+        E.A[1] = p2.x; E.A[2] = p2.y; E.A[3] = p2.z; E.B[0] = p2.w;
+        E.B[1] = p3.x; E.B[2] = p3.y; E.B[3] = p3.z; E.K[0] = p3.w;
+        E.K[1] = lv.x; E.K[2] = lv.y; E.K[3] = lv.z;
     } else {
         E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
         E.k0 = P.ft0; E.k1 = P.ft1;
 #pragma unroll
         for (int k = 0; k < 4; ++k) { E.A[k] = P.A; E.B[k] = P.B; E.K[k] = P.K; }
+        if (need_level) lv = T.ld(G_PARAM + 4);
     }
-    if (P.dstb_mode == DSTB_CONST_T || P.dstb_mode == DSTB_GUST_T) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.dstb[k] = LD(F_DSTB + k);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.dstb[k] = 0.0f;
-    }
-    E.level = need_level ? LD(F_LEVEL) : P.level_fixed;
-#undef LD
-    E.ep_step = SI.ldi(I_EP_STEP);
-    E.rng = (uint32_t)SI.ldi(I_RNG);
-    const int fl = SI.ldi(I_FLAGS);
-    E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
-    E.level_idx = need_level ? SI.ldi(I_LEVEL) : 0;
-    E.gust_left = P.dstb_mode == DSTB_GUST_T ? SI.ldi(I_GUST) : 0;
+    E.level = need_level ? lv.w : P.level_fixed;
+    E.level_idx = need_level ? bi(T.ld(G_LEVEL_IDX).x) : 0;
 }
 
-// state the physics sub-steps update (stored as soon as the last sub-step is done)
+// state the physics sub-steps update (stored as soon as the last sub-step is done; group 3,
+// which carries the counters, is stored with the history at the end of the step)
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
-    const SoA S(sf, P.N, NF, i);
-#define ST(f, val) S.st(f, val)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ST(F_POS + k, E.p[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ST(F_QUAT + k, E.q[k]);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ST(F_VEL + k, E.v[k]);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) ST(F_OMEGA + k, E.w[k]);
-    if (PHYS == PHYS_SIMPLE_T) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) ST(F_RPY + k, E.rpy[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ST(F_MOTOR + k, E.x[k]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ST(F_OU + k, E.ou[k]);
+    const Tile T(sf, P.N, i);
+    T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
+    T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
+    T.st(2, f4(E.v[1], E.v[2], E.w[0], E.w[1]));
+    T.st(G_MOTOR, f4(E.x[0], E.x[1], E.x[2], E.x[3]));
+    T.st(G_OU, f4(E.ou[0], E.ou[1], E.ou[2], E.ou[3]));
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) if (r < P.buf_size) ST(F_ABUF + 4 * r + k, E.abuf[r][k]);
+        if (r < P.buf_size) T.st(G_ABUF + r, f4(E.abuf[r][0], E.abuf[r][1], E.abuf[r][2], E.abuf[r][3]));
+    if (NOISE || gust_mode(P))
+        T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(E.gust_left)));
     if (NOISE) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) ST(F_BIAS + k, E.bias[k]);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) ST(F_LPF + k, E.lpf[k]);
+        T.st(G_LPF, f4(E.lpf[0], E.lpf[1], E.lpf[2], 0.0f));
         if (P.held_persistent) {
-#pragma unroll
-            for (int k = 0; k < 10; ++k) ST(F_HELD + k, E.held[k]);
+            T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
+            T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
+            T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
         }
     }
-    if (P.dstb_mode == DSTB_GUST_T) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) ST(F_DSTB + k, E.dstb[k]);
-    }
-#undef ST
+    if (PHYS == PHYS_SIMPLE_T) T.st(G_RPY, f4(E.rpy[0], E.rpy[1], E.rpy[2], 0.0f));
+    if (gust_mode(P)) T.st(G_DSTB, f4(E.dstb[0], E.dstb[1], E.dstb[2], 0.0f));
 }
 
+// end of the step: history, counters (group 3 with the last angular-rate component)
 template <bool NOISE>
-__device__ __forceinline__ void store_hist(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
-    const SoA S(sf, P.N, NF, i);
+__device__ __forceinline__ void store_tail(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
     constexpr int OL = NOISE ? 13 : 17;
+    const Tile T(sf, P.N, i);
+    T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
+    T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
 #pragma unroll
-    for (int k = 0; k < OL; ++k) S.st(F_OBS_PREV + k, E.obs_prev[k]);
+    for (int g = 0; g < (OL + 3) / 4; ++g) {
+        float v[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) S.st(F_HIST_ACT + 4 * s + k, E.hact[s][k]);
-}
-
-__device__ __forceinline__ void store_ints(const KParams& P, int32_t* __restrict__ si, uint32_t i, const Env& E,
-                                           bool with_level) {
-    const SoA SI(si, P.N, NI, i);
-    SI.sti(I_EP_STEP, E.ep_step);
-    SI.sti(I_RNG, (int32_t)E.rng);
-    SI.sti(I_FLAGS, (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6));
-    if (with_level) SI.sti(I_LEVEL, E.level_idx);
-    if (P.dstb_mode == DSTB_GUST_T) SI.sti(I_GUST, E.gust_left);
+        for (int k = 0; k < 4; ++k) v[k] = 4 * g + k < OL ? E.obs_prev[4 * g + k] : 0.0f;
+        T.st(G_OBSP + g, f4(v[0], v[1], v[2], v[3]));
+    }
+    const int fl = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6);
+    T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
 }
 
 // whole state (reset paths): core + history + per-episode parameters + counters
 template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
-                                          uint32_t i, const Env& E, bool params_dirty) {
-    const SoA S(sf, P.N, NF, i);
+__device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E,
+                                          bool params_dirty) {
+    const Tile T(sf, P.N, i);
     store_core<NOISE, DR, PHYS>(P, sf, i, E);
-    store_hist<NOISE>(P, sf, i, E);
-#define ST(f, val) S.st(f, val)
-    if (DR && params_dirty) {
-        ST(F_PARAM + 0, E.dt); ST(F_PARAM + 1, E.m);
-        ST(F_PARAM + 2, E.J[0]); ST(F_PARAM + 3, E.J[1]); ST(F_PARAM + 4, E.J[2]);
-        ST(F_PARAM + 5, E.k0); ST(F_PARAM + 6, E.k1);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { ST(F_PARAM + 7 + k, E.A[k]); ST(F_PARAM + 11 + k, E.B[k]); ST(F_PARAM + 15 + k, E.K[k]); }
+    store_tail<NOISE>(P, sf, i, E);
+    if (P.dstb_mode == DSTB_CONST_T && params_dirty) T.st(G_DSTB, f4(E.dstb[0], E.dstb[1], E.dstb[2], 0.0f));
+    if (params_dirty) {
+        if (DR) {
+            T.st(G_PARAM, f4(E.dt, E.m, E.J[0], E.J[1]));
+            T.st(G_PARAM + 1, f4(E.J[2], E.k0, E.k1, E.A[0]));
+            T.st(G_PARAM + 2, f4(E.A[1], E.A[2], E.A[3], E.B[0]));
+            T.st(G_PARAM + 3, f4(E.B[1], E.B[2], E.B[3], E.K[0]));
+        }
+        T.st(G_PARAM + 4, f4(E.K[1], E.K[2], E.K[3], E.level));
+        T.st(G_LEVEL_IDX, f4(ib(E.level_idx), 0.0f, 0.0f, 0.0f));
     }
-    if (P.dstb_mode == DSTB_CONST_T && params_dirty) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) ST(F_DSTB + k, E.dstb[k]);
-    }
-    if (params_dirty) ST(F_LEVEL, E.level);
-#undef ST
-    store_ints(P, si, i, E, params_dirty);
 }
 
 // ------------------------------------------------------------------------------------
@@ -684,8 +692,8 @@ __device__ __forceinline__ void omega_noise(const KParams& P, Env& E, const floa
 // need_held = false: the held measurement of this call is dead (it is overwritten by a later
 // full measurement before any observation is emitted), so a full measurement only advances the
 // gyro (bias walk + LPF) and draws just the gyro normals n[6..15) of its stream positions.
-template <bool NOISE>
-__device__ __forceinline__ void compute_observation(const KParams& P, Env& E, const Rng& g, uint32_t base,
+template <bool NOISE, class G>
+__device__ __forceinline__ void compute_observation(const KParams& P, Env& E, const G& g, uint32_t base,
                                                     int iteration, float* obs, bool need_held = true) {
     if (!NOISE) {
 #pragma unroll
@@ -837,9 +845,8 @@ __device__ __forceinline__ int boltzmann_index(const KParams& P, float u) {
 // ------------------------------------------------------------------------------------
 // reset (base.py:420-464 + task_specific_reset + apply_domain_randomization)
 // ------------------------------------------------------------------------------------
-template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void reset_env(const KParams& P, Env& E, uint32_t gid, float* out) {
-    Rng g{P.key0, P.key1, E.rng, gid, TAG_RESET};
+template <bool NOISE, bool DR, int PHYS, class G>
+__device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, float* out) {
     const U4 b0 = g.block(0), b1 = g.block(1), b2 = g.block(2), b3 = g.block(3);
     const uint32_t u[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
                             b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
@@ -1023,13 +1030,14 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     Env E;
     // every state load is issued up front: on gfx9 vmcnt also counts stores, so a load issued
     // after the state stores would wait for the whole store burst to drain
-    load_env<NOISE, DR, PHYS>(P, io.sf, io.si, i, E, P.need_level || io.level != nullptr, /*with_hist=*/true);
+    load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/true);
     const uint32_t gid = P.gid_off + i;
     const float4 a4 = reinterpret_cast<const float4*>(io.act)[i];
     TREADY("v"(E.p[0]), "v"(E.obs_prev[OL - 1]), "v"(E.hact[1][3]), "v"(E.K[3]), "v"(a4.w), "v"(E.rng));
     TSTAMP(1);   // every state load has landed
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-    const Rng g{P.key0, P.key1, E.rng, gid, TAG_STEP};
+    const Keys K = make_keys(P.key0, P.key1);
+    const Rng g{K, E.rng, gid, TAG_STEP};
     if (PHYS == PHYS_BULLET_T) {
         euler_from_quat(E.q, E.rpy);
         const M3 R = rotmat(E.q);
@@ -1142,9 +1150,8 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
         rs.level_idx = E.level_idx;
         rs.ctr = E.rng;
     }
-    store_hist<NOISE>(P, io.sf, i, E);
     E.rng += 1;
-    store_ints(P, io.si, i, E, false);
+    store_tail<NOISE>(P, io.sf, i, E);
     TSTAMP(3);   // epilogue issued
     return do_reset;
 }
@@ -1153,16 +1160,12 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
 // stale body rates for the gyro LPF, the never-reset gyro bias and OU state, the RNG counter
 // and the disturbance level), writes the reset observation row and the whole state.
 template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
-                                          uint32_t i, float* __restrict__ obs, uint32_t rng_ctr) {
+__device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ sf, uint32_t i, float* __restrict__ obs) {
     constexpr int OD = NOISE ? 34 : 42;
-    const SoA S(sf, P.N, NF, i), SI(si, P.N, NI, i);
+    const Tile T(sf, P.N, i);
     Env E;
-    float q[4], w[3];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[k] = S.ld(F_QUAT + k);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) w[k] = S.ld(F_OMEGA + k);
+    const F4 g0 = T.ld(0), g1 = T.ld(1), g2 = T.ld(2), g3 = T.ld(3), go = T.ld(G_OU);
+    const float q[4] = {g0.w, g1.x, g1.y, g1.z}, w[3] = {g2.z, g2.w, g3.x};
     if (PHYS == PHYS_BULLET_T) {
         const M3 R = rotmat(q);
         mtv(R, w, E.wb);
@@ -1171,25 +1174,27 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
         for (int k = 0; k < 3; ++k) E.wb[k] = w[k];
     }
     if (NOISE) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.bias[k] = S.ld(F_BIAS + k);
+        const F4 b = T.ld(G_BIAS);
+        E.bias[0] = b.x; E.bias[1] = b.y; E.bias[2] = b.z;
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) E.ou[k] = S.ld(F_OU + k);
+    E.ou[0] = go.x; E.ou[1] = go.y; E.ou[2] = go.z; E.ou[3] = go.w;
+    const uint32_t rng_ctr = (uint32_t)bi(g3.z);
     E.rng = rng_ctr;
-    E.level = S.ld(F_LEVEL);
-    E.level_idx = SI.ldi(I_LEVEL);
+    E.level = T.ld(G_PARAM + 4).w;
+    E.level_idx = bi(T.ld(G_LEVEL_IDX).x);
     float o[OD];
-    reset_env<NOISE, DR, PHYS>(P, E, P.gid_off + i, o);
+    const Keys K = make_keys(P.key0, P.key1);
+    const Rng g{K, rng_ctr, P.gid_off + i, TAG_RESET};
+    reset_env<NOISE, DR, PHYS>(P, E, g, o);
     E.rng = rng_ctr + 1;
     if (obs) write_obs<NOISE>(obs, i, o);
-    store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
+    store_env<NOISE, DR, PHYS>(P, sf, i, E, true);
 }
 
 // Auto-reset of env i from a seed handed over in LDS; the reset observation goes to obs_row (LDS).
 template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict__ sf, int32_t* __restrict__ si,
-                                             uint32_t i, const ResetSeed& rs, float* __restrict__ obs_row) {
+__device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict__ sf, uint32_t i, const ResetSeed& rs,
+                                             const TableRng& g, float* __restrict__ obs_row) {
     constexpr int OD = NOISE ? 34 : 42;
     Env E;
 #pragma unroll
@@ -1201,13 +1206,13 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
     E.rng = rs.ctr;
     float o[OD];
     TSTAMP(6);
-    reset_env<NOISE, DR, PHYS>(P, E, P.gid_off + i, o);
+    reset_env<NOISE, DR, PHYS>(P, E, g, o);
     TREADY("v"(o[OD - 1]), "v"(E.p[0]), "v"(E.K[3]));
     TSTAMP(7);   // reset state + observation computed
     E.rng = rs.ctr + 1;
 #pragma unroll
     for (int k = 0; k < OD; k += 2) *reinterpret_cast<float2*>(obs_row + k) = make_float2(o[k], o[k + 1]);
-    store_env<NOISE, DR, PHYS>(P, sf, si, i, E, true);
+    store_env<NOISE, DR, PHYS>(P, sf, i, E, true);
     TSTAMP(8);   // reset stores issued
 }
 
@@ -1242,6 +1247,8 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     __shared__ __align__(16) float s_obs[B * OD];          // the block's obs rows, global layout
     __shared__ uint32_t s_seed[SEED_WORDS][B];             // reset seeds by queue position
     __shared__ uint32_t s_list[B];                         // queue: block-local env index
+    constexpr uint32_t C = 32;                             // auto-resets per chunk
+    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
     const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
@@ -1274,20 +1281,41 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
         __syncthreads();
         TSTAMP(4);   // block barrier passed
         const uint32_t cnt = s_cnt;
-        for (uint32_t k = tid; k < cnt; k += B) {
-            const uint32_t t = s_list[k];
-            ResetSeed q;
+        // Resets run in chunks of C envs.  Their ~26 Philox blocks per env are drawn by every
+        // thread of the block in parallel into LDS; then one lane per env runs the reset math
+        // on the table.  (On one lane each, the draws made the reset tail, which every wave of
+        // the block waits for, about as long as the env-step itself.)
+        for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
+            const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
+            {
+                const Keys K = make_keys(P.key0, P.key1);
+                for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
+                    const uint32_t sl = w / nc, e = w - sl * nc, pos = c0 + e;
+                    const U4 u = philox(K, reset_block_of_slot((int)sl), s_seed[12][pos], P.gid_off + base + s_list[pos],
+                                        TAG_RESET);
+                    uint32_t* q = s_rand + sl * 4 * C + e;
+                    q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
+                }
+            }
+            __syncthreads();
+            if (tid < nc) {
+                const uint32_t pos = c0 + tid, t = s_list[pos];
+                ResetSeed q;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(s_seed[c][k]); q.bias[c] = __uint_as_float(s_seed[3 + c][k]); }
+                for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(s_seed[c][pos]); q.bias[c] = __uint_as_float(s_seed[3 + c][pos]); }
 #pragma unroll
-            for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(s_seed[6 + c][k]);
-            q.level = __uint_as_float(s_seed[10][k]);
-            q.level_idx = (int)s_seed[11][k];
-            q.ctr = s_seed[12][k];
-            reset_seeded<NOISE, DR, PHYS>(P, io.sf, io.si, base + t, q, s_obs + t * OD);
+                for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(s_seed[6 + c][pos]);
+                q.level = __uint_as_float(s_seed[10][pos]);
+                q.level_idx = (int)s_seed[11][pos];
+                q.ctr = s_seed[12][pos];
+                const TableRng tg{s_rand + tid, C};
+                reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD);
+            }
+            __syncthreads();     // the next chunk reuses s_rand
         }
+    } else {
+        __syncthreads();         // every obs row of the block is in LDS
     }
-    __syncthreads();
     // coalesced write of the block's obs rows (contiguous in global memory)
     {
         const uint32_t nvalid = P.N - base < B ? P.N - base : B;
@@ -1310,44 +1338,80 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 }
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
-__global__ void __launch_bounds__(256) reset_kernel(KParams P0, float* __restrict__ sf, int32_t* __restrict__ si,
+__global__ void __launch_bounds__(256) reset_kernel(KParams P0, float* __restrict__ sf,
                                                     const uint8_t* __restrict__ mask, float* __restrict__ obs) {
     const KParams P = shape_view<SPEC>(P0);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
     if (mask && !mask[i]) return;
-    reset_one<NOISE, DR, PHYS>(P, sf, si, i, obs, (uint32_t)si[(size_t)I_RNG * P.N + i]);
+    reset_one<NOISE, DR, PHYS>(P, sf, i, obs);
 }
 
 // initial (pre-reset) state: AgentBase defaults, nominal params
-__global__ void init_kernel(KParams P, float* __restrict__ sf, int32_t* __restrict__ si) {
+__global__ void init_kernel(KParams P, float* __restrict__ sf) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.N) return;
-    const uint32_t N = P.N;
-    for (int f = 0; f < NF; ++f) sf[(size_t)f * N + i] = 0.0f;
-    sf[(size_t)(F_POS + 2) * N + i] = 1.0f;
-    sf[(size_t)(F_QUAT + 3) * N + i] = 1.0f;
-    sf[(size_t)(F_PARAM + 0) * N + i] = P.time_step;
-    sf[(size_t)(F_PARAM + 1) * N + i] = P.mass;
-    sf[(size_t)(F_PARAM + 2) * N + i] = P.ixx;
-    sf[(size_t)(F_PARAM + 3) * N + i] = P.iyy;
-    sf[(size_t)(F_PARAM + 4) * N + i] = P.izz;
-    sf[(size_t)(F_PARAM + 5) * N + i] = P.ft0;
-    sf[(size_t)(F_PARAM + 6) * N + i] = P.ft1;
-    for (int k = 0; k < 4; ++k) {
-        sf[(size_t)(F_PARAM + 7 + k) * N + i] = P.A;
-        sf[(size_t)(F_PARAM + 11 + k) * N + i] = P.B;
-        sf[(size_t)(F_PARAM + 15 + k) * N + i] = P.K;
-    }
-    sf[(size_t)F_LEVEL * N + i] = P.level_fixed;
-    for (int f = 0; f < NI; ++f) si[(size_t)f * N + i] = 0;
+    const Tile T(sf, P.N, i);
+    const F4 z = f4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int g = 0; g < NG; ++g) T.st(g, z);
+    T.st(0, f4(0.0f, 0.0f, 1.0f, 0.0f));                 // pos (0, 0, 1), quat x
+    T.st(1, f4(0.0f, 0.0f, 1.0f, 0.0f));                 // quat (.., w = 1), vel x
+    T.st(G_PARAM, f4(P.time_step, P.mass, P.ixx, P.iyy));
+    T.st(G_PARAM + 1, f4(P.izz, P.ft0, P.ft1, P.A));
+    T.st(G_PARAM + 2, f4(P.A, P.A, P.A, P.B));
+    T.st(G_PARAM + 3, f4(P.B, P.B, P.B, P.K));
+    float level = P.level_fixed;
+    int li = 0;
     if (P.level_mode == LEVEL_BOLTZMANN_T) {
         // construction-time Boltzmann() draw (hover_free.py:488), rng counter 0xFFFFFFFF
-        const Rng g{P.key0, P.key1, 0xFFFFFFFFu, P.gid_off + i, TAG_RESET};
+        const Keys K = make_keys(P.key0, P.key1);
+        const Rng g{K, 0xFFFFFFFFu, P.gid_off + i, TAG_RESET};
         const U4 u = g.block(0);
-        const int li = boltzmann_index(P, u01(u.x));
-        si[(size_t)I_LEVEL * N + i] = li;
-        sf[(size_t)F_LEVEL * N + i] = P.tab->level_values[li];
+        li = boltzmann_index(P, u01(u.x));
+        level = P.tab->level_values[li];
+    }
+    T.st(G_PARAM + 4, f4(P.K, P.K, P.K, level));
+    T.st(G_LEVEL_IDX, f4(ib(li), 0.0f, 0.0f, 0.0f));
+}
+
+// public snapshot field -> internal slot (cf2sim_internal.h)
+__device__ __forceinline__ int pub_float_slot(int f) {
+    if (f < F_RPY) return f;                              // pos, quat, vel, omega: same slots
+    if (f < F_MOTOR) return S_RPY + (f - F_RPY);
+    if (f < F_LPF) return f;                              // motor, ou, abuf, bias: same slots
+    if (f < F_HELD) return S_LPF + (f - F_LPF);
+    if (f < F_OBS_PREV) return S_HELD + (f - F_HELD);
+    if (f < F_HIST_ACT) return S_OBSP + (f - F_OBS_PREV);
+    if (f < F_PARAM) return S_HACT + (f - F_HIST_ACT);
+    if (f < F_DSTB) return S_PARAM + (f - F_PARAM);
+    if (f < F_LEVEL) return S_DSTB + (f - F_DSTB);
+    return S_LEVEL;
+}
+__device__ __forceinline__ int pub_int_slot(int f) {
+    switch (f) {
+    case I_EP_STEP: return S_EP;
+    case I_RNG: return S_RNG;
+    case I_FLAGS: return S_FLAGS;
+    case I_LEVEL: return S_LEVEL_IDX;
+    default: return S_GUST;
+    }
+}
+__device__ __forceinline__ size_t slot_index(uint32_t i, int slot) {     // in floats
+    return (size_t)(i >> 6) * (NG * 256) + (size_t)(slot >> 2) * 256 + (i & 63u) * 4 + (slot & 3);
+}
+__global__ void state_convert_kernel(uint32_t N, float* __restrict__ sf, float* __restrict__ pf,
+                                     int32_t* __restrict__ pi, int to_public) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    for (int f = 0; f < NF; ++f) {
+        float* in = sf + slot_index(i, pub_float_slot(f));
+        if (to_public) pf[(size_t)f * N + i] = *in;
+        else *in = pf[(size_t)f * N + i];
+    }
+    for (int f = 0; f < NI; ++f) {
+        float* in = sf + slot_index(i, pub_int_slot(f));
+        if (to_public) pi[(size_t)f * N + i] = __float_as_int(*in);
+        else *in = __int_as_float(pi[(size_t)f * N + i]);
     }
 }
 
@@ -1378,9 +1442,9 @@ static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t 
     return hipGetLastError();
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
-static hipError_t launch_reset_t(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s) {
+static hipError_t launch_reset_t(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
-    hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, sf, si, mask, obs);
+    hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, sf, mask, obs);
     return hipGetLastError();
 }
 
@@ -1419,12 +1483,18 @@ extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
 }
 #endif
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
-hipError_t launch_reset(const KParams& P, float* sf, int32_t* si, const uint8_t* mask, float* obs, hipStream_t s) {
-    CF2_DISPATCH(launch_reset_t, P, sf, si, mask, obs, s);
+hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
+    CF2_DISPATCH(launch_reset_t, P, sf, mask, obs, s);
 }
-hipError_t launch_init(const KParams& P, float* sf, int32_t* si, hipStream_t s) {
+hipError_t launch_state_convert(const KParams& P, float* sf, float* state_f, int32_t* state_i, int to_public,
+                                hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
-    hipLaunchKernelGGL(init_kernel, grid, block, 0, s, P, sf, si);
+    hipLaunchKernelGGL(state_convert_kernel, grid, block, 0, s, P.N, sf, state_f, state_i, to_public);
+    return hipGetLastError();
+}
+hipError_t launch_init(const KParams& P, float* sf, hipStream_t s) {
+    const dim3 grid((P.N + 255) / 256), block(256);
+    hipLaunchKernelGGL(init_kernel, grid, block, 0, s, P, sf);
     return hipGetLastError();
 }
 hipError_t launch_hj(const KParams& P, const float* V, const float* states, uint32_t n, float level, float* dstb,
