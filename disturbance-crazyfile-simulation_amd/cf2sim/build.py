@@ -15,7 +15,8 @@ HEADERS = ["cf2sim_internal.h"]
 # ~1 ulp) and the hardware sin/cos/log are allowed: the kernel is compared against the fp32 and
 # fp64 CPU restatements with stated tolerances (tests/test_gpu_parity.py), not bitwise.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=fast",
-         "-fgpu-approx-transcendentals", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-pass-failed"]
+         "-fgpu-approx-transcendentals", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-pass-failed",
+         "-fno-slp-vectorize"]   # SLP-packed v_pk_* f32 ops need register-pair shuffles that cost more than they save
 
 
 def _hipcc() -> str:

@@ -162,7 +162,8 @@ __device__ __forceinline__ void mtv(const M3& R, const float v[3], float o[3]) {
     o[2] = R.m[2] * v[0] + R.m[5] * v[1] + R.m[8] * v[2];
 }
 __device__ __forceinline__ float norm3(const float v[3]) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
-__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+// clip(x, lo, hi) for lo <= hi as one v_med3_f32 (identical to the compare form for non-NaN x)
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 // Makes a register value opaque to the optimiser.  Used before data-dependent selects among
 // Env fields: otherwise InstCombine turns select(c, load p, load q) chains into a load of a
 // select of pointers, SROA can no longer promote the Env struct and it lands in scratch.
@@ -219,15 +220,17 @@ __device__ __forceinline__ void quat_from_euler(const float e[3], float q[4]) {
 __device__ __forceinline__ void euler_from_quat(const float q[4], float e[3]) {
     const float sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
     const float sarg = -2.0f * (q[0] * q[2] - q[3] * q[1]);
-    if (sarg <= -0.99999f) {
-        e[0] = 0.0f; e[1] = -0.5f * 3.141592653589793f; e[2] = 2.0f * atan2_fast(q[0], -q[1]);
-    } else if (sarg >= 0.99999f) {
-        e[0] = 0.0f; e[1] = 0.5f * 3.141592653589793f; e[2] = 2.0f * atan2_fast(-q[0], q[1]);
-    } else {
-        e[0] = atan2_fast(2.0f * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
-        e[1] = asin_fast(sarg);
-        e[2] = atan2_fast(2.0f * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
-    }
+    // branch-free form of the three cases (gimbal lock at sarg <= -0.99999 / >= 0.99999): the
+    // atan2 of the yaw takes case-selected arguments, so each function is evaluated once
+    const bool lo = sarg <= -0.99999f, hi = sarg >= 0.99999f, mid = !(lo || hi);
+    const float e0 = atan2_fast(2.0f * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+    const float e1 = asin_fast(fminf(fmaxf(sarg, -1.0f), 1.0f));
+    const float y2 = mid ? 2.0f * (q[0] * q[1] + q[3] * q[2]) : (lo ? q[0] : -q[0]);
+    const float x2 = mid ? squ + sqx - sqy - sqz : (lo ? -q[1] : q[1]);
+    const float e2 = atan2_fast(y2, x2);
+    e[0] = mid ? e0 : 0.0f;
+    e[1] = mid ? e1 : (lo ? -0.5f * 3.141592653589793f : 0.5f * 3.141592653589793f);
+    e[2] = mid ? e2 : 2.0f * e2;
 }
 __device__ __forceinline__ void quat2euler(const float q[4], float e[3]) {
     const float x = q[0], y = q[1], z = q[2], w = q[3];
@@ -625,15 +628,13 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
     for (int k = 0; k < 3; ++k) E.p[k] += dt * E.v[k];
     {
         float ang = norm3(E.w);
-        if (ang * dt > 0.7853981633974483f) ang = 0.7853981633974483f * rcp(dt);
+        ang = ang * dt > 0.7853981633974483f ? 0.7853981633974483f * rcp(dt) : ang;
         // half-angle h = ang*dt/2 <= pi/8 after the clamp: odd/even Taylor polynomials are exact to
         // fp32 there (truncation < 3e-13), cheaper and more accurate than the hardware sin/cos
         const float h = 0.5f * ang * dt, h2 = h * h;
         const float sin_h = h * (1.0f + h2 * (-1.6666667e-1f + h2 * (8.3333333e-3f + h2 * (-1.9841270e-4f + h2 * 2.7557319e-6f))));
         const float cw = 1.0f + h2 * (-0.5f + h2 * (4.1666668e-2f + h2 * (-1.3888889e-3f + h2 * (2.4801587e-5f - h2 * 2.7557319e-7f))));
-        float s;
-        if (ang < 0.001f) s = 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang;
-        else s = sin_h * rcp(ang);
+        const float s = ang < 0.001f ? 0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang : sin_h * rcp(ang);
         const float axs[3] = {E.w[0] * s, E.w[1] * s, E.w[2] * s};
         const float qx = E.q[0], qy = E.q[1], qz = E.q[2], qw = E.q[3];
         const float nx = cw * qx + axs[0] * qw + axs[1] * qz - axs[2] * qy;

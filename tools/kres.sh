@@ -3,7 +3,7 @@
 # usage: tools/kres.sh [extra hipcc flags...]
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -fgpu-approx-transcendentals \
-  -fno-hip-fp32-correctly-rounded-divide-sqrt -I "$ROOT/include" --cuda-device-only -c \
+  -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -I "$ROOT/include" --cuda-device-only -c \
   -Rpass-analysis=kernel-resource-usage "$@" "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_kernels.hip" \
   -o /tmp/kres.o 2>&1 | python3 -c '
 import re,sys
