@@ -1246,9 +1246,11 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     constexpr int OD = NOISE ? 34 : 42;
     constexpr uint32_t B = CF2_STEP_BLOCK;
     __shared__ __align__(16) float s_obs[B * OD];          // the block's obs rows, global layout
-    __shared__ uint32_t s_seed[SEED_WORDS][B];             // reset seeds by queue position
     __shared__ uint32_t s_list[B];                         // queue: block-local env index
-    constexpr uint32_t C = 32;                             // auto-resets per chunk
+#ifndef CF2_RESET_CHUNK
+#define CF2_RESET_CHUNK 32
+#endif
+    constexpr uint32_t C = CF2_RESET_CHUNK;                // auto-resets per chunk
     __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
     __shared__ uint32_t s_cnt;
     if (threadIdx.x == 0) s_cnt = 0;
@@ -1265,19 +1267,19 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
             uint32_t pos = 0;
             if (lane == leader) pos = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
             pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (do_reset) {
-                s_list[pos] = tid;
+            if (do_reset) s_list[pos] = tid;
+        }
+        // a resetting env's seed is parked in its own LDS obs row (its final obs is already in
+        // final_obs; the row is overwritten by the reset observation after the seed is read)
+        if (do_reset) {
+            uint32_t* row = reinterpret_cast<uint32_t*>(s_obs + tid * OD);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    s_seed[k][pos] = __float_as_uint(rs.wb[k]);
-                    s_seed[3 + k][pos] = __float_as_uint(rs.bias[k]);
-                }
+            for (int k = 0; k < 3; ++k) { row[k] = __float_as_uint(rs.wb[k]); row[3 + k] = __float_as_uint(rs.bias[k]); }
 #pragma unroll
-                for (int k = 0; k < 4; ++k) s_seed[6 + k][pos] = __float_as_uint(rs.ou[k]);
-                s_seed[10][pos] = __float_as_uint(rs.level);
-                s_seed[11][pos] = (uint32_t)rs.level_idx;
-                s_seed[12][pos] = rs.ctr;
-            }
+            for (int k = 0; k < 4; ++k) row[6 + k] = __float_as_uint(rs.ou[k]);
+            row[10] = __float_as_uint(rs.level);
+            row[11] = (uint32_t)rs.level_idx;
+            row[12] = rs.ctr;
         }
         __syncthreads();
         TSTAMP(4);   // block barrier passed
@@ -1292,8 +1294,9 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
                 const Keys K = make_keys(P.key0, P.key1);
                 for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
                     const uint32_t sl = w / nc, e = w - sl * nc, pos = c0 + e;
-                    const U4 u = philox(K, reset_block_of_slot((int)sl), s_seed[12][pos], P.gid_off + base + s_list[pos],
-                                        TAG_RESET);
+                    const uint32_t t = s_list[pos];
+                    const uint32_t ctr = reinterpret_cast<const uint32_t*>(s_obs + t * OD)[12];
+                    const U4 u = philox(K, reset_block_of_slot((int)sl), ctr, P.gid_off + base + t, TAG_RESET);
                     uint32_t* q = s_rand + sl * 4 * C + e;
                     q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
                 }
@@ -1301,14 +1304,15 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
             __syncthreads();
             if (tid < nc) {
                 const uint32_t pos = c0 + tid, t = s_list[pos];
+                const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
                 ResetSeed q;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(s_seed[c][pos]); q.bias[c] = __uint_as_float(s_seed[3 + c][pos]); }
+                for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(row[c]); q.bias[c] = __uint_as_float(row[3 + c]); }
 #pragma unroll
-                for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(s_seed[6 + c][pos]);
-                q.level = __uint_as_float(s_seed[10][pos]);
-                q.level_idx = (int)s_seed[11][pos];
-                q.ctr = s_seed[12][pos];
+                for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(row[6 + c]);
+                q.level = __uint_as_float(row[10]);
+                q.level_idx = (int)row[11];
+                q.ctr = row[12];
                 const TableRng tg{s_rand + tid, C};
                 reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD);
             }
