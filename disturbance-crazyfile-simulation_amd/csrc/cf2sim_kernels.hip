@@ -31,17 +31,21 @@ namespace cf2 {
 // ------------------------------------------------------------------------------------
 struct U4 { uint32_t x, y, z, w; };
 
-// Round keys k + r * (W0, W1), built once per kernel and held in VGPRs: as wave-uniform values
-// the compiler keeps them in SGPRs, where with the kernel's parameter block they spill (each
-// use then costs a v_readlane), and laundering them per block costs 18 SALU per block instead.
+// Round keys k + r * (W0, W1), built once per kernel.  Wave-uniform, so they live in SGPRs (an
+// SGPR operand of v_xor costs nothing); -DCF2_VGPR_KEYS holds them in VGPRs instead, for kernels
+// whose SGPR budget is exhausted (each spilled SGPR use costs a v_readlane).
 struct Keys { uint32_t k0[10], k1[10]; };
 __device__ __forceinline__ Keys make_keys(uint32_t k0, uint32_t k1) {
     Keys K;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint32_t a = k0 + (uint32_t)r * 0x9E3779B9u, b = k1 + (uint32_t)r * 0xBB67AE85u;
+#ifdef CF2_VGPR_KEYS
         asm volatile("v_mov_b32 %0, %1" : "=v"(K.k0[r]) : "s"(a));
         asm volatile("v_mov_b32 %0, %1" : "=v"(K.k1[r]) : "s"(b));
+#else
+        K.k0[r] = a; K.k1[r] = b;
+#endif
     }
     return K;
 }
@@ -1218,7 +1222,7 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
 }
 
 #ifndef CF2_STEP_MIN_WAVES
-#define CF2_STEP_MIN_WAVES 2   // waves per SIMD the register allocator must leave room for
+#define CF2_STEP_MIN_WAVES 3   // waves per SIMD: <= 168 VGPRs (and <= 53 KB LDS per block)
 #endif
 // Step kernel: one lane per env.  Auto-reset is compacted per block: with random actions a few
 // % of envs finish per step, so nearly every wave would hold one and run the whole reset path
