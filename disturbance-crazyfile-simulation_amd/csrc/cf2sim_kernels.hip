@@ -50,9 +50,12 @@ __device__ __forceinline__ Keys make_keys(uint32_t k0, uint32_t k1) {
     return K;
 }
 
+#ifndef CF2_PHILOX_ROUNDS
+#define CF2_PHILOX_ROUNDS 10   // diagnostic knob only: the stream (and parity) is defined for 10
+#endif
 __device__ __forceinline__ U4 philox(const Keys& K, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < CF2_PHILOX_ROUNDS; ++r) {
         // one v_mad_u64_u32 per product yields both halves
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
