@@ -23,47 +23,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "cf2sim_internal.h"
+#include "cf2sim_rng.h"
 
 namespace cf2 {
-
-// ------------------------------------------------------------------------------------
-// Philox4x32-10 counter RNG (same stream as oracle/cf2_oracle.c)
-// ------------------------------------------------------------------------------------
-struct U4 { uint32_t x, y, z, w; };
-
-// Round keys k + r * (W0, W1), built once per kernel.  Wave-uniform, so they live in SGPRs (an
-// SGPR operand of v_xor costs nothing); -DCF2_VGPR_KEYS holds them in VGPRs instead, for kernels
-// whose SGPR budget is exhausted (each spilled SGPR use costs a v_readlane).
-struct Keys { uint32_t k0[10], k1[10]; };
-__device__ __forceinline__ Keys make_keys(uint32_t k0, uint32_t k1) {
-    Keys K;
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t a = k0 + (uint32_t)r * 0x9E3779B9u, b = k1 + (uint32_t)r * 0xBB67AE85u;
-#ifdef CF2_VGPR_KEYS
-        asm volatile("v_mov_b32 %0, %1" : "=v"(K.k0[r]) : "s"(a));
-        asm volatile("v_mov_b32 %0, %1" : "=v"(K.k1[r]) : "s"(b));
-#else
-        K.k0[r] = a; K.k1[r] = b;
-#endif
-    }
-    return K;
-}
-
-#ifndef CF2_PHILOX_ROUNDS
-#define CF2_PHILOX_ROUNDS 10   // diagnostic knob only: the stream (and parity) is defined for 10
-#endif
-__device__ __forceinline__ U4 philox(const Keys& K, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-#pragma unroll
-    for (int r = 0; r < CF2_PHILOX_ROUNDS; ++r) {
-        // one v_mad_u64_u32 per product yields both halves
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ K.k0[r], n2 = (uint32_t)(p0 >> 32) ^ c3 ^ K.k1[r];
-        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
-    }
-    return U4{c0, c1, c2, c3};
-}
 
 // Random-word sources: Rng computes Philox blocks; TableRng reads blocks a whole block of
 // threads precomputed into LDS (auto-reset, see step_kernel).  Counter = (block, rng counter,
@@ -87,18 +49,6 @@ struct TableRng {
         return U4{q[0], q[stride], q[2 * stride], q[3 * stride]};
     }
 };
-
-__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
-
-// Box-Muller on the hardware transcendental unit: v_log_f32 is log2, v_sin/v_cos_f32 take
-// their argument in revolutions, so sin(2 pi u2) needs no range reduction at all.
-__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-    const float u1 = ((float)(a >> 8) + 1.0f) * 5.9604644775390625e-08f;
-    const float u2 = (float)(b >> 8) * 5.9604644775390625e-08f;
-    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln2 log2(u1)
-    z0 = r * __builtin_amdgcn_cosf(u2);
-    z1 = r * __builtin_amdgcn_sinf(u2);
-}
 
 // N normals from consecutive blocks starting at b0 (pair k uses u32 2k, 2k+1)
 template <int N, class G>

@@ -207,6 +207,24 @@ int  cf2_set_state(cf2_ctx* ctx, const float* state_f_dev, const int32_t* state_
 int  cf2_hj_disturbance(const cf2_config* cfg, const float* V_dev, const float* states_dev,
                         uint32_t n, float level, float* dstb_dev, float* uopt_dev, void* stream);
 
+/* ---- batched rollout caller ----
+ * Gaussian MLP actor-critic forward of the reference's PPO networks for a batch of observations,
+ * one fused launch: ActorCritic.step (algs/core.py:371-395), MLPGaussianActor (core.py:228-291)
+ * pi D->50->50->4 ReLU, MLPCritic D->64->64->1 tanh (algs/ppo/defaults.py:8-13).  fp32.
+ * weights_dev: cf2_policy_weights_count(D) floats (layout in csrc/cf2sim_policy.hip: input-major
+ * matrices, pi then v, log_std after the pi head); obs_dev [n, D] (D = 34 or 42, 16-B aligned);
+ * sample != 0: act = mu + exp(log_std) * eps, eps ~ N(0,1) from Philox keyed (seed,
+ * counter, row + row_offset); else act = mu.  Outputs act_dev [n,4] (16-B aligned), val_dev [n],
+ * logp_dev [n] (sum of Normal log-densities; may be NULL). */
+size_t cf2_policy_weights_count(uint32_t obs_dim);
+int  cf2_policy_forward(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
+                        uint64_t seed, uint32_t counter, uint32_t row_offset, int sample,
+                        float* act_dev, float* val_dev, float* logp_dev, void* stream);
+/* Value of the rows with mask_dev[r] != 0 only (time-out bootstraps V(final obs)); other rows of
+ * val_dev are left untouched. */
+int  cf2_value_forward_masked(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
+                              const uint8_t* mask_dev, float* val_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,9 +52,8 @@ def test_make_step_api(gpu, env_id):
     """tests/test_envs.py:96-123 of the reference, through make(): obs in the observation space,
     4-tuple step with float reward, bool done and a dict info carrying the cost signal."""
     env = R.make(env_id, seed=1)
-    if "WithAdversary" in env_id and "Random" not in env_id and "Without" not in env_id:
+    if env._env.cfg.disturbance == 5:                  # HJ adversary: bind a (synthetic) value table
         import torch
-        from cf2sim.vec_env import BatchedCrazyflieEnv  # noqa: F401
         V = torch.zeros(1, 15 ** 6, device=gpu)
         env._env.bind_hj_tables(V, [0] * int(env._env.cfg.num_levels))
     if env._env.cfg.disturbance == 1:                  # external dstb: not a single-env gym API

@@ -6,4 +6,5 @@ name=$1; shift
 mkdir -p "$ROOT/build_ab"
 cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=fast -fgpu-approx-transcendentals \
   -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -Wall -Wno-pass-failed -I "$ROOT/include" "$@" -o "$ROOT/build_ab/$name.so" \
-  "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_kernels.hip" "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_api.cpp"
+  "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_kernels.hip" "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_policy.hip" \
+  "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_api.cpp"
