@@ -131,6 +131,15 @@ class FusedActorCritic:
         return act, val, logp
 
     @torch.no_grad()
+    def step_into(self, obs: torch.Tensor, act: torch.Tensor, val: torch.Tensor, logp: torch.Tensor):
+        from . import _native
+        _native.check(self.lib.cf2_policy_forward(
+            self.w.data_ptr(), obs.shape[0], self.obs_dim, obs.data_ptr(), self.seed, self.counter & 0xFFFFFFFF, 0, 1,
+            act.data_ptr(), val.data_ptr(), logp.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream),
+            "cf2_policy_forward")
+        self.counter += 1
+
+    @torch.no_grad()
     def value_masked(self, obs: torch.Tensor, mask: torch.Tensor, out: torch.Tensor):
         from . import _native
         _native.check(self.lib.cf2_value_forward_masked(
@@ -165,6 +174,21 @@ def gae(rew, val, done, trunc, last_val, trunc_val, gamma: float = 0.99, lam: fl
         adv[t] = a
         nxt_adv, nxt_val = a, val[t]
     return adv, adv + val
+
+
+def gae_device(rew, val, done_u8, trunc_u8, last_val, trunc_val, gamma: float = 0.99, lam: float = 0.95):
+    """``gae`` as one HIP launch (cf2_gae): one thread per env scans T backward."""
+    from . import _native
+    T, n = rew.shape
+    adv = torch.empty_like(rew)
+    ret = torch.empty_like(rew)
+    lib = _native.load()
+    _native.check(lib.cf2_gae(T, n, rew.contiguous().data_ptr(), val.contiguous().data_ptr(),
+                              done_u8.contiguous().data_ptr(), trunc_u8.contiguous().data_ptr(),
+                              trunc_val.contiguous().data_ptr(), last_val.contiguous().data_ptr(), float(gamma),
+                              float(lam), adv.data_ptr(), ret.data_ptr(),
+                              torch.cuda.current_stream(rew.device).cuda_stream), "cf2_gae")
+    return adv, ret
 
 
 @dataclasses.dataclass
@@ -202,8 +226,24 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
     buf_tr = torch.empty(steps, n, dtype=torch.bool, device=dev)
     trunc_val = torch.zeros(steps, n, device=dev)
     fused = isinstance(ac, FusedActorCritic)
+    if fused:
+        # zero-copy: the policy and the env write straight into the rollout storage
+        obs_buf = torch.empty(steps + 1, n, d, device=dev)
+        obs_buf[0] = o
+        d8 = torch.empty(steps, n, dtype=torch.uint8, device=dev)
+        tr8 = torch.empty(steps, n, dtype=torch.uint8, device=dev)
+        fin = envs.final_obs
+        for t in range(steps):
+            ac.step_into(obs_buf[t], buf_a[t], buf_v[t], buf_lp[t])
+            envs.step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], final_obs_out=fin)
+            ac.value_masked(fin, tr8[t], trunc_val[t])              # V(final obs) of the time-outs only
+        o = obs_buf[steps]
+        last_val = ac.value(o)
+        adv, ret = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam)
+        buf_o, buf_d, buf_tr = obs_buf[:steps], d8.bool(), tr8.bool()
+        return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val)
     for t in range(steps):
-        a, v, lp = ac.step(o) if fused else ac.step(o, generator=generator)
+        a, v, lp = ac.step(o, generator=generator)
         buf_o[t] = o
         buf_a[t] = a
         buf_v[t] = v
@@ -212,13 +252,10 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         buf_r[t] = r
         buf_d[t] = dn.bool()
         buf_tr[t] = info["truncated"].bool()
-        if fused:       # V(final obs) of the time-outs only
-            ac.value_masked(info["final_obs"], info["truncated"], trunc_val[t])
-        else:
-            trunc_val[t] = ac.value(info["final_obs"])      # only read where truncated
+        trunc_val[t] = ac.value(info["final_obs"])      # only read where truncated
     last_val = ac.value(o)
     adv, ret = gae(buf_r, buf_v, buf_d, buf_tr, last_val, trunc_val, gamma, lam)
     return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val)
 
 
-__all__ = ["MLPActorCritic", "FusedActorCritic", "pack_policy_weights", "gae", "collect", "Rollout"]
+__all__ = ["MLPActorCritic", "FusedActorCritic", "pack_policy_weights", "gae", "gae_device", "collect", "Rollout"]

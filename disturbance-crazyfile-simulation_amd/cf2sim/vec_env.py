@@ -116,6 +116,19 @@ class BatchedCrazyflieEnv:
             info["final_obs"] = self.final_obs
         return self.obs, self.rew, self.done, info
 
+    def step_into(self, actions: torch.Tensor, obs_out: torch.Tensor, rew_out: torch.Tensor, done_out: torch.Tensor,
+                  trunc_out: torch.Tensor | None = None, cost_out: torch.Tensor | None = None,
+                  final_obs_out: torch.Tensor | None = None):
+        """step() writing straight into caller buffers (rollout storage); done/trunc are uint8."""
+        for t in (obs_out, rew_out, done_out, trunc_out, cost_out, final_obs_out):
+            if t is not None and (t.device != self.device or not t.is_contiguous()):
+                raise ValueError("output buffers must be contiguous tensors on the env's device")
+        if done_out.dtype != torch.uint8 or (trunc_out is not None and trunc_out.dtype != torch.uint8):
+            raise ValueError("done/trunc buffers are uint8")
+        _native.check(self.lib.cf2_step(
+            self._ctx, actions.data_ptr(), None, obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
+            _native.ptr(trunc_out), _native.ptr(cost_out), None, _native.ptr(final_obs_out), self.stream), "cf2_step")
+
     def step_raw(self, act_ptr: int, obs_ptr: int | None = None):
         """Launch one env-step with raw device pointers (benchmark / graph-capture helper)."""
         _native.check(self.lib.cf2_step(

@@ -225,6 +225,13 @@ int  cf2_policy_forward(const float* weights_dev, uint32_t n, uint32_t obs_dim, 
 int  cf2_value_forward_masked(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
                               const uint8_t* mask_dev, float* val_dev, void* stream);
 
+/* Batched GAE over [T, n] rollout buffers (algs/core.py:459-480 finish_path on every env's
+ * episode slices): done/trunc uint8 (terminal -> bootstrap 0, time-out -> trunc_val), the end of
+ * the buffer bootstraps last_val [n].  Outputs adv [T, n], ret = adv + val [T, n]. */
+int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev, const uint8_t* done_dev,
+             const uint8_t* trunc_dev, const float* trunc_val_dev, const float* last_val_dev, float gamma,
+             float lam, float* adv_dev, float* ret_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -166,3 +166,25 @@ def test_fused_value_masked_and_collect(gpu):
         ra, _ = reference_gae(rew[:, k], val[:, k], d[:, k], tr[:, k], trunc_val[:, k], last_val[k], 0.99, 0.95)
         np.testing.assert_allclose(ro.adv[:, k].double().cpu().numpy(), ra, rtol=1e-4, atol=1e-4)
     envs.close()
+
+
+@pytest.mark.gpu
+def test_gae_kernel_matches_reference(gpu):
+    from cf2sim.rollout import gae_device
+    rng = np.random.default_rng(7)
+    T, N = 29, 1000
+    rew = rng.normal(size=(T, N)).astype(np.float32)
+    val = rng.normal(size=(T, N)).astype(np.float32)
+    done = rng.random((T, N)) < 0.1
+    trunc = done & (rng.random((T, N)) < 0.4)
+    trunc_val = rng.normal(size=(T, N)).astype(np.float32)
+    last_val = rng.normal(size=N).astype(np.float32)
+    g = lambda x: torch.as_tensor(x, device=gpu)
+    adv, ret = gae_device(g(rew), g(val), g(done.astype(np.uint8)), g(trunc.astype(np.uint8)), g(last_val),
+                          g(trunc_val), 0.99, 0.95)
+    adv, ret = adv.cpu().numpy(), ret.cpu().numpy()
+    for k in range(0, N, 13):
+        ra, rr = reference_gae(rew[:, k].astype(np.float64), val[:, k].astype(np.float64), done[:, k], trunc[:, k],
+                               trunc_val[:, k].astype(np.float64), float(last_val[k]), 0.99, 0.95)
+        np.testing.assert_allclose(adv[:, k], ra, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(ret[:, k], rr, rtol=1e-4, atol=1e-4)
