@@ -1,6 +1,7 @@
 """In-tree build of libcf2sim.so with hipcc for gfx950 (no JIT cache: the .so travels with the repo)."""
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -26,20 +27,83 @@ def _hipcc() -> str:
     return h
 
 
+BUILD_DIR = os.path.join(PKG_DIR, "_build")
+
+
+def _digest(*parts: bytes) -> str:
+    h = hashlib.sha256()
+    for p in parts:
+        h.update(p)
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _read(path: str) -> bytes:
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def _headers_blob() -> bytes:
+    return b"".join(_read(os.path.join(SRC_DIR, h)) for h in HEADERS) + _read(os.path.join(INC_DIR, "cf2sim.h"))
+
+
+def _compile_flags():
+    return [f for f in FLAGS if f != "-shared"] + ["-c"]
+
+
+def _obj_key(src: str) -> str:
+    return _digest(" ".join(_compile_flags()).encode(), _read(os.path.join(SRC_DIR, src)), _headers_blob())
+
+
+def _lib_key() -> str:
+    return _digest(*[_obj_key(s).encode() for s in SOURCES])
+
+
+def _stamp(path: str) -> str | None:
+    try:
+        with open(path + ".stamp") as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
-        return False
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(SRC_DIR, s) for s in SOURCES + HEADERS] + [os.path.join(INC_DIR, "cf2sim.h")]
-    return all(os.path.getmtime(d) <= t for d in deps)
+    """Content-addressed (sources, headers, flags), not mtime-based: a copied tree (e.g. the GPU
+    box snapshot) with an already built library does not rebuild."""
+    return os.path.exists(LIB) and _stamp(LIB) == _lib_key()
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
-    cmd = [_hipcc(), *FLAGS, "-I", INC_DIR, "-o", LIB + ".tmp", *[os.path.join(SRC_DIR, s) for s in SOURCES]]
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    procs = []
+    objs = []
+    for src in SOURCES:      # one object per source, compiled in parallel, skipped when unchanged
+        obj = os.path.join(BUILD_DIR, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        key = _obj_key(src)
+        if not force and os.path.exists(obj) and _stamp(obj) == key:
+            continue
+        cmd = [_hipcc(), *_compile_flags(), "-I", INC_DIR, "-o", obj + ".tmp", os.path.join(SRC_DIR, src)]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((subprocess.Popen(cmd), obj, key))
+    failed = False
+    for p, obj, key in procs:
+        if p.wait() != 0:
+            failed = True
+            continue
+        os.replace(obj + ".tmp", obj)
+        with open(obj + ".stamp", "w") as f:
+            f.write(key)
+    if failed:
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    with open(LIB + ".stamp", "w") as f:
+        f.write(_lib_key())
     return LIB

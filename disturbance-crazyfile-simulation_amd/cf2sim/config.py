@@ -70,6 +70,8 @@ class CF2Config(ctypes.Structure):
         ("gust_onset_prob", _d), ("gust_max_level", _d), ("gust_duration", _i), ("num_levels", _i),
         ("level_values", _d * NUM_LEVELS_MAX), ("level_cdf", _d * NUM_LEVELS_MAX),
         ("hj_grid_min", _d * 6), ("hj_grid_dx", _d * 6), ("hj_grid_points", (_d * HJ_PTS) * 6),
+        ("num_drones", _i), ("downwash_on", _i), ("dw_coeff", _d * 3), ("prop_radius", _d),
+        ("formation_dx", _d), ("formation_dz", _d),
     ]
 
     def to_dict(self) -> dict:
@@ -162,6 +164,8 @@ class EnvSpec:
     initial_angle: float = np.pi / 6
     reset_rate_deg: float = 200.0    # DroneHover*EnvWithAdversaryInitial: deg2rad(300) (rpy_dot_limit)
     registered_id: str | None = None
+    num_drones: int = 1              # drones per env group (multi-drone extension, BASELINE config 5)
+    downwash: bool = False
 
 
 def _hover_specs():
@@ -192,21 +196,27 @@ def _hover_specs():
         # build-defined workloads of BASELINE.json (not reference classes)
         add(EnvSpec(prefix + "WithConstWind", mod, PHYS_BULLET, task, DSTB_CONST, disturbance_level=1.0, **adv))
         add(EnvSpec(prefix + "WithGust", mod, PHYS_BULLET, task, DSTB_GUST, disturbance_level=1.5, **adv))
+        if task == TASK_HOVER_FREE:   # position-free reward: formations need no per-drone target
+            # BASELINE config 5: 4-drone formations with downwash + the per-step stochastic torque
+            add(EnvSpec(prefix + "WithDownwash", mod, PHYS_BULLET, task, DSTB_UNIFORM, num_drones=4,
+                        downwash=True, **adv))
     for name in ("WithAdversary", "WithRandomHJAdversary", "WithoutAdversary", "WithRandomAdversary",
                  "WithAdversaryInitial", "WithCurriculumHJAdversary"):
         specs["DroneHoverBulletEnv" + name].registered_id = "DroneHoverBulletEnv" + name + "-v0"
     for name in ("WithoutAdversary", "WithAdversary", "WithRandomHJAdversary"):
         specs["DroneHoverBulletFreeEnv" + name].registered_id = "DroneHoverBulletFreeEnv" + name + "-v0"
-    for name in ("WithConstWind", "WithGust"):   # extensions, registered under their own ids
+    for name in ("WithConstWind", "WithGust", "WithDownwash"):   # extensions, under their own ids
         for prefix in ("DroneHoverBulletEnv", "DroneHoverBulletFreeEnv"):
-            specs[prefix + name].registered_id = prefix + name + "-v0"
+            if prefix + name in specs:
+                specs[prefix + name].registered_id = prefix + name + "-v0"
     return specs
 
 
 ENV_SPECS = _hover_specs()
 # the 12 hover ids of the reference registry (phoenix_drone_simulation/__init__.py:8-109)
+EXTENSION_KEYS = ("ConstWind", "Gust", "Downwash")
 REFERENCE_IDS = [s.registered_id for s in ENV_SPECS.values()
-                 if s.registered_id and "ConstWind" not in s.registered_id and "Gust" not in s.registered_id]
+                 if s.registered_id and not any(k in s.registered_id for k in EXTENSION_KEYS)]
 # registered by the reference but outside the accelerated hover path
 OUT_OF_SCOPE_IDS = ["DroneTakeOffSimpleEnv-v0", "DroneTakeOffBulletEnv-v0",
                     "DroneCircleSimpleEnv-v0", "DroneCircleBulletEnv-v0"]
@@ -388,6 +398,18 @@ def build_config(env_id_or_spec, num_envs: int, seed: int = 0, env_id_offset: in
         c.hj_grid_dx[d] = float(dx[d])
         for k in range(HJ_PTS):
             c.hj_grid_points[d][k] = float(points[d][k])
+    # multi-drone formation + downwash (extension; gym-pybullet-drones' _downwash formula with the
+    # URDF coefficients the reference parses but never uses, agents.py:251-257)
+    c.num_drones = int(kw.pop("num_drones", spec.num_drones))
+    c.downwash_on = int(bool(kw.pop("downwash", spec.downwash)))
+    c.dw_coeff[0], c.dw_coeff[1], c.dw_coeff[2] = robot.DW_COEFF_1, robot.DW_COEFF_2, robot.DW_COEFF_3
+    c.prop_radius = robot.PROP_RADIUS
+    c.formation_dx = float(kw.pop("formation_dx", 0.5))
+    c.formation_dz = float(kw.pop("formation_dz", 1.0))
+    if c.num_drones not in (1, 2, 4, 8):
+        raise ValueError("num_drones must be 1, 2, 4 or 8")
+    if c.num_envs % c.num_drones or c.env_id_offset % c.num_drones:
+        raise ValueError("num_envs and env_id_offset must be multiples of num_drones (whole formations)")
     if kw:
         raise TypeError(f"unsupported env kwargs: {sorted(kw)}")
     return c

@@ -41,6 +41,10 @@ static int validate(const cf2_config* c) {
     if (c->buf_size < 1 || c->buf_size > 4) return CF2_ERR_UNSUPPORTED;
     if (c->num_levels < 1 || c->num_levels > CF2_NUM_LEVELS_MAX) return CF2_ERR_INVALID_ARG;
     if (c->time_step <= 0.0 || c->mass <= 0.0) return CF2_ERR_INVALID_ARG;
+    const int M = c->num_drones > 0 ? c->num_drones : 1;
+    if (M != 1 && M != 2 && M != 4 && M != 8) return CF2_ERR_UNSUPPORTED;
+    if (c->num_envs % (uint32_t)M || c->env_id_offset % (uint32_t)M) return CF2_ERR_INVALID_ARG;
+    if (M > 1 && c->physics != CF2_PHYS_BULLET) return CF2_ERR_UNSUPPORTED;
     return CF2_OK;
 }
 
@@ -138,6 +142,12 @@ static void fill_params(const cf2_config* c, KParams& P) {
         P.umax_d[k] = c->dstb_umax[k];
         P.uni_hi[k] = c->dstb_uniform_hi[k];
     }
+    P.num_drones = c->num_drones > 0 ? c->num_drones : 1;
+    P.downwash_on = c->downwash_on;
+    for (int k = 0; k < 3; ++k) P.dw_coeff[k] = (float)c->dw_coeff[k];
+    P.prop_radius = (float)c->prop_radius;
+    P.formation_dx = (float)c->formation_dx;
+    P.formation_dz = (float)c->formation_dz;
     P.gust_p = (float)c->gust_onset_prob;
     P.gust_max = (float)c->gust_max_level;
     P.tab = nullptr;

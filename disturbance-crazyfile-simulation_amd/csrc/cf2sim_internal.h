@@ -86,6 +86,8 @@ struct KParams {
     float done_rp, done_rate_deg, done_zmin, cost_xy, cost_z, cost_rp, cost_vel, cost_rate;
     float level_fixed, umax[3], gust_p, gust_max;
     double umax_d[3], uni_hi[3];
+    int32_t num_drones, downwash_on;                  // multi-drone formations (f4)
+    float dw_coeff[3], prop_radius, formation_dx, formation_dz;
     const struct KTables* tab;   // device-resident lookup tables (dynamically indexed)
     const float* V;              // HJ value tables [num_tables][15^6]
 };

@@ -508,7 +508,7 @@ __device__ __forceinline__ void apply_action(const KParams& P, Env& E, const flo
 }
 
 __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const float a[4], const float d[3],
-                                               const float on[4], bool first_after_reset) {
+                                               const float on[4], bool first_after_reset, float dw = 0.0f) {
     float xprev[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) xprev[j] = E.x[j];
@@ -534,9 +534,10 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
     const float mp = P.prop_mass, Ip = P.prop_inertia, Lz = P.prop_z;
     const float mtot = E.m + 4.0f * mp;
     float Fw[3];
-    Fw[0] = R.m[2] * fsum + dragw[0];
-    Fw[1] = R.m[5] * fsum + dragw[1];
-    Fw[2] = R.m[8] * fsum + dragw[2] - P.g_world * mtot;
+    const float fz = fsum - dw;      // downwash of formation mates: -z of the body, at the COM
+    Fw[0] = R.m[2] * fz + dragw[0];
+    Fw[1] = R.m[5] * fz + dragw[1];
+    Fw[2] = R.m[8] * fz + dragw[2] - P.g_world * mtot;
     float wb[3], vb[3];
     mtv(R, E.w, wb);
     mtv(R, E.v, vb);
@@ -801,10 +802,38 @@ __device__ __forceinline__ int boltzmann_index(const KParams& P, float u) {
 }
 
 // ------------------------------------------------------------------------------------
+// multi-drone formations (no reference implementation): the drones of a
+// group are consecutive lanes of one wave, so mates' positions are wave shuffles
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void formation_offset(const KParams& P, uint32_t member, float off[3]) {
+    const int ncol = (P.num_drones + 1) / 2;
+    off[0] = P.num_drones > 1 ? ((float)(int)(member / 2) - (float)(ncol - 1) * 0.5f) * P.formation_dx : 0.0f;
+    off[1] = 0.0f;
+    off[2] = P.num_drones > 1 ? (float)(int)(member % 2) * P.formation_dz : 0.0f;
+}
+// gym-pybullet-drones BaseAviary._downwash summed over the mates above this drone
+__device__ __forceinline__ float downwash(const KParams& P, const float p[3], uint32_t member) {
+    float F = 0.0f;
+    for (int j = 0; j < P.num_drones; ++j) {
+        const float qx = __shfl(p[0], j, P.num_drones), qy = __shfl(p[1], j, P.num_drones),
+                    qz = __shfl(p[2], j, P.num_drones);
+        const float dz = qz - p[2], dx = qx - p[0], dy = qy - p[1];
+        const float dxy = __builtin_sqrtf(dx * dx + dy * dy);
+        if ((uint32_t)j != member && dz > 0.0f && dxy < 10.0f) {
+            const float rr = P.prop_radius * rcp(4.0f * dz);
+            const float alpha = P.dw_coeff[0] * rr * rr;
+            const float q = dxy * rcp(P.dw_coeff[1] * dz + P.dw_coeff[2]);
+            F += alpha * __builtin_amdgcn_exp2f(-0.72134752044448170f * q * q);   // exp(-q^2/2)
+        }
+    }
+    return F;
+}
+
+// ------------------------------------------------------------------------------------
 // reset (base.py:420-464 + task_specific_reset + apply_domain_randomization)
 // ------------------------------------------------------------------------------------
 template <bool NOISE, bool DR, int PHYS, class G>
-__device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, float* out) {
+__device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, uint32_t gid, float* out) {
     const U4 b0 = g.block(0), b1 = g.block(1), b2 = g.block(2), b3 = g.block(3);
     const uint32_t u[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
                             b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
@@ -818,6 +847,12 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) E.abuf[r][j] = 0.0f;
     float pos[3] = {P.init_xyz[0], P.init_xyz[1], P.init_xyz[2]};
+    if (P.num_drones > 1) {
+        float off[3];
+        formation_offset(P, gid % (uint32_t)P.num_drones, off);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pos[k] += off[k];
+    }
     float quat[4] = {0.0f, 0.0f, 0.0f, 1.0f};
     float vel[3] = {0.0f, 0.0f, 0.0f}, rate[3] = {0.0f, 0.0f, 0.0f};
     if (P.reset_dist) {
@@ -943,9 +978,10 @@ __device__ __forceinline__ void write_obs(float* __restrict__ dst, uint32_t i, c
 template <int SPEC>
 __device__ __forceinline__ KParams shape_view(const KParams& P) {
     KParams Q = P;
-    if (SPEC == 1) {
+    if (SPEC == 1 || SPEC == 2) {
         Q.agg = 2; Q.obs_rate = 2; Q.buf_size = 2; Q.use_latency = 1; Q.use_motor_dyn = 1; Q.held_persistent = 0;
     }
+    if (SPEC == 1) { Q.num_drones = 1; Q.downwash_on = 0; }   // single drones: formation code drops out
     return Q;
 }
 
@@ -1063,7 +1099,10 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     for (int s = 0; s < P.agg; ++s) {
         float on[4];
         normals<4>(g, 1 + s, on);
-        if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0);
+        float dw = 0.0f;
+        if (PHYS == PHYS_BULLET_T && P.num_drones > 1 && P.downwash_on)
+            dw = downwash(P, E.p, gid % (uint32_t)P.num_drones);   // mates' positions before this sub-step
+        if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0, dw);
         else simple_substep(P, E, a, on);
         float dummy[17];
         // a sub-step's held measurement reaches an observation only if the final measurement
@@ -1143,7 +1182,7 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
     float o[OD];
     const Keys K = make_keys(P.key0, P.key1);
     const Rng g{K, rng_ctr, P.gid_off + i, TAG_RESET};
-    reset_env<NOISE, DR, PHYS>(P, E, g, o);
+    reset_env<NOISE, DR, PHYS>(P, E, g, P.gid_off + i, o);
     E.rng = rng_ctr + 1;
     if (obs) write_obs<NOISE>(obs, i, o);
     store_env<NOISE, DR, PHYS>(P, sf, i, E, true);
@@ -1164,7 +1203,7 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
     E.rng = rs.ctr;
     float o[OD];
     TSTAMP(6);
-    reset_env<NOISE, DR, PHYS>(P, E, g, o);
+    reset_env<NOISE, DR, PHYS>(P, E, g, P.gid_off + i, o);
     TREADY("v"(o[OD - 1]), "v"(E.p[0]), "v"(E.K[3]));
     TSTAMP(7);   // reset state + observation computed
     E.rng = rs.ctr + 1;
@@ -1410,7 +1449,8 @@ static hipError_t launch_reset_t(const KParams& P, float* sf, const uint8_t* mas
     return hipGetLastError();
 }
 
-// SPEC 1 when the config has the reference-default Bullet env-step shape (see shape_view)
+// SPEC 1 when the config has the reference-default Bullet env-step shape (see shape_view), SPEC 2
+// for the same shape flown in multi-drone formations
 static inline bool spec_default_shape(const KParams& P) {
     return P.phys == PHYS_BULLET_T && P.agg == 2 && P.obs_rate == 2 && P.buf_size == 2 && P.use_latency &&
            P.use_motor_dyn;
@@ -1419,12 +1459,20 @@ static inline bool spec_default_shape(const KParams& P) {
 #define CF2_DISPATCH(FN, ...)                                                                          \
     do {                                                                                               \
         const int key = (P.noise ? 4 : 0) | (P.dr ? 2 : 0) | (P.phys == PHYS_SIMPLE_T ? 1 : 0);           \
-        if (spec_default_shape(P)) {                                                                   \
+        if (spec_default_shape(P) && P.num_drones == 1) {                                              \
             switch (key) {                                                                             \
             case 0: return FN<false, false, PHYS_BULLET_T, 1>(__VA_ARGS__);                            \
             case 2: return FN<false, true, PHYS_BULLET_T, 1>(__VA_ARGS__);                             \
             case 4: return FN<true, false, PHYS_BULLET_T, 1>(__VA_ARGS__);                             \
             default: return FN<true, true, PHYS_BULLET_T, 1>(__VA_ARGS__);                             \
+            }                                                                                          \
+        }                                                                                              \
+        if (spec_default_shape(P)) {                                                                   \
+            switch (key) {                                                                             \
+            case 0: return FN<false, false, PHYS_BULLET_T, 2>(__VA_ARGS__);                            \
+            case 2: return FN<false, true, PHYS_BULLET_T, 2>(__VA_ARGS__);                             \
+            case 4: return FN<true, false, PHYS_BULLET_T, 2>(__VA_ARGS__);                             \
+            default: return FN<true, true, PHYS_BULLET_T, 2>(__VA_ARGS__);                             \
             }                                                                                          \
         }                                                                                              \
         switch (key) {                                                                                 \

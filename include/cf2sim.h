@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 1
+#define CF2SIM_ABI_VERSION 2
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -148,6 +148,20 @@ typedef struct cf2_config {
     double hj_grid_min[6];         /* per-dim lower bounds (Grid.min)                */
     double hj_grid_dx[6];          /* Grid.dx                                       */
     double hj_grid_points[6][CF2_HJ_PTS]; /* np.linspace node values (Grid.grid_points) */
+
+    /* ---- multi-drone envs (BASELINE config 5; no reference code) ----
+     * num_drones consecutive envs form one env group of drones flying a formation: drone k sits at
+     * init_xyz + ((k/2 - (ceil(num_drones/2)-1)/2) * formation_dx, 0, (k%2) * formation_dz).
+     * downwash_on: each drone feels, from every drone j of its group above it (dz > 0, dxy < 10),
+     * the downwash force of gym-pybullet-drones BaseAviary._downwash with the URDF coefficients
+     * parsed but unused by the reference (agents.py:251-257):
+     *   F = dw_coeff_1 (prop_radius / (4 dz))^2 exp(-0.5 (dxy / (dw_coeff_2 dz + dw_coeff_3))^2)
+     * along -z of the body (LINK_FRAME), at the centre of mass.  Bullet physics only. */
+    int32_t num_drones;            /* 1 (default), 2, 4 or 8; num_envs and env_id_offset multiples of it */
+    int32_t downwash_on;
+    double dw_coeff[3];            /* 2267.18, 0.16, -0.11 */
+    double prop_radius;            /* 2.31348e-2 m */
+    double formation_dx, formation_dz;   /* 0.5 m, 1.0 m */
 } cf2_config;
 
 /* SoA layout descriptor returned by cf2_layout(): state_f[field*num_envs + env],

@@ -329,7 +329,7 @@ static void update_information(orc_env* E) {
  * prop links' own angular damping.  The zero-mass centre-of-mass link passes its wrench
  * straight to the base (invD = 0 guard in the ABA). */
 static void bullet_substep(const orc_ctx* X, orc_env* E, const REAL a[4], const REAL dstb[3],
-                           const REAL ou_n[4], int first_after_reset) {
+                           const REAL ou_n[4], int first_after_reset, REAL dw) {
     const cf2_config* c = &X->cfg;
     REAL xprev[4];
     for (int j = 0; j < 4; ++j) xprev[j] = E->x[j];
@@ -364,11 +364,13 @@ static void bullet_substep(const orc_ctx* X, orc_env* E, const REAL a[4], const 
     REAL mp = R(c->prop_mass), Ip = R(c->prop_inertia), Lz = R(c->prop_z);
     REAL mtot = E->m + R(4.0) * mp;
     REAL g = R(c->gravity_world);
-    /* world force */
+    /* world force; dw = downwash from formation mates (multi-drone extension), a force along -z
+     * of the body applied at the centre of mass (LINK_FRAME, posObj 0) */
     REAL Fw[3];
-    Fw[0] = Rm[2] * fsum + dragw[0];
-    Fw[1] = Rm[5] * fsum + dragw[1];
-    Fw[2] = Rm[8] * fsum + dragw[2] - g * mtot;
+    REAL fz = fsum - dw;
+    Fw[0] = Rm[2] * fz + dragw[0];
+    Fw[1] = Rm[5] * fz + dragw[1];
+    Fw[2] = Rm[8] * fz + dragw[2] - g * mtot;
 
     /* base spatial velocity in the base frame */
     REAL wb[3], vb[3];
@@ -621,6 +623,36 @@ static void set_level(const orc_ctx* X, orc_env* E, int idx) {
 
 /* DroneBaseEnv.reset base.py:420-464 with task_specific_reset hover_free.py:237-289,
  * apply_domain_randomization base.py:241-298; writes obs (obs_dim) */
+/* ---- multi-drone extension (no reference implementation) ---- */
+/* formation slot of drone k of a group of M: columns of 2, formation_dx apart in x, the second
+ * drone of a column formation_dz above the first */
+static void formation_offset(const cf2_config* c, uint32_t k, REAL off[3]) {
+    const int M = c->num_drones > 0 ? c->num_drones : 1;
+    const int ncol = (M + 1) / 2;
+    off[0] = ((REAL)(int)(k / 2) - (REAL)(ncol - 1) * R(0.5)) * R(c->formation_dx);
+    off[1] = R(0.0);
+    off[2] = (REAL)(int)(k % 2) * R(c->formation_dz);
+    if (M == 1) off[0] = off[2] = R(0.0);
+}
+/* gym-pybullet-drones BaseAviary._downwash, summed over the group's drones above drone n */
+REAL orc_downwash(const cf2_config* c, const REAL pn[3], const REAL (*pos)[3], int M, int self) {
+    REAL F = R(0.0);
+    for (int j = 0; j < M; ++j) {
+        if (j == self) continue;
+        const REAL dz = pos[j][2] - pn[2];
+        const REAL dx = pos[j][0] - pn[0], dy = pos[j][1] - pn[1];
+        const REAL dxy = RSQRT(dx * dx + dy * dy);
+        if (dz > R(0.0) && dxy < R(10.0)) {
+            const REAL rr = R(c->prop_radius) / (R(4.0) * dz);
+            const REAL alpha = R(c->dw_coeff[0]) * rr * rr;
+            const REAL beta = R(c->dw_coeff[1]) * dz + R(c->dw_coeff[2]);
+            const REAL q = dxy / beta;
+            F += alpha * REXP(R(-0.5) * q * q);
+        }
+    }
+    return F;
+}
+
 static void reset_env(orc_ctx* X, int i, REAL* obs) {
     const cf2_config* c = &X->cfg;
     orc_env* E = &X->e[i];
@@ -638,6 +670,11 @@ static void reset_env(orc_ctx* X, int i, REAL* obs) {
     for (int r = 0; r < 4; ++r) for (int j = 0; j < 4; ++j) E->abuf[r][j] = R(0.0);
     /* task_specific_reset */
     REAL pos[3] = {R(c->init_xyz[0]), R(c->init_xyz[1]), R(c->init_xyz[2])};
+    {
+        REAL off[3];
+        formation_offset(c, (c->env_id_offset + (uint32_t)i) % (uint32_t)(c->num_drones > 0 ? c->num_drones : 1), off);
+        for (int k = 0; k < 3; ++k) pos[k] += off[k];
+    }
     REAL quat[4] = {R(0.0), R(0.0), R(0.0), R(1.0)};
     REAL vel[3] = {R(0.0), R(0.0), R(0.0)}, rate[3] = {R(0.0), R(0.0), R(0.0)};
     if (c->enable_reset_distribution) {
@@ -842,23 +879,41 @@ void orc_step(void* h, const float* act, const double* dstb_ext, double* obs, do
     orc_ctx* X = (orc_ctx*)h;
     const cf2_config* c = &X->cfg;
     int ol = obs_len(c), od = 2 * (ol + 4);
-    for (int i = 0; i < X->n; ++i) {
-        orc_env* E = &X->e[i];
-        rng_t g = mk_rng(X, i, TAG_STEP);
-        REAL a[4];
-        for (int k = 0; k < 4; ++k) a[k] = R(act[(size_t)i * 4 + k]);
-        REAL level_used = E->level;
-        REAL d[3];
-        disturbance_for_step(X, i, &g, dstb_ext, d);
-        for (int s = 0; s < c->aggregate_phy_steps; ++s) {
-            REAL ou_n[4];
-            rng_normals(&g, 1 + (uint32_t)s, 4, ou_n);
-            if (c->physics == CF2_PHYS_BULLET) bullet_substep(X, E, a, d, ou_n, E->ep_step == 0 && s == 0);
-            else simple_substep(X, E, a, ou_n);
-            REAL dummy[17];
-            compute_observation(X, E, &g, 8 + 8 * (uint32_t)s, dummy);
-            E->iteration += 1;
+    const int M = c->num_drones > 0 ? c->num_drones : 1;
+    for (int g0 = 0; g0 < X->n; g0 += M) {
+      /* the drones of one formation advance their sub-steps in lock step: the downwash of sub-step
+       * s uses every mate's position before that sub-step (single drones: M = 1) */
+      REAL a_g[8][4], d_g[8][3], level_g[8];
+      rng_t g_g[8];
+      for (int m = 0; m < M; ++m) {
+        const int i = g0 + m;
+        g_g[m] = mk_rng(X, i, TAG_STEP);
+        for (int k = 0; k < 4; ++k) a_g[m][k] = R(act[(size_t)i * 4 + k]);
+        level_g[m] = X->e[i].level;
+        disturbance_for_step(X, i, &g_g[m], dstb_ext, d_g[m]);
+      }
+      for (int s = 0; s < c->aggregate_phy_steps; ++s) {
+        REAL pos[8][3];
+        for (int m = 0; m < M; ++m)
+          for (int k = 0; k < 3; ++k) pos[m][k] = X->e[g0 + m].p[k];
+        for (int m = 0; m < M; ++m) {
+          orc_env* E = &X->e[g0 + m];
+          const REAL dw = (M > 1 && c->downwash_on) ? orc_downwash(c, pos[m], (const REAL(*)[3])pos, M, m) : R(0.0);
+          REAL ou_n[4];
+          rng_normals(&g_g[m], 1 + (uint32_t)s, 4, ou_n);
+          if (c->physics == CF2_PHYS_BULLET) bullet_substep(X, E, a_g[m], d_g[m], ou_n, E->ep_step == 0 && s == 0, dw);
+          else simple_substep(X, E, a_g[m], ou_n);
+          REAL dummy[17];
+          compute_observation(X, E, &g_g[m], 8 + 8 * (uint32_t)s, dummy);
+          E->iteration += 1;
         }
+      }
+      for (int m = 0; m < M; ++m) {
+        const int i = g0 + m;
+        orc_env* E = &X->e[i];
+        rng_t g = g_g[m];
+        REAL* a = a_g[m];
+        const REAL level_used = level_g[m];
         REAL on[17], o[42];
         compute_observation(X, E, &g, 8 + 8 * (uint32_t)c->aggregate_phy_steps, on);
         compute_history(c, E, on, o);
@@ -880,6 +935,7 @@ void orc_step(void* h, const float* act, const double* dstb_ext, double* obs, do
         }
         E->rng_ctr += 1;
         if (obs) for (int k = 0; k < od; ++k) obs[(size_t)i * od + k] = (double)o[k];
+      }
     }
 }
 
@@ -1035,7 +1091,7 @@ void orc_t_bullet_substep(const cf2_config* cfg, double* st /* p3 q4 v3 ww3 x4 o
     REAL aa[4], dd[3], nn[4];
     for (int k = 0; k < 4; ++k) { aa[k] = R(a[k]); nn[k] = R(ou_n[k]); }
     for (int k = 0; k < 3; ++k) dd[k] = R(dstb[k]);
-    bullet_substep(&X, &E, aa, dd, nn, first_after_reset);
+    bullet_substep(&X, &E, aa, dd, nn, first_after_reset, R(0.0));
     for (int k = 0; k < 3; ++k) { st[k] = E.p[k]; st[7 + k] = E.v[k]; st[10 + k] = E.ww[k]; }
     for (int k = 0; k < 4; ++k) { st[3 + k] = E.q[k]; st[13 + k] = E.x[k]; st[17 + k] = E.ou[k]; }
     for (int r = 0; r < 2; ++r) for (int k = 0; k < 4; ++k) st[21 + 4 * r + k] = E.abuf[r][k];

@@ -63,6 +63,19 @@ class _Lib:
         return cls._cache[precision]
 
 
+def downwash(cfg, pn, positions, self_index, precision="f64"):
+    """orc_downwash: downwash force on drone `self_index` from the others of its group."""
+    lib = _Lib.get(precision)
+    fn = lib.orc_downwash
+    fn.restype = ctypes.c_double if precision == "f64" else ctypes.c_float
+    real = ctypes.c_double if precision == "f64" else ctypes.c_float
+    M = len(positions)
+    p = (real * 3)(*pn)
+    arr = (real * (3 * M))(*[float(x) for row in positions for x in row])
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    return float(fn(ctypes.byref(cfg), p, arr, M, int(self_index)))
+
+
 def philox(ctr, key, precision="f64"):
     lib = _Lib.get(precision)
     c = (ctypes.c_uint32 * 4)(*[int(x) & 0xFFFFFFFF for x in ctr])

@@ -227,3 +227,15 @@ def test_hj_adversary_env_matches_restatement(gpu, env_id):
         ro, rr, rd, ri = ref.step(a)
         assert np.abs(go.cpu().numpy() - ro).max() < 5e-4
         np.testing.assert_allclose(gi["disturbance_level"].cpu().numpy(), ri["level"], atol=1e-6)
+
+
+@pytest.mark.parametrize("kw", [{}, dict(latency=0.02)])      # SPEC 2 (default shape) and the generic path
+def test_downwash_formations_match_restatement(gpu, kw):
+    """4-drone formations with downwash (f4).  The downwash force is a Gaussian in the horizontal
+    offset with a 5 cm width (beta = 0.16 dz - 0.11 at dz = 1 m), so ulp-level differences
+    (FMA contraction, v_rcp / v_exp) are amplified chaotically: the horizon is 25 env-steps,
+    within which the trajectories must agree to the same 5e-4 as the single-drone cases."""
+    errs, dmis, rew_err, (gsf, gsi), (rsf, rsi) = _run_pair("DroneHoverBulletFreeEnvWithDownwash-v0", kw, 512, 25, "f32")
+    assert errs[0] < 2e-5, f"reset observation {errs[0]}"
+    assert errs.max() < 5e-4, f"obs max err {errs.max()} {errs}"
+    assert dmis == 0
