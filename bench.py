@@ -55,6 +55,21 @@ def algorithmic_bytes_per_env_step(cfg, outputs=("obs", "rew", "done")) -> int:
     return b + sum(per_out[o] for o in outputs)
 
 
+def describe(cfg) -> str:
+    """Human-readable workload summary of a cf2_config (bench config string)."""
+    dstb = {0: "no disturbance", 1: "external disturbance", 2: "per-step uniform torque (C3)",
+            3: "const wind (C2)", 4: "gust (C4)", 5: "HJ value-table disturbance"}[int(cfg.disturbance)]
+    parts = [dstb]
+    if cfg.num_drones > 1:
+        parts.append(f"{cfg.num_drones}-drone formations{' with downwash (C5)' if cfg.downwash_on else ''}")
+    parts.append("sensor noise" if cfg.observation_noise_on else "no sensor noise")
+    parts.append(f"{100 * cfg.domain_randomization:.0f}% DR" if cfg.domain_randomization_on else "no DR")
+    parts.append(f"{'Bullet' if cfg.physics == 0 else 'Simple'} physics x{cfg.aggregate_phy_steps} sub-steps")
+    if cfg.max_episode_steps:
+        parts.append(f"TimeLimit {cfg.max_episode_steps} + auto-reset")
+    return ", ".join(parts)
+
+
 def cpu_baseline(n_envs=2048, steps=300, seed=0):
     """Time the CPU restatement (oracle/, scalar C, one core) on a bounded sample of the same
     workload.  Reported baseline only, not the target."""
@@ -211,8 +226,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: uniform(-1,1) actions, Philox-seeded resets/noise/gusts",
-            "config": {"workload": f"{args.env_id} (C4 gust, reference default noise/DR/latency, "
-                                   f"TimeLimit 500 + auto-reset), {n} envs per GPU",
+            "config": {"workload": f"{args.env_id} ({describe(env.cfg)}), {n} envs per GPU",
                        "envs_per_gpu": n, "global_envs": n * world, "aggregate_phy_steps": 2,
                        "parallelism": f"env-shard x{world}", "gather_obs": bool(args.gather_obs),
                        "graph": bool(args.graph)},
