@@ -70,26 +70,44 @@ def describe(cfg) -> str:
     return ", ".join(parts)
 
 
-def cpu_baseline(n_envs=2048, steps=300, seed=0):
-    """Time the CPU restatement (oracle/, scalar C, one core) on a bounded sample of the same
-    workload.  Reported baseline only, not the target."""
+def _host_threads() -> int:
+    """Host threads this process may use (the GPU box's CPU share, not the machine's core count)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, len(os.sched_getaffinity(0)))
+
+
+def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
+    """Time the CPU restatement (oracle/, scalar C fp64) on a bounded sample of the same workload:
+    one thread, then OpenMP over the host threads this process may use (envs split by index).
+    Reported baseline only, not the target; `value` is the all-thread rate."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from cf2sim.config import build_config
-    cfg = build_config(ENV_ID, n_envs, seed=seed)
-    env = orc.OracleEnv(cfg, precision="f64")
-    env.reset()
-    rng = np.random.default_rng(seed)
-    acts = rng.uniform(-1, 1, size=(8, n_envs, 4)).astype(np.float32)
-    t0 = time.perf_counter()
-    for k in range(steps):
-        env.step(acts[k % 8])
-    dt = time.perf_counter() - t0
-    env.close()
-    return {"value": n_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/cf2_oracle.c fp64, {n_envs} envs x {steps} env-steps of {ENV_ID} "
-                      f"(gust, noise, DR), 1 thread, {dt:.1f} s"}
+    threads = threads or _host_threads()
+
+    def rate(n, k, t):
+        env = orc.OracleEnv(build_config(ENV_ID, n, seed=seed), precision="f64")
+        env.set_threads(t)
+        env.reset()
+        rng = np.random.default_rng(seed)
+        acts = rng.uniform(-1, 1, size=(8, n, 4)).astype(np.float32)
+        env.step(acts[0])                      # first touch of the outputs outside the timing
+        t0 = time.perf_counter()
+        for j in range(k):
+            env.step(acts[j % 8])
+        dt = time.perf_counter() - t0
+        env.close()
+        return n * k / dt, dt
+
+    one, dt1 = rate(2048, 600, 1)
+    allt, dtn = rate(n_envs, steps, threads) if threads > 1 else (one, dt1)
+    return {"value": allt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/cf2_oracle.c fp64 on {ENV_ID} (gust, noise, DR): {n_envs} envs x {steps} "
+                      f"env-steps on {threads} OpenMP threads in {dtn:.1f} s; 1 thread: {one:.3g} env-steps/s "
+                      f"(2048 envs x 600 env-steps, {dt1:.1f} s)"}
 
 
 def load_traffic(workload_key: str):
@@ -116,8 +134,8 @@ def main():
     ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of obs every step")
     ap.add_argument("--graph", action="store_true", help="capture the timed steps in a hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=4096)
-    ap.add_argument("--cpu-steps", type=int, default=1500)
+    ap.add_argument("--cpu-envs", type=int, default=16384)
+    ap.add_argument("--cpu-steps", type=int, default=1000)
     ap.add_argument("--env-kw", default="{}", help="JSON env kwargs (ablations), e.g. '{\"observation_noise\": 0}'")
     args = ap.parse_args()
     env_kw = json.loads(args.env_kw)

@@ -1456,6 +1456,11 @@ static inline bool spec_default_shape(const KParams& P) {
            P.use_motor_dyn;
 }
 
+#ifdef CF2_BENCH_ONLY
+// A/B builds (tools/build_variant.sh): only the bench workload's instance, so a variant compiles
+// in seconds.  Never the shipped library.
+#define CF2_DISPATCH(FN, ...) return FN<true, true, PHYS_BULLET_T, 1>(__VA_ARGS__)
+#else
 #define CF2_DISPATCH(FN, ...)                                                                          \
     do {                                                                                               \
         const int key = (P.noise ? 4 : 0) | (P.dr ? 2 : 0) | (P.phys == PHYS_SIMPLE_T ? 1 : 0);           \
@@ -1486,6 +1491,7 @@ static inline bool spec_default_shape(const KParams& P) {
         default: return FN<true, true, PHYS_SIMPLE_T, 0>(__VA_ARGS__);                                 \
         }                                                                                              \
     } while (0)
+#endif
 
 #ifdef CF2_TIMING
 extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {

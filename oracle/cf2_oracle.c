@@ -252,6 +252,7 @@ typedef struct {
     const float* V;           /* HJ tables [num_tables][15^6] */
     int num_tables;
     int32_t table_of_level[CF2_NUM_LEVELS_MAX];
+    int threads;              /* OpenMP threads of orc_step (formations are independent) */
 } orc_ctx;
 
 static int obs_len(const cf2_config* c) { return c->observation_noise_on ? 13 : 17; }
@@ -798,6 +799,9 @@ void* orc_create(const cf2_config* cfg) {
     for (int l = 0; l < CF2_NUM_LEVELS_MAX; ++l) X->table_of_level[l] = -1;
     return X;
 }
+/* OpenMP threads used by orc_step (default 1; the bench's all-core CPU baseline raises it). */
+void orc_set_threads(void* h, int threads) { ((orc_ctx*)h)->threads = threads; }
+
 void orc_destroy(void* h) {
     orc_ctx* X = (orc_ctx*)h;
     free(X->e);
@@ -880,6 +884,8 @@ void orc_step(void* h, const float* act, const double* dstb_ext, double* obs, do
     const cf2_config* c = &X->cfg;
     int ol = obs_len(c), od = 2 * (ol + 4);
     const int M = c->num_drones > 0 ? c->num_drones : 1;
+    /* formations touch only their own envs: they split across threads with identical results */
+#pragma omp parallel for schedule(static) num_threads(X->threads > 0 ? X->threads : 1) if (X->threads > 1)
     for (int g0 = 0; g0 < X->n; g0 += M) {
       /* the drones of one formation advance their sub-steps in lock step: the downwash of sub-step
        * s uses every mate's position before that sub-step (single drones: M = 1) */

@@ -43,6 +43,7 @@ class _Lib:
             lib.orc_create.restype = _P
             lib.orc_create.argtypes = [_P]
             lib.orc_destroy.argtypes = [_P]
+            lib.orc_set_threads.argtypes = [_P, ctypes.c_int]
             lib.orc_reset.argtypes = [_P, _u8p, _dp]
             lib.orc_step.argtypes = [_P, _fp, _dp, _dp, _dp, _u8p, _u8p, _dp, _dp, _dp]
             lib.orc_get_state.argtypes = [_P, _dp, _ip]
@@ -106,6 +107,10 @@ class OracleEnv:
             self.close()
         except Exception:
             pass
+
+    def set_threads(self, threads: int):
+        """OpenMP threads of step() (formations split across threads; results are identical)."""
+        self.lib.orc_set_threads(self.h, int(threads))
 
     def bind_tables(self, V: np.ndarray, table_of_level):
         V = np.ascontiguousarray(V, dtype=np.float32)
