@@ -68,6 +68,28 @@ __device__ __forceinline__ void normals(const G& g, uint32_t b0, float (&z)[N]) 
     }
 }
 
+// The auto-reset table holds the Box-Muller outputs, not the raw words, of the word pairs the
+// reset turns into normals (reset_env: blocks 4-8; its two sensor calls: blocks 32-35 and 40-43
+// whole, 36 and 44 first pair).  They are transformed block-parallel while the table is drawn,
+// which takes ~110 transcendentals off the one-lane-per-env reset path.
+__host__ __device__ constexpr bool reset_slot_normal_xy(int s) {
+    return (s >= 4 && s <= 8) || (s >= 14 && s <= 18) || (s >= 20 && s <= 24);
+}
+__host__ __device__ constexpr bool reset_slot_normal_zw(int s) {
+    return (s >= 4 && s <= 8) || (s >= 14 && s <= 17) || (s >= 20 && s <= 23);
+}
+template <int N>
+__device__ __forceinline__ void normals(const TableRng& g, uint32_t b0, float (&z)[N]) {
+#pragma unroll
+    for (int blk = 0; blk < (N + 3) / 4; ++blk) {
+        const U4 u = g.block(b0 + blk);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (4 * blk + k < N) z[4 * blk + k] = __uint_as_float(w[k]);
+    }
+}
+
 // Normals LO..HI-1 of the sequence normals<N>(g, b0, .) would produce, drawing only the Philox
 // blocks and Box-Muller pairs that cover them (the stream positions of all other draws are
 // unchanged, so skipping dead draws is invisible to everything else).
@@ -118,7 +140,10 @@ __device__ __forceinline__ void mtv(const M3& R, const float v[3], float o[3]) {
     o[1] = R.m[1] * v[0] + R.m[4] * v[1] + R.m[7] * v[2];
     o[2] = R.m[2] * v[0] + R.m[5] * v[1] + R.m[8] * v[2];
 }
-__device__ __forceinline__ float norm3(const float v[3]) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+// v_sqrt_f32 without the denormal pre-scaling sqrtf adds (6 instructions -> 1): the same result
+// for every normal operand; a denormal operand (|v| < 1e-19) gives 0
+__device__ __forceinline__ float sqrt_fast(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float norm3(const float v[3]) { return sqrt_fast(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
 // clip(x, lo, hi) for lo <= hi as one v_med3_f32 (identical to the compare form for non-NaN x)
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 // Makes a register value opaque to the optimiser.  Used before data-dependent selects among
@@ -158,7 +183,7 @@ __device__ __forceinline__ float atan2_fast(float y, float x) {
     return __builtin_copysignf(r, y);
 }
 __device__ __forceinline__ float asin_fast(float x) {
-    return atan2_fast(x, __builtin_sqrtf(fmaxf(0.0f, (1.0f - x) * (1.0f + x))));
+    return atan2_fast(x, sqrt_fast(fmaxf(0.0f, (1.0f - x) * (1.0f + x))));
 }
 
 __device__ __forceinline__ void quat_from_euler(const float e[3], float q[4]) {
@@ -493,7 +518,7 @@ __device__ __forceinline__ void apply_action(const KParams& P, Env& E, const flo
         const float tn = pwm[j] / 60000.0f;
         float noisy;
         if (P.use_motor_dyn) {
-            const float rot = sqrtf(tn);
+            const float rot = sqrt_fast(tn);
             E.x[j] = E.A[j] * E.x[j] + E.B[j] * rot;
             noisy = (1.0f + E.ou[j]) * (E.x[j] * E.x[j]);
         } else {
@@ -727,8 +752,8 @@ __device__ __forceinline__ float compute_reward(const KParams& P, const Env& E, 
     float na[4], ad[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) { na[k] = 0.5f * (clampf(a[k], -1.0f, 1.0f) + 1.0f); ad[k] = a[k] - E.la[k]; }
-    const float nna = sqrtf(na[0] * na[0] + na[1] * na[1] + na[2] * na[2] + na[3] * na[3]);
-    const float nad = sqrtf(ad[0] * ad[0] + ad[1] * ad[1] + ad[2] * ad[2] + ad[3] * ad[3]);
+    const float nna = sqrt_fast(na[0] * na[0] + na[1] * na[1] + na[2] * na[2] + na[3] * na[3]);
+    const float nad = sqrt_fast(ad[0] * ad[0] + ad[1] * ad[1] + ad[2] * ad[2] + ad[3] * ad[3]);
     float dr[3], dw[3], dp[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -818,7 +843,7 @@ __device__ __forceinline__ float downwash(const KParams& P, const float p[3], ui
         const float qx = __shfl(p[0], j, P.num_drones), qy = __shfl(p[1], j, P.num_drones),
                     qz = __shfl(p[2], j, P.num_drones);
         const float dz = qz - p[2], dx = qx - p[0], dy = qy - p[1];
-        const float dxy = __builtin_sqrtf(dx * dx + dy * dy);
+        const float dxy = sqrt_fast(dx * dx + dy * dy);
         if ((uint32_t)j != member && dz > 0.0f && dxy < 10.0f) {
             const float rr = P.prop_radius * rcp(4.0f * dz);
             const float alpha = P.dw_coeff[0] * rr * rr;
@@ -1292,7 +1317,17 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
                     const uint32_t sl = w / nc, e = w - sl * nc, pos = c0 + e;
                     const uint32_t t = s_list[pos];
                     const uint32_t ctr = reinterpret_cast<const uint32_t*>(s_obs + t * OD)[12];
-                    const U4 u = philox(K, reset_block_of_slot((int)sl), ctr, P.gid_off + base + t, TAG_RESET);
+                    U4 u = philox(K, reset_block_of_slot((int)sl), ctr, P.gid_off + base + t, TAG_RESET);
+                    if (reset_slot_normal_xy((int)sl)) {
+                        float z0, z1;
+                        box_muller(u.x, u.y, z0, z1);
+                        u.x = __float_as_uint(z0); u.y = __float_as_uint(z1);
+                    }
+                    if (reset_slot_normal_zw((int)sl)) {
+                        float z2, z3;
+                        box_muller(u.z, u.w, z2, z3);
+                        u.z = __float_as_uint(z2); u.w = __float_as_uint(z3);
+                    }
                     uint32_t* q = s_rand + sl * 4 * C + e;
                     q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
                 }

@@ -36,7 +36,9 @@ __device__ __forceinline__ U4 philox(const Keys& K, uint32_t c0, uint32_t c1, ui
         // one v_mad_u64_u32 per product yields both halves
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ K.k0[r], n2 = (uint32_t)(p0 >> 32) ^ c3 ^ K.k1[r];
+        // three-input XOR in one v_bitop3_b32 (gfx950; truth table 0x96)
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, K.k0[r], 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, K.k1[r], 0x96);
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
     }
     return U4{c0, c1, c2, c3};

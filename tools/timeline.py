@@ -61,6 +61,11 @@ def main():
     dur = {f"{a}->{b}": np.diff(st[:, [a, b]], axis=1)[:, 0] for a, b in [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (0, 5)]}
     names = {"0->1": "entry->loads landed", "1->2": "physics", "2->3": "obs/history/stores",
              "3->4": "block barrier wait", "4->5": "resets+final barrier+copy", "0->5": "wave lifetime"}
+    ex = t[:, 12:15].astype(np.float64)
+    if (ex[:, 0] != 0).all():
+        s2, s3 = t[:, 5].astype(np.float64), t[:, 6].astype(np.float64)
+        print(f"  epilogue split: final sensor {np.mean(ex[:, 0] - s2):.0f}, store_core+done/reward {np.mean(ex[:, 1] - ex[:, 0]):.0f}, "
+              f"history {np.mean(ex[:, 2] - ex[:, 1]):.0f}, obs stage+store_tail {np.mean(s3 - ex[:, 2]):.0f}")
     rw = t[:, 9] != 0       # waves that ran a reset (stamps 6..8)
     if rw.any():
         r6, r7, r8 = (t[rw, 9 + k].astype(np.float64) for k in range(3))
