@@ -1333,8 +1333,11 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
                 }
             }
             __syncthreads();
-            if (tid < nc) {
-                const uint32_t pos = c0 + tid, t = s_list[pos];
+            // the resetting wave rotates with the block index, so that the resets of the blocks
+            // sharing a CU do not all queue on one SIMD
+            const uint32_t rl = tid - 64u * (blockIdx.x % (B / 64u));
+            if (rl < nc) {
+                const uint32_t pos = c0 + rl, t = s_list[pos];
                 const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
                 ResetSeed q;
 #pragma unroll
@@ -1344,7 +1347,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
                 q.level = __uint_as_float(row[10]);
                 q.level_idx = (int)row[11];
                 q.ctr = row[12];
-                const TableRng tg{s_rand + tid, C};
+                const TableRng tg{s_rand + rl, C};
                 reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD);
             }
             __syncthreads();     // the next chunk reuses s_rand

@@ -224,6 +224,26 @@ def test_reward_done_cost_known_answers():
     assert abs(r - -(0.5 + 1e-4 * 2.0)) < 1e-12
 
 
+@pytest.mark.parametrize("env_id,kw", [("DroneHoverBulletFreeEnvWithGust-v0", {}),
+                                        ("DroneHoverBulletFreeEnvWithDownwash-v0", {"num_drones": 4})])
+def test_threaded_step_is_bit_identical(env_id, kw):
+    """The all-core CPU baseline (bench.py) steps formations on OpenMP threads: same results."""
+    c = build_config(env_id, 256, seed=5, **kw)
+    e1 = O.OracleEnv(c, "f64"); e4 = O.OracleEnv(c, "f64")
+    e4.set_threads(4)
+    np.testing.assert_array_equal(e1.reset(), e4.reset())
+    rng = np.random.default_rng(2)
+    for t in range(40):
+        a = rng.uniform(-1, 1, (256, 4)).astype(np.float32)
+        r1, r4 = e1.step(a, want_final=True), e4.step(a, want_final=True)
+        for x, y in zip(r1[:3], r4[:3]):
+            np.testing.assert_array_equal(x, y)
+        np.testing.assert_array_equal(r1[3]["final_obs"], r4[3]["final_obs"])
+    s1, s4 = e1.get_state(), e4.get_state()
+    np.testing.assert_array_equal(s1[0], s4[0]); np.testing.assert_array_equal(s1[1], s4[1])
+    e1.close(); e4.close()
+
+
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 def test_fp32_restatement_tracks_fp64(prec):
     c = build_config("DroneHoverBulletFreeEnvWithoutAdversary-v0", 64, seed=9)
