@@ -1253,6 +1253,11 @@ template <bool NOISE, bool DR, int PHYS, int SPEC>
 #endif
 __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
     const KParams P = shape_view<SPEC>(P0);
+    // Issue priority: the blocks that start only after the first residency round (the partial
+    // last round at 262 144 envs) run mostly alone on their SIMDs and end the kernel; their waves
+    // get the issue slots first, so they overlap the tail of the first round (-1 us measured).
+    if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
 #ifdef CF2_TIMING
     if (uint64_t* r = timing_row()) {
         if ((threadIdx.x & 63) == 0) {
@@ -1477,7 +1482,20 @@ __global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* _
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
     const dim3 grid((P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK), block(CF2_STEP_BLOCK);
-    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, io);
+    // blocks resident at once = CUs x blocks per CU at this kernel's VGPR/LDS use (queried once)
+    static int round_blocks = -1;
+    if (round_blocks < 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<NOISE, DR, PHYS, SPEC>, CF2_STEP_BLOCK, 0);
+        if (e != hipSuccess) return e;
+        round_blocks = cus * per_cu;
+    }
+    KParams Pl = P;
+    Pl.late_block = (uint32_t)round_blocks;
+    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, Pl, io);
     return hipGetLastError();
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
