@@ -1143,7 +1143,7 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
     const bool term = compute_done(P, E);
     const float r = compute_reward(P, E, a, term);
-    const float cost = compute_cost(P, E);
+    const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
     E.ep_step += 1;
     const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
     const bool done = term || trunc;
