@@ -155,6 +155,16 @@ def main():
 
     n = args.envs_per_gpu
     env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=rank * n, device=dev, **env_kw)
+    hj_tables = 0
+    if int(env.cfg.disturbance) == 5:
+        # HJ-adversary envs: the reference's fastrack_{level}_15x15.npy tables are not in its
+        # checkout (.MISSING_LARGE_BLOBS); bind smooth synthetic 15^6 tables (one per 3 levels)
+        hj_tables = 3
+        ax = torch.linspace(-1.0, 1.0, 15, device=dev)
+        g = [ax.view([-1 if i == d else 1 for i in range(6)]) for d in range(6)]
+        V = torch.stack([sum((0.3 + 0.1 * t + 0.05 * d) * g[d] ** (1 + (d + t) % 2) for d in range(6))
+                         + 0.1 * torch.sin(3 * g[3] + 2 * g[4] - g[5] + t) for t in range(hj_tables)])
+        env.bind_hj_tables(V.reshape(hj_tables, -1), [lv % hj_tables for lv in range(int(env.cfg.num_levels))])
     env.reset()
     ring = 8
     g = torch.Generator(device=dev)
@@ -243,7 +253,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: uniform(-1,1) actions, Philox-seeded resets/noise/gusts",
+            "data": "synthetic: uniform(-1,1) actions, Philox-seeded resets/noise/gusts"
+                    + (f", {hj_tables} synthetic 15^6 HJ value tables" if hj_tables else ""),
             "config": {"workload": f"{args.env_id} ({describe(env.cfg)}), {n} envs per GPU",
                        "envs_per_gpu": n, "global_envs": n * world, "aggregate_phy_steps": 2,
                        "parallelism": f"env-shard x{world}", "gather_obs": bool(args.gather_obs),

@@ -240,11 +240,13 @@ __device__ __forceinline__ int grid_nearest(const double* pts, double s) {
 }
 __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
 
-// returns bit i set <=> dV/dx_{3+i} > 0 (opt disturbance = -dmax_i)
-__device__ __forceinline__ unsigned hj_signs(const KParams& P, const float* __restrict__ V, const double st[6]) {
+// returns bit i set <=> dV/dx_{3+i} > 0 (opt disturbance = -dmax_i).  grid: the 6 x 15 grid
+// points (KTables::hj_grid) staged in LDS by the calling kernel: the nearest-node searches then
+// cost LDS round trips instead of serialised global loads.
+__device__ __forceinline__ unsigned hj_signs(const float* __restrict__ V, const double st[6], const double* grid) {
     int idx[6];
 #pragma unroll
-    for (int d = 0; d < 6; ++d) idx[d] = grid_nearest(P.tab->hj_grid[d], st[d]);
+    for (int d = 0; d < 6; ++d) idx[d] = grid_nearest(grid + d * HJ_PTS, st[d]);
     const int stride[6] = {759375, 50625, 3375, 225, 15, 1};
     int c = 0;
 #pragma unroll
@@ -271,6 +273,12 @@ __device__ __forceinline__ unsigned hj_signs(const KParams& P, const float* __re
         bits |= (L > -Rr ? 1u : 0u) << i;
     }
     return bits;
+}
+
+// every thread of the block takes part (contains a block barrier)
+__device__ __forceinline__ void stage_hj_grid(const KParams& P, double* s_grid) {
+    for (uint32_t k = threadIdx.x; k < 6u * HJ_PTS; k += blockDim.x) s_grid[k] = P.tab->hj_grid[k / HJ_PTS][k % HJ_PTS];
+    __syncthreads();
 }
 
 // ------------------------------------------------------------------------------------
@@ -1043,7 +1051,7 @@ enum { SEED_WORDS = 13 };
 
 template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
-                                         ResetSeed& rs) {
+                                         ResetSeed& rs, const double* hj_grid) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     Env E;
@@ -1109,7 +1117,7 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
             float e[3];
             quat2euler(E.q, e);
             const double st[6] = {(double)e[0], (double)e[1], (double)e[2], (double)E.wb[0], (double)E.wb[1], (double)E.wb[2]};
-            const unsigned bits = hj_signs(P, P.V + (size_t)t * HJ_TABLE, st);
+            const unsigned bits = hj_signs(P.V + (size_t)t * HJ_TABLE, st, hj_grid);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const float dm = (float)((double)E.level * (double)P.umax_d[k]);
@@ -1283,7 +1291,9 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
     bool do_reset = false;
     ResetSeed rs;
-    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs);
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P, s_hjgrid);     // uniform branch
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     if (P.auto_reset) {
         __syncthreads();     // s_cnt initialised
         const uint64_t m = __ballot(do_reset);
@@ -1461,12 +1471,14 @@ __global__ void state_convert_kernel(uint32_t N, float* __restrict__ sf, float* 
 
 __global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* __restrict__ states, uint32_t n,
                           float level, float* __restrict__ dstb, float* __restrict__ uopt) {
+    __shared__ double s_grid[6 * HJ_PTS];
+    stage_hj_grid(P, s_grid);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double st[6];
 #pragma unroll
     for (int d = 0; d < 6; ++d) st[d] = (double)states[(size_t)i * 6 + d];
-    const unsigned bits = hj_signs(P, V, st);
+    const unsigned bits = hj_signs(V, st, s_grid);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const double um = P.umax_d[k];
