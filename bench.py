@@ -147,8 +147,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one process per GPU over RCCL ("nccl"); CF2_BENCH_BACKEND=gloo rehearses the multi-rank
+        # path with several ranks sharing the GPUs of a smaller box
+        backend = os.environ.get("CF2_BENCH_BACKEND", "nccl")
+        local_dev = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from cf2sim.vec_env import BatchedCrazyflieEnv
@@ -216,7 +223,7 @@ def main():
     # average step-kernel duration over the timed region, HIP events on the launch stream
     kern_ms = ev_start.elapsed_time(ev_end) / args.steps
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
