@@ -72,3 +72,49 @@ def test_full_size_slices_and_sharding(gpu, env_id, T):
     np.testing.assert_array_equal(si.cpu().numpy(), np.concatenate([x[1].cpu().numpy() for x in hs], 1))
     for e in [full] + halves:
         e.close()
+
+
+def test_full_size_hj_adversary_slices(gpu):
+    """f1 at the full size: the HJ gather (grid staged in LDS per block) on synthetic tables.
+    The HJ disturbance is bang-bang: its sign comes from the nearest grid node and a comparison of
+    value differences, so an env whose fp32 state sits within an ulp of a node midpoint or a sign
+    tie can take the other branch than the restatement and then diverge (seen for 1-2 of 1536 envs
+    over 30 env-steps, at any N).  The gather itself is bit-exact on identical inputs
+    (test_gpu_parity.test_hj_disturbance_batched_matches_restatement); here at most 2 envs may
+    leave the 5e-4 band, and every other env must match exactly as in the small-case tests."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    from test_gpu_parity import _synthetic_tables
+    env_id, T = "DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", 30
+    V = _synthetic_tables(tuple(range(3)), seed=1)
+    table_of_level = [lv % 3 for lv in range(21)]
+    full = BatchedCrazyflieEnv(env_id, N, seed=5)
+    full.bind_hj_tables(torch.from_numpy(V).cuda(), table_of_level)
+    refs = []
+    for k in SLICES:
+        r = O.OracleEnv(build_config(env_id, SLICE, seed=5, env_id_offset=k), precision="f32")
+        r.bind_tables(V, table_of_level)
+        refs.append(r)
+    go = full.reset().cpu().numpy()
+    for k, r in zip(SLICES, refs):
+        assert _nerr(go[k:k + SLICE], r.reset()) < 2e-5
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(12)
+    diverged = np.zeros(len(SLICES) * SLICE, bool)
+    worst = 0.0
+    for t in range(T):
+        a = ((torch.rand(N, 4, device="cuda", generator=gen) * 2 - 1) * 0.25 + 0.1111).contiguous()
+        g_o, _, g_d, g_i = full.step(a)
+        g_o, g_d = g_o.cpu().numpy(), g_d.cpu().numpy().astype(bool)
+        lv = g_i["disturbance_level"].cpu().numpy()
+        a_np = a.cpu().numpy()
+        for si, (k, r) in enumerate(zip(SLICES, refs)):
+            r_o, _, r_d, r_i = r.step(a_np[k:k + SLICE])
+            e = (np.abs(g_o[k:k + SLICE] - r_o) / (1.0 + np.abs(r_o))).max(1)
+            dv = diverged[si * SLICE:(si + 1) * SLICE]
+            dv |= e >= 5e-4
+            np.testing.assert_array_equal(g_d[k:k + SLICE][~dv], r_d[~dv])
+            np.testing.assert_allclose(lv[k:k + SLICE], r_i["level"], atol=1e-6)
+            worst = max(worst, float(e[~dv].max()) if (~dv).any() else 0.0)
+    assert diverged.sum() <= 2, f"{int(diverged.sum())} envs left the 5e-4 band"
+    assert worst < 5e-4
+    full.close()
