@@ -43,7 +43,10 @@ def algorithmic_bytes_per_env_step(cfg, outputs=("obs", "rew", "done")) -> int:
     persist_f = 13 + 8 + 4 * B + (6 if noise else 0) + (10 if noise and held else 0) + ol + 8
     if cfg.physics == 1:
         persist_f += 3
-    rd_f = persist_f + (19 if dr else 0) + (3 if gust_or_const else 0) + (1 if level else 0)
+    if cfg.use_motor_dynamics:
+        persist_f += 4          # low words of the compensated motor state
+    # DR parameters: dt, m, J[3], k0, k1, B[4], K[4] (A = 1 - B is not stored)
+    rd_f = persist_f + (15 if dr else 0) + (3 if gust_or_const else 0) + (1 if level else 0)
     wr_f = persist_f + (3 if cfg.disturbance == 4 else 0)
     rd_i = 3 + (1 if level else 0) + (1 if cfg.disturbance == 4 else 0)
     wr_i = 3 + (1 if cfg.disturbance == 4 else 0)

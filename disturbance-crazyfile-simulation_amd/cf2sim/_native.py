@@ -33,7 +33,7 @@ class CF2Layout(ctypes.Structure):
         "num_envs", "num_float_fields", "num_int_fields", "obs_dim", "obs_len",
         "f_pos", "f_quat", "f_vel", "f_omega", "f_rpy", "f_motor", "f_ou", "f_abuf", "f_bias", "f_lpf", "f_held",
         "f_obs_prev", "f_hist_act", "f_param", "f_dstb", "i_ep_step", "i_rng", "i_flags", "i_level", "i_gust",
-        "num_params")]
+        "num_params", "f_motor_lo")]
 
 
 class CF2Error(RuntimeError):

@@ -224,6 +224,7 @@ int cf2_layout_get(const cf2_ctx* ctx, cf2_layout* o) {
     o->f_dstb = F_DSTB;
     o->i_ep_step = I_EP_STEP; o->i_rng = I_RNG; o->i_flags = I_FLAGS; o->i_level = I_LEVEL; o->i_gust = I_GUST;
     o->num_params = NUM_PARAMS;
+    o->f_motor_lo = F_MOTOR_LO;
     return CF2_OK;
 }
 

@@ -24,7 +24,8 @@ enum : int {
     F_PARAM = 81,       // 19 per-env DR params: dt, m, Jx, Jy, Jz, k0, k1, A[4], B[4], K[4]
     F_DSTB = 100,       // 3  per-episode / current-gust disturbance torque
     F_LEVEL = 103,      // 1  disturbance level of the episode
-    NF = 104
+    F_MOTOR_LO = 104,   // 4  low word of the motor state (x + x_lo, compensated recurrence)
+    NF = 108
 };
 // ---- int state fields ----
 enum : int {
@@ -57,8 +58,10 @@ enum : int {
     S_HACT = 56,                                          // G14-G15
     S_OBSP = 64,                                          // G16-G20 (13 or 17 used)
     S_HELD = 84,                                          // G21-G23 (held_persistent only)
-    S_PARAM = 96,                                         // G24-G28.z (19 DR params)
-    S_LEVEL = 115,                                        // G28.w
+    S_PARAM = 96,                                         // G24-G27.z: 15 DR params (dt, m, J, k0, k1,
+                                                          //   B[4], K[4]; A = 1 - B is not stored)
+    S_LEVEL = 111,                                        // G27.w
+    S_MOTOR_LO = 112,                                     // G28: motor-state low words
     S_LEVEL_IDX = 116,                                    // G29.x (int)
     NS = 120, NG = 30
 };

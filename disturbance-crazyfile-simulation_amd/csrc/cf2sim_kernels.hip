@@ -305,11 +305,11 @@ __device__ __forceinline__ void stage_hj_grid(const KParams& P, double* s_grid) 
 struct Env {
     float p[3], q[4], v[3], w[3];   // w: world angular velocity (bullet) / body rates (simple)
     float rpy[3], wb[3];            // derived readback (drone.rpy, drone.rpy_dot)
-    float x[4], ou[4], abuf[4][4];
+    float x[4], xl[4], ou[4], abuf[4][4];   // motor state x + xl (compensated pair)
     float bias[3], lpf[3], held[10];
     float obs_prev[17];
     float hact[2][4];
-    float dt, m, J[3], k0, k1, A[4], B[4], K[4];
+    float dt, m, J[3], k0, k1, B[4], K[4];
     float dstb[3], level;
     int ep_step, aidx, halias0, halias1, la_view, level_idx, gust_left;
     uint32_t rng;
@@ -345,7 +345,8 @@ struct Tile {
 };
 
 enum : int { G_CORE3 = 3, G_MOTOR = 4, G_OU = 5, G_ABUF = 6, G_BIAS = 10, G_LPF = 11, G_RPY = 12, G_DSTB = 13,
-             G_HACT = 14, G_OBSP = 16, G_HELD = 21, G_PARAM = 24, G_LEVEL_IDX = 29 };
+             G_HACT = 14, G_OBSP = 16, G_HELD = 21, G_PARAM = 24, G_LEVEL = 27, G_MOTOR_LO = 28,
+             G_LEVEL_IDX = 29 };
 
 __device__ __forceinline__ bool gust_mode(const KParams& P) { return P.dstb_mode == DSTB_GUST_T; }
 __device__ __forceinline__ bool dstb_stored(const KParams& P) {
@@ -382,6 +383,11 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
     const int fl = bi(g3.w);
     E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
     E.x[0] = gx.x; E.x[1] = gx.y; E.x[2] = gx.z; E.x[3] = gx.w;
+    {
+        F4 xl = f4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (P.use_motor_dyn) xl = T.ld(G_MOTOR_LO);
+        E.xl[0] = xl.x; E.xl[1] = xl.y; E.xl[2] = xl.z; E.xl[3] = xl.w;
+    }
     E.ou[0] = go.x; E.ou[1] = go.y; E.ou[2] = go.z; E.ou[3] = go.w;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -420,19 +426,18 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
     if (with_hist) load_hist<NOISE>(T, E);
     F4 lv = f4(0.0f, 0.0f, 0.0f, P.level_fixed);
     if (DR) {
-        const F4 p0 = T.ld(G_PARAM), p1 = T.ld(G_PARAM + 1), p2 = T.ld(G_PARAM + 2), p3 = T.ld(G_PARAM + 3);
-        lv = T.ld(G_PARAM + 4);
+        const F4 p0 = T.ld(G_PARAM), p1 = T.ld(G_PARAM + 1), p2 = T.ld(G_PARAM + 2);
+        lv = T.ld(G_LEVEL);
         E.dt = p0.x; E.m = p0.y; E.J[0] = p0.z; E.J[1] = p0.w;
-        E.J[2] = p1.x; E.k0 = p1.y; E.k1 = p1.z; E.A[0] = p1.w;
-        E.A[1] = p2.x; E.A[2] = p2.y; E.A[3] = p2.z; E.B[0] = p2.w;
-        E.B[1] = p3.x; E.B[2] = p3.y; E.B[3] = p3.z; E.K[0] = p3.w;
+        E.J[2] = p1.x; E.k0 = p1.y; E.k1 = p1.z; E.B[0] = p1.w;
+        E.B[1] = p2.x; E.B[2] = p2.y; E.B[3] = p2.z; E.K[0] = p2.w;
         E.K[1] = lv.x; E.K[2] = lv.y; E.K[3] = lv.z;
     } else {
         E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
         E.k0 = P.ft0; E.k1 = P.ft1;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { E.A[k] = P.A; E.B[k] = P.B; E.K[k] = P.K; }
-        if (need_level) lv = T.ld(G_PARAM + 4);
+        for (int k = 0; k < 4; ++k) { E.B[k] = P.B; E.K[k] = P.K; }
+        if (need_level) lv = T.ld(G_LEVEL);
     }
     E.level = need_level ? lv.w : P.level_fixed;
     E.level_idx = need_level ? bi(T.ld(G_LEVEL_IDX).x) : 0;
@@ -447,6 +452,7 @@ __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__
     T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
     T.st(2, f4(E.v[1], E.v[2], E.w[0], E.w[1]));
     T.st(G_MOTOR, f4(E.x[0], E.x[1], E.x[2], E.x[3]));
+    if (P.use_motor_dyn) T.st(G_MOTOR_LO, f4(E.xl[0], E.xl[1], E.xl[2], E.xl[3]));
     T.st(G_OU, f4(E.ou[0], E.ou[1], E.ou[2], E.ou[3]));
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -494,11 +500,10 @@ __device__ __forceinline__ void store_env(const KParams& P, float* __restrict__ 
     if (params_dirty) {
         if (DR) {
             T.st(G_PARAM, f4(E.dt, E.m, E.J[0], E.J[1]));
-            T.st(G_PARAM + 1, f4(E.J[2], E.k0, E.k1, E.A[0]));
-            T.st(G_PARAM + 2, f4(E.A[1], E.A[2], E.A[3], E.B[0]));
-            T.st(G_PARAM + 3, f4(E.B[1], E.B[2], E.B[3], E.K[0]));
+            T.st(G_PARAM + 1, f4(E.J[2], E.k0, E.k1, E.B[0]));
+            T.st(G_PARAM + 2, f4(E.B[1], E.B[2], E.B[3], E.K[0]));
         }
-        T.st(G_PARAM + 4, f4(E.K[1], E.K[2], E.K[3], E.level));
+        T.st(G_LEVEL, f4(E.K[1], E.K[2], E.K[3], E.level));
         T.st(G_LEVEL_IDX, f4(ib(E.level_idx), 0.0f, 0.0f, 0.0f));
     }
 }
@@ -544,8 +549,15 @@ __device__ __forceinline__ void apply_action(const KParams& P, Env& E, const flo
         const float tn = pwm[j] / 60000.0f;
         float noisy;
         if (P.use_motor_dyn) {
+            // x(k+1) = A x(k) + B u with A = 1 - B (agents.py:288), evaluated as x += B (u - x) on the
+            // unevaluated pair x + xl (TwoSum): the recurrence then carries no fp32 rounding from
+            // step to step (it dominated the drift vs the fp64 reference)
             const float rot = sqrt_fast(tn);
-            E.x[j] = E.A[j] * E.x[j] + E.B[j] * rot;
+            const float inc = E.B[j] * ((rot - E.x[j]) - E.xl[j]);
+            const float sum = E.x[j] + inc, bb = sum - E.x[j];                  // TwoSum
+            const float lo = ((E.x[j] - (sum - bb)) + (inc - bb)) + E.xl[j];
+            E.x[j] = sum + lo;                                                    // renormalise
+            E.xl[j] = lo - (E.x[j] - sum);
             noisy = (1.0f + E.ou[j]) * (E.x[j] * E.x[j]);
         } else {
             noisy = (1.0f + E.ou[j]) * tn;
@@ -891,7 +903,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
     const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
     E.ep_step = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) E.x[j] = 0.0f;
+    for (int j = 0; j < 4; ++j) E.x[j] = E.xl[j] = 0.0f;
     E.aidx = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -944,7 +956,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
     E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
     E.k0 = P.ft0; E.k1 = P.ft1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { E.A[j] = P.A; E.B[j] = P.B; E.K[j] = P.K; }
+    for (int j = 0; j < 4; ++j) { E.B[j] = P.B; E.K[j] = P.K; }
     if (DR) {
         const U4 d0 = g.block(9), d1 = g.block(10), d2 = g.block(11), d3 = g.block(12);
         const uint32_t d[16] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w,
@@ -959,8 +971,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
                 const float mtc = DRAW(7, 7 + j);
                 const float t2w = DRAW(8, 11 + j);
                 const float T = mtc < E.dt ? E.dt : mtc;
-                E.A[j] = 1.0f - E.dt / T;
-                E.B[j] = E.dt / T;
+                E.B[j] = E.dt / T;             // A = 1 - B (apply_action's compensated form)
                 E.K[j] = 0.028f * P.g_agent * t2w / 4.0f;
             }
         }
@@ -1258,7 +1269,7 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
     E.ou[0] = go.x; E.ou[1] = go.y; E.ou[2] = go.z; E.ou[3] = go.w;
     const uint32_t rng_ctr = (uint32_t)bi(g3.z);
     E.rng = rng_ctr;
-    E.level = T.ld(G_PARAM + 4).w;
+    E.level = T.ld(G_LEVEL).w;
     E.level_idx = bi(T.ld(G_LEVEL_IDX).x);
     float o[OD];
     const Keys K = make_keys(P.key0, P.key1);
@@ -1459,9 +1470,8 @@ __global__ void init_kernel(KParams P, float* __restrict__ sf) {
     T.st(0, f4(0.0f, 0.0f, 1.0f, 0.0f));                 // pos (0, 0, 1), quat x
     T.st(1, f4(0.0f, 0.0f, 1.0f, 0.0f));                 // quat (.., w = 1), vel x
     T.st(G_PARAM, f4(P.time_step, P.mass, P.ixx, P.iyy));
-    T.st(G_PARAM + 1, f4(P.izz, P.ft0, P.ft1, P.A));
-    T.st(G_PARAM + 2, f4(P.A, P.A, P.A, P.B));
-    T.st(G_PARAM + 3, f4(P.B, P.B, P.B, P.K));
+    T.st(G_PARAM + 1, f4(P.izz, P.ft0, P.ft1, P.B));
+    T.st(G_PARAM + 2, f4(P.B, P.B, P.B, P.K));
     float level = P.level_fixed;
     int li = 0;
     if (P.level_mode == LEVEL_BOLTZMANN_T) {
@@ -1472,7 +1482,7 @@ __global__ void init_kernel(KParams P, float* __restrict__ sf) {
         li = boltzmann_index(P, u01(u.x));
         level = P.tab->level_values[li];
     }
-    T.st(G_PARAM + 4, f4(P.K, P.K, P.K, level));
+    T.st(G_LEVEL, f4(P.K, P.K, P.K, level));
     T.st(G_LEVEL_IDX, f4(ib(li), 0.0f, 0.0f, 0.0f));
 }
 
@@ -1485,9 +1495,15 @@ __device__ __forceinline__ int pub_float_slot(int f) {
     if (f < F_OBS_PREV) return S_HELD + (f - F_HELD);
     if (f < F_HIST_ACT) return S_OBSP + (f - F_OBS_PREV);
     if (f < F_PARAM) return S_HACT + (f - F_HIST_ACT);
-    if (f < F_DSTB) return S_PARAM + (f - F_PARAM);
+    if (f < F_DSTB) {                                     // dt m J k0 k1 | A[4] | B[4] K[4]
+        const int k = f - F_PARAM;
+        if (k < 7) return S_PARAM + k;
+        if (k < 11) return -1;                            // A = 1 - B: derived, not stored
+        return S_PARAM + k - 4;
+    }
     if (f < F_LEVEL) return S_DSTB + (f - F_DSTB);
-    return S_LEVEL;
+    if (f == F_LEVEL) return S_LEVEL;
+    return S_MOTOR_LO + (f - F_MOTOR_LO);
 }
 __device__ __forceinline__ int pub_int_slot(int f) {
     switch (f) {
@@ -1506,7 +1522,12 @@ __global__ void state_convert_kernel(uint32_t N, float* __restrict__ sf, float* 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     for (int f = 0; f < NF; ++f) {
-        float* in = sf + slot_index(i, pub_float_slot(f));
+        const int slot = pub_float_slot(f);
+        if (slot < 0) {      // motor A[j]: exported as 1 - B[j], ignored on import
+            if (to_public) pf[(size_t)f * N + i] = 1.0f - sf[slot_index(i, pub_float_slot(f + 4))];
+            continue;
+        }
+        float* in = sf + slot_index(i, slot);
         if (to_public) pf[(size_t)f * N + i] = *in;
         else *in = pf[(size_t)f * N + i];
     }

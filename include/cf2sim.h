@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 2
+#define CF2SIM_ABI_VERSION 3
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -175,7 +175,8 @@ typedef struct cf2_layout {
     uint32_t f_pos, f_quat, f_vel, f_omega, f_rpy, f_motor, f_ou, f_abuf, f_bias, f_lpf, f_held,
              f_obs_prev, f_hist_act, f_param, f_dstb;
     uint32_t i_ep_step, i_rng, i_flags, i_level, i_gust;
-    uint32_t num_params;           /* per-env DR parameters (19) */
+    uint32_t num_params;           /* per-env DR parameters (19; the motor A[4] = 1 - B[4] is derived) */
+    uint32_t f_motor_lo;           /* 4: low words of the motor state (state = f_motor + f_motor_lo) */
 } cf2_layout;
 
 typedef struct cf2_ctx cf2_ctx;

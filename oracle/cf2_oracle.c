@@ -225,6 +225,7 @@ typedef struct {
     /* CrazyFlieAgent attributes */
     REAL rpy[3], wb[3];                 /* drone.rpy, drone.rpy_dot (body) */
     REAL x[4], ou[4], abuf[4][4];
+    REAL xl[4];                         /* f32 build: low word of the motor state (x + xl) */
     int aidx;
     REAL last_action[4];
     int last_action_is_view;            /* drone.last_action aliases action_buffer[-1] */
@@ -295,7 +296,20 @@ static void apply_action(const orc_ctx* X, orc_env* E, const REAL a[4], const RE
         REAL noisy;
         if (c->use_motor_dynamics) {
             REAL rot = RSQRT(tn);
+#ifdef ORACLE_F32
+            /* the HIP kernel's form: x += B (rot - x) with x kept as an unevaluated pair x + xl
+             * (TwoSum), so the 5 ms recurrence does not accumulate fp32 rounding.  Equal to
+             * A x + B rot for A = 1 - B (agents.py:288); see DESIGN.md section 5. */
+            {
+                REAL inc = E->B[j] * ((rot - E->x[j]) - E->xl[j]);
+                REAL sum = E->x[j] + inc, bb = sum - E->x[j];                       /* TwoSum */
+                REAL lo = ((E->x[j] - (sum - bb)) + (inc - bb)) + E->xl[j];
+                E->x[j] = sum + lo;                                                  /* renormalise */
+                E->xl[j] = lo - (E->x[j] - sum);
+            }
+#else
             E->x[j] = E->A[j] * E->x[j] + E->B[j] * rot;
+#endif
             noisy = (R(1.0) + E->ou[j]) * (E->x[j] * E->x[j]);
         } else {
             noisy = (R(1.0) + E->ou[j]) * tn;
@@ -666,7 +680,7 @@ static void reset_env(orc_ctx* X, int i, REAL* obs) {
     E->iteration = 0;
     E->ep_step = 0;
     /* drone.reset() agents.py:377-386 */
-    for (int j = 0; j < 4; ++j) E->x[j] = R(0.0);
+    for (int j = 0; j < 4; ++j) E->x[j] = E->xl[j] = R(0.0);
     E->aidx = 0;
     for (int r = 0; r < 4; ++r) for (int j = 0; j < 4; ++j) E->abuf[r][j] = R(0.0);
     /* task_specific_reset */
@@ -946,7 +960,7 @@ void orc_step(void* h, const float* act, const double* dstb_ext, double* obs, do
 }
 
 /* SoA snapshot in the HIP kernel's layout (DESIGN.md "State layout"). */
-#define NF 104
+#define NF 108
 #define NI 5
 void orc_get_state(void* h, double* sf, int32_t* si) {
     orc_ctx* X = (orc_ctx*)h;
@@ -974,6 +988,7 @@ void orc_get_state(void* h, double* sf, int32_t* si) {
         for (int k = 0; k < 4; ++k) { f[88 + k] = E->A[k]; f[92 + k] = E->B[k]; f[96 + k] = E->K[k]; }
         for (int k = 0; k < 3; ++k) f[100 + k] = E->dstb[k];
         f[103] = E->level;
+        for (int k = 0; k < 4; ++k) f[104 + k] = E->xl[k];
         for (int k = 0; k < NF; ++k) sf[(size_t)k * N + i] = f[k];
         si[0 * N + i] = E->ep_step;
         si[1 * N + i] = (int32_t)E->rng_ctr;
@@ -1005,6 +1020,7 @@ void orc_set_state(void* h, const double* sf, const int32_t* si) {
         for (int k = 0; k < 4; ++k) { E->A[k] = F(88 + k); E->B[k] = F(92 + k); E->K[k] = F(96 + k); }
         for (int k = 0; k < 3; ++k) E->dstb[k] = F(100 + k);
         E->level = F(103);
+        for (int k = 0; k < 4; ++k) E->xl[k] = F(104 + k);
         if (c->physics == CF2_PHYS_BULLET) {
             for (int k = 0; k < 3; ++k) E->ww[k] = F(10 + k);
             update_information(E);

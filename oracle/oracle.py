@@ -13,7 +13,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD = os.path.join(HERE, "_build")
-NF, NI = 104, 5
+NF, NI = 108, 5
 
 _P = ctypes.c_void_p
 _dp = ctypes.POINTER(ctypes.c_double)

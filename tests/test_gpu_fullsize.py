@@ -113,7 +113,7 @@ def test_full_size_hj_adversary_slices(gpu):
             dv = diverged[si * SLICE:(si + 1) * SLICE]
             dv |= e >= 5e-4
             np.testing.assert_array_equal(g_d[k:k + SLICE][~dv], r_d[~dv])
-            np.testing.assert_allclose(lv[k:k + SLICE], r_i["level"], atol=1e-6)
+            np.testing.assert_allclose(lv[k:k + SLICE][~dv], r_i["level"][~dv], atol=1e-6)   # a diverged env resets at another step
             worst = max(worst, float(e[~dv].max()) if (~dv).any() else 0.0)
     assert diverged.sum() <= 2, f"{int(diverged.sum())} envs left the 5e-4 band"
     assert worst < 5e-4

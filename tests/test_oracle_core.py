@@ -255,3 +255,25 @@ def test_fp32_restatement_tracks_fp64(prec):
         o64, r64, d64, _ = e64.step(a)
         ox, rx, dx, _ = ex.step(a)
     assert np.abs(o64 - ox).max() < (1e-12 if prec == "f64" else 2e-3)
+
+
+@pytest.mark.parametrize("noisy", [False, True])
+def test_fp32_restatement_meets_state_tolerance(noisy):
+    """The fp32 restatement (the kernel's arithmetic, incl. the compensated motor state) tracks the
+    fp64 restatement within BASELINE.json's 1e-4 state tolerance over 240 closed-loop env-steps
+    (metric: parity_util.state_rel_err).  The GPU tests hold the kernel to the same bound."""
+    from parity_util import CLEAN, pd_actions, state_rel_err
+    env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
+    kw = dict(max_episode_steps=0) if noisy else CLEAN
+    n = 128
+    sl = slice(17, 30) if noisy else slice(21, 34)
+    a32 = O.OracleEnv(build_config(env_id, n, seed=11, **kw), "f32")
+    a64 = O.OracleEnv(build_config(env_id, n, seed=11, **kw), "f64")
+    cfg = a64.cfg
+    go, ro = a32.reset(), a64.reset()
+    for _ in range(240):
+        go = a32.step(pd_actions(go[:, sl], cfg.hover_action))[0]
+        ro = a64.step(pd_actions(ro[:, sl], cfg.hover_action))[0]
+    g, r = a32.get_state()[0][:13], a64.get_state()[0][:13]
+    worst = {k: float(v.max()) for k, v in state_rel_err(g, r).items()}
+    assert max(worst.values()) < 1e-4, worst
