@@ -26,7 +26,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
 
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0
+# what one timed env-step writes: the reference's step() returns obs, reward, done and
+# info{cost, disturbance_level} (envs/hover_free.py:138-166, 391-444) plus TimeLimit's truncation
+BOUNDARY_OUTPUTS = ("obs", "rew", "done", "trunc", "cost", "level")   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 ENV_ID = "DroneHoverBulletFreeEnvWithGust-v0"
 
 
@@ -114,12 +117,17 @@ def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
 
 
 def load_traffic(workload_key: str):
-    """Per-launch HBM bytes of the step kernel from rocprofv3 PMC passes (tools/pmc_traffic.py)."""
+    """Per-launch HBM bytes of the step kernel from rocprofv3 PMC passes (tools/pmc_traffic.sh),
+    used only if they were measured on this workload with this very library build (content stamp
+    of libcf2sim.so); otherwise None."""
     p = os.path.join(ROOT, "profiles", "step_kernel_traffic.json")
+    stamp = os.path.join(ROOT, "disturbance-crazyfile-simulation_amd", "cf2sim", "libcf2sim.so.stamp")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload_key:
+        with open(stamp) as f:
+            cur = f.read().strip()
+        if d.get("workload") == workload_key and d.get("library_stamp") == cur:
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -242,7 +250,7 @@ def main():
 
     total_env_steps = n * args.steps * world
     value = total_env_steps / elapsed
-    bytes_per = algorithmic_bytes_per_env_step(env.cfg)
+    bytes_per = algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
     achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
     workload_key = f"{args.env_id}:N={n}"
     traffic = load_traffic(workload_key)

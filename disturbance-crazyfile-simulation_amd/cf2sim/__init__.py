@@ -3,7 +3,8 @@ phoenix_drone_simulation, the package of Hu-Hanyang/disturbance-CrazyFile-simula
 
 * ``BatchedCrazyflieEnv``: N envs per GPU, one fused HIP kernel per env-step (vec_env.py).
 * ``make(id)``: single-env gym-style adapter with the reference's ids, spaces and 4-tuple API.
-* ``HipBatchedPhysics``: physics plugin name usable where the reference selects physics by string.
+* ``cf2sim.physics``: the reference's physics plugin classes (``PybulletPhysicsWithAdversary``, ...,
+  ``HipBatchedPhysics``) over the HIP physics kernel, for ``getattr(module, physics)`` lookups.
 """
 from .config import (ENV_SPECS, OUT_OF_SCOPE_IDS, REFERENCE_IDS, CF2Config, build_config,  # noqa: F401
                      spec_for_id)

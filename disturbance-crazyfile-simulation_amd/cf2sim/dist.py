@@ -22,21 +22,46 @@ def shard_range(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:
     return offset, count
 
 
-def gather_rows(x, group=None):
+def exchange_sizes(n: int, group=None) -> list[int]:
+    """Every rank's row count (one small all_gather; call once per layout, not per step)."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([int(n)], dtype=torch.int64, device=dev)
+    parts = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, t, group=group)
+    return [int(p.item()) for p in parts]
+
+
+def gather_rows(x, group=None, sizes=None, out=None):
     """Concatenate every rank's [n_r, ...] tensor along dim 0 in rank order (all ranks get it).
-    Equal shard sizes use all_gather_into_tensor (one RCCL call on GPUs); ragged shards fall back
-    to a size exchange + padded all_gather."""
+
+    sizes: every rank's n_r (exchange_sizes, cached by the caller); without it one size exchange
+    runs first.  Equal shards gather straight into `out` (allocated if None): one RCCL
+    all_gather_into_tensor on GPUs, an all_gather into views of `out` on gloo; no host sync.
+    Ragged shards pad to the largest shard."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        sizes = exchange_sizes(x.shape[0], group)
+    if len(sizes) != world or sizes[dist.get_rank(group)] != x.shape[0]:
+        raise ValueError("sizes do not match this rank's tensor / the group")
     m = max(sizes)
-    if all(s == m for s in sizes) and dist.get_backend(group) == "nccl":
-        out = torch.empty((world * m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    x = x.contiguous()
+    if x.is_cuda and dist.get_backend(group) != "nccl":
+        # gloo moves host memory: stage through the host (multi-rank rehearsal on shared GPUs)
+        res = gather_rows(x.cpu(), group, sizes=sizes)
+        if out is not None and out.shape == res.shape:
+            return out.copy_(res)
+        return res.to(x.device)
+    if all(s == m for s in sizes):
+        if out is None:
+            out = torch.empty((world * m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if dist.get_backend(group) == "nccl":
+            dist.all_gather_into_tensor(out, x, group=group)
+        else:
+            dist.all_gather(list(out.chunk(world)), x, group=group)
         return out
     pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     pad[: x.shape[0]] = x

@@ -16,7 +16,8 @@ obs, r, done, info = env.step(a)`` (tests/test_envs.py:96-123, algs/iwpg/iwpg.py
 The physics plugin is chosen by name like the reference's ``physics=`` string
 (envs/base.py:223-231): 'PybulletPhysicsWithAdversary', 'PyBulletPhysics' (the Bullet
 restatement), 'SimplePhysics' (physics.py:127-200) and 'HipBatchedPhysics' (whatever the env id
-uses, run by the fused HIP kernel).  Unknown names fail like the reference's assert.
+uses).  Unknown names fail like the reference's assert.  The same names are classes with the
+reference's plugin contract in cf2sim.physics.
 """
 from __future__ import annotations
 
@@ -32,20 +33,16 @@ PHYSICS_PLUGINS = {
 }
 
 
-class HipBatchedPhysics:
-    """Name-level stand-in for the reference's physics classes (envs/physics.py): the physics of
-    this framework is not a separate object but the fused env-step kernel, so selecting it by
-    name only picks the Bullet or Simple restatement the kernel runs."""
-    name = "HipBatchedPhysics"
-
-    @staticmethod
-    def resolve(physics: str | None, default: int) -> int:
-        if physics is None:
-            return default
-        if physics not in PHYSICS_PLUGINS:
-            raise AssertionError(f"Physics={physics} not found.")   # envs/base.py:224-225
-        p = PHYSICS_PLUGINS[physics]
-        return default if p is None else p
+def resolve_physics(physics: str | None, default: int) -> int:
+    """The physics type an env runs for the reference's ``physics=`` string; unknown names fail
+    like the reference's assert (envs/base.py:224-225).  The plugin classes themselves
+    (constructor, set_parameters, step_forward) are in cf2sim.physics."""
+    if physics is None:
+        return default
+    if physics not in PHYSICS_PLUGINS:
+        raise AssertionError(f"Physics={physics} not found.")
+    p = PHYSICS_PLUGINS[physics]
+    return default if p is None else p
 
 
 # registered ids + the framework's extension ids (C2 const wind, C4 gust) of BASELINE.json
@@ -62,7 +59,7 @@ class CrazyflieEnv:
         self.env_id = env_id
         self._kwargs = dict(env_kwargs)
         self._device = device
-        self._physics = HipBatchedPhysics.resolve(physics, self.spec.physics)
+        self._physics = resolve_physics(physics, self.spec.physics)
         self.max_episode_steps = int(self._kwargs.pop("max_episode_steps", 500))
         self._cls = BatchedCrazyflieEnv
         self._seed = int(seed)
@@ -126,4 +123,4 @@ def make(env_id: str, **kwargs) -> CrazyflieEnv:
     return CrazyflieEnv(env_id, **kwargs)
 
 
-__all__ = ["make", "registry", "CrazyflieEnv", "HipBatchedPhysics", "PHYSICS_PLUGINS", "REFERENCE_IDS"]
+__all__ = ["make", "registry", "CrazyflieEnv", "resolve_physics", "PHYSICS_PLUGINS", "REFERENCE_IDS"]

@@ -22,6 +22,26 @@ from .config import CF2Config, DSTB_EXTERNAL, DSTB_HJ, build_config, obs_dim, sp
 from .spaces import make_box
 
 
+def _check_buf(t, name, shape, dtype, device, align=4):
+    """Raise ValueError unless t is a contiguous `dtype` tensor of `shape` on `device` whose data
+    pointer is `align`-byte aligned (the kernel reads and writes these buffers with no bounds
+    information of its own)."""
+    if t is None:
+        return
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name} must be a torch tensor")
+    if t.device != device:
+        raise ValueError(f"{name} must be on {device}, got {t.device}")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.data_ptr() % align:
+        raise ValueError(f"{name} must be {align}-byte aligned")
+
+
 class BatchedCrazyflieEnv:
     def __init__(self, env_id: str, num_envs: int, seed: int = 0, device=None, env_id_offset: int = 0,
                  auto_reset: bool = True, want_final_obs: bool = False, config: CF2Config | None = None,
@@ -76,12 +96,23 @@ class BatchedCrazyflieEnv:
     # ---- HJ tables (distur_gener.py:155 loads fastrack_{level}_15x15.npy each call; here once) ----
     def bind_hj_tables(self, V: torch.Tensor, table_of_level=None):
         """V: [T, 15,15,15,15,15,15] (or [T, 15**6]) float32 device tensor.  table_of_level maps the
-        Boltzmann level index (0.0, 0.1, ..., 2.0) to a row of V; default: fixed-level envs use row 0."""
+        level index (0.0, 0.1, ..., 2.0; distur_gener.py:155 loads fastrack_{level}_15x15.npy per
+        level) to a row of V.  Default: fixed-level envs use row 0; Boltzmann-level envs need one
+        table per level (T == num_levels, identity map) or an explicit map."""
         V = V.reshape(V.shape[0], -1).contiguous().to(self.device, torch.float32)
         if V.shape[1] != 15 ** 6:
             raise ValueError("HJ value tables must be 15^6 grids")
+        nl = int(self.cfg.num_levels)
         if table_of_level is None:
-            table_of_level = [0] * int(self.cfg.num_levels)
+            if int(self.cfg.level_mode) == 1:   # Boltzmann level per episode
+                if V.shape[0] != nl:
+                    raise ValueError(f"this env draws one of {nl} levels per episode: bind {nl} tables (one per "
+                                     f"level) or pass table_of_level explicitly")
+                table_of_level = list(range(nl))
+            else:
+                table_of_level = [0] * nl
+        if len(table_of_level) != nl:
+            raise ValueError(f"table_of_level must have {nl} entries")
         t = (ctypes.c_int32 * int(self.cfg.num_levels))(*[int(x) for x in table_of_level])
         _native.check(self.lib.cf2_bind_hj_tables(self._ctx, V.data_ptr(), V.shape[0], t), "cf2_bind_hj_tables")
         self._tables = V   # keep alive
@@ -95,16 +126,20 @@ class BatchedCrazyflieEnv:
         return self.obs
 
     def step(self, actions: torch.Tensor, dstb: torch.Tensor | None = None):
-        a = actions
+        a = torch.as_tensor(actions)
         if a.device != self.device or a.dtype != torch.float32 or not a.is_contiguous() or a.data_ptr() % 16:
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
+            if a.data_ptr() % 16:
+                a = a.clone()
         if a.shape != (self.num_envs, 4):
             raise ValueError(f"actions must be [{self.num_envs}, 4], got {tuple(a.shape)}")
         d = None
         if self.cfg.disturbance == DSTB_EXTERNAL:
             if dstb is None:
                 raise ValueError("this env takes an external disturbance tensor dstb[N,3]")
-            d = dstb.to(device=self.device, dtype=torch.float32).contiguous()
+            d = torch.as_tensor(dstb).to(device=self.device, dtype=torch.float32).contiguous()
+            if d.shape != (self.num_envs, 3):
+                raise ValueError(f"dstb must be [{self.num_envs}, 3], got {tuple(d.shape)}")
         if self.cfg.disturbance == DSTB_HJ and self._tables is None:
             raise _native.CF2Error("HJ-adversary env: bind value tables with bind_hj_tables() first")
         _native.check(self.lib.cf2_step(
@@ -119,21 +154,31 @@ class BatchedCrazyflieEnv:
     def step_into(self, actions: torch.Tensor, obs_out: torch.Tensor, rew_out: torch.Tensor, done_out: torch.Tensor,
                   trunc_out: torch.Tensor | None = None, cost_out: torch.Tensor | None = None,
                   final_obs_out: torch.Tensor | None = None):
-        """step() writing straight into caller buffers (rollout storage); done/trunc are uint8."""
-        for t in (obs_out, rew_out, done_out, trunc_out, cost_out, final_obs_out):
-            if t is not None and (t.device != self.device or not t.is_contiguous()):
-                raise ValueError("output buffers must be contiguous tensors on the env's device")
-        if done_out.dtype != torch.uint8 or (trunc_out is not None and trunc_out.dtype != torch.uint8):
-            raise ValueError("done/trunc buffers are uint8")
+        """step() writing straight into caller buffers (rollout storage); done/trunc are uint8.
+        Every buffer is checked (device, dtype, shape, contiguity, alignment): the kernel trusts them."""
+        n, od, dev = self.num_envs, self.obs_dim, self.device
+        _check_buf(actions, "actions", (n, 4), torch.float32, dev, 16)
+        _check_buf(obs_out, "obs_out", (n, od), torch.float32, dev, 16)
+        _check_buf(rew_out, "rew_out", (n,), torch.float32, dev)
+        _check_buf(done_out, "done_out", (n,), torch.uint8, dev, 1)
+        _check_buf(trunc_out, "trunc_out", (n,), torch.uint8, dev, 1)
+        _check_buf(cost_out, "cost_out", (n,), torch.float32, dev)
+        _check_buf(final_obs_out, "final_obs_out", (n, od), torch.float32, dev, 8)
+        if self.cfg.disturbance == DSTB_EXTERNAL:
+            raise ValueError("this env takes an external disturbance tensor: use step(actions, dstb)")
         _native.check(self.lib.cf2_step(
             self._ctx, actions.data_ptr(), None, obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
             _native.ptr(trunc_out), _native.ptr(cost_out), None, _native.ptr(final_obs_out), self.stream), "cf2_step")
 
-    def step_raw(self, act_ptr: int, obs_ptr: int | None = None):
-        """Launch one env-step with raw device pointers (benchmark / graph-capture helper)."""
+    def step_raw(self, act_ptr: int, obs_ptr: int | None = None, full_info: bool = True):
+        """Launch one env-step with a raw device pointer to [N, 4] float32 actions (benchmark /
+        graph-capture helper; the pointer is not checked).  full_info: also write the truncation,
+        cost and level outputs step() returns in info (the reference's compute_info runs every step,
+        envs/hover_free.py:138-166)."""
         _native.check(self.lib.cf2_step(
             self._ctx, act_ptr, None, obs_ptr or self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
-            None, None, None, None, self.stream), "cf2_step")
+            self.trunc.data_ptr() if full_info else None, self.cost.data_ptr() if full_info else None,
+            self.level.data_ptr() if full_info else None, None, self.stream), "cf2_step")
 
     # ---- state snapshot ----
     def get_state(self):
@@ -152,8 +197,16 @@ class BatchedCrazyflieEnv:
     def gather_observations(self, group=None) -> torch.Tensor:
         """RCCL all-gather of every rank's obs slab (optional policy-side exchange; the physics
         itself needs no collective).  Returns [sum of N over ranks, obs_dim] in rank order."""
-        from .dist import gather_rows
-        return gather_rows(self.obs, group)
+        from .dist import exchange_sizes, gather_rows
+        key = id(group)
+        if getattr(self, "_gather_key", None) != key:   # shard sizes: exchanged once per group
+            self._gather_sizes = exchange_sizes(self.num_envs, group)
+            self._gather_out = None
+            self._gather_key = key
+        out = gather_rows(self.obs, group, sizes=self._gather_sizes, out=self._gather_out)
+        if len(set(self._gather_sizes)) == 1:
+            self._gather_out = out                        # reused by the next call
+        return out
 
 
 def hj_disturbance(V: torch.Tensor, states: torch.Tensor, level: float, cfg: CF2Config | None = None):

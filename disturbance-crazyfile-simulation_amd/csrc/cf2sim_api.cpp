@@ -259,6 +259,13 @@ int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* o
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
+int cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float time_step, void* stream) {
+    if (!ctx || !act_dev || ((uintptr_t)act_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
+    if (!(time_step < 1.0f)) return CF2_ERR_INVALID_ARG;       // NaN or absurd step
+    const hipError_t e = launch_physics(ctx->P, ctx->sf, act_dev, dstb_dev, time_step, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
 int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems, float* obs_dev, float* rew_dev,
                 uint8_t* done_dev, void* stream) {
     if (!ctx || K < 1 || !act_dev) return CF2_ERR_INVALID_ARG;
@@ -287,27 +294,14 @@ int cf2_hj_disturbance(const cf2_config* cfg, const float* V_dev, const float* s
                        float* dstb_dev, float* uopt_dev, void* stream) {
     if (!cfg || !V_dev || !states_dev || !dstb_dev) return CF2_ERR_INVALID_ARG;
     if (!(level <= 3.0f)) return CF2_ERR_INVALID_ARG;            // assert disturbance <= 3.0 (distur_gener.py:154)
-    // the grid nodes travel in a small per-call device table; no allocation on the hot path:
-    // the table lives in a static device buffer sized for one KTables.
-    static KTables* s_tab = nullptr;
-    static int s_dev = -1;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return hip_fail(e);
-    if (!s_tab || s_dev != dev) {
-        e = hipMalloc((void**)&s_tab, sizeof(KTables));
-        if (e != hipSuccess) return hip_fail(e);
-        s_dev = dev;
-    }
-    KParams P;
-    KTables T;
-    fill_params(cfg, P);
-    fill_tables(cfg, T);
-    e = hipStreamSynchronize((hipStream_t)stream);   // previous users of s_tab on this stream are done
-    if (e == hipSuccess) e = hipMemcpy(s_tab, &T, sizeof(KTables), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e);
-    P.tab = s_tab;
-    e = launch_hj(P, V_dev, states_dev, n, level, dstb_dev, uopt_dev, (hipStream_t)stream);
+    // the grid nodes travel by value in the kernel arguments: no device table, no allocation, no
+    // host synchronisation (the call can be captured into a hipGraph)
+    HjGrid G;
+    for (int d = 0; d < 6; ++d)
+        for (int k = 0; k < HJ_PTS; ++k) G.p[d][k] = cfg->hj_grid_points[d][k];
+    double umax[3];
+    for (int k = 0; k < 3; ++k) umax[k] = cfg->dstb_umax[k];
+    const hipError_t e = launch_hj(G, umax, V_dev, states_dev, n, level, dstb_dev, uopt_dev, (hipStream_t)stream);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 

@@ -31,7 +31,8 @@ enum : int {
 enum : int {
     I_EP_STEP = 0,      // env-steps since reset (TimeLimit, iteration = ep_step * agg)
     I_RNG = 1,          // Philox counter (one per env-step / reset)
-    I_FLAGS = 2,        // bits 0-3 action_idx, 4-5 action_history alias bits, 6 last_action alias
+    I_FLAGS = 2,        // bits 0-3 action_idx, 4-5 action_history alias bits, 6 last_action alias,
+                        // 7 a physics sub-step ran since the reset (prop joints spin)
     I_LEVEL = 3,        // Boltzmann level index / HJ table row
     I_GUST = 4,         // env-steps left in the current gust
     NI = 5
@@ -71,7 +72,7 @@ enum { HJ_PTS = 15, HJ_TABLE = 11390625 };
 enum { PHYS_BULLET_T = 0, PHYS_SIMPLE_T = 1 };
 enum { DSTB_NONE_T = 0, DSTB_EXTERNAL_T = 1, DSTB_UNIFORM_T = 2, DSTB_CONST_T = 3, DSTB_GUST_T = 4, DSTB_HJ_T = 5 };
 enum { LEVEL_FIXED_T = 0, LEVEL_BOLTZMANN_T = 1 };
-enum : uint32_t { TAG_STEP = 1, TAG_RESET = 2 };
+enum : uint32_t { TAG_STEP = 1, TAG_RESET = 2, TAG_PHYS = 3 };
 
 // Kernel parameter block, passed by value (kernarg segment -> scalar loads).
 struct KParams {
@@ -121,10 +122,14 @@ struct StepIO {
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s);
 hipError_t launch_init(const KParams& P, float* sf, hipStream_t s);
+// one physics sub-step of every env (physics plugin step_forward); dt_override <= 0: per-env dt
+hipError_t launch_physics(const KParams& P, float* sf, const float* act, const float* dstb, float dt_override,
+                          hipStream_t s);
 // public SoA snapshot <-> internal AoSoA (to_public = 1: internal -> state_f/state_i)
 hipError_t launch_state_convert(const KParams& P, float* sf, float* state_f, int32_t* state_i, int to_public,
                                 hipStream_t s);
-hipError_t launch_hj(const KParams& P, const float* V, const float* states, uint32_t n, float level, float* dstb,
-                     float* uopt, hipStream_t s);
+struct HjGrid { double p[6][HJ_PTS]; };   // grid nodes by value (hj_kernel kernarg)
+hipError_t launch_hj(const HjGrid& G, const double umax[3], const float* V, const float* states, uint32_t n,
+                     float level, float* dstb, float* uopt, hipStream_t s);
 
 }  // namespace cf2

@@ -294,8 +294,8 @@ __device__ __forceinline__ unsigned hj_signs(const float* __restrict__ V, const 
 }
 
 // every thread of the block takes part (contains a block barrier)
-__device__ __forceinline__ void stage_hj_grid(const KParams& P, double* s_grid) {
-    for (uint32_t k = threadIdx.x; k < 6u * HJ_PTS; k += blockDim.x) s_grid[k] = P.tab->hj_grid[k / HJ_PTS][k % HJ_PTS];
+__device__ __forceinline__ void stage_hj_grid(const double (*src)[HJ_PTS], double* s_grid) {
+    for (uint32_t k = threadIdx.x; k < 6u * HJ_PTS; k += blockDim.x) s_grid[k] = src[k / HJ_PTS][k % HJ_PTS];
     __syncthreads();
 }
 
@@ -311,7 +311,7 @@ struct Env {
     float hact[2][4];
     float dt, m, J[3], k0, k1, B[4], K[4];
     float dstb[3], level;
-    int ep_step, aidx, halias0, halias1, la_view, level_idx, gust_left;
+    int ep_step, aidx, halias0, halias1, la_view, props_on, level_idx, gust_left;
     uint32_t rng;
     float la[4];                    // drone.last_action
 };
@@ -382,6 +382,7 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
     E.rng = (uint32_t)bi(g3.z);
     const int fl = bi(g3.w);
     E.aidx = fl & 15; E.halias0 = (fl >> 4) & 1; E.halias1 = (fl >> 5) & 1; E.la_view = (fl >> 6) & 1;
+    E.props_on = (fl >> 7) & 1;
     E.x[0] = gx.x; E.x[1] = gx.y; E.x[2] = gx.z; E.x[3] = gx.w;
     {
         F4 xl = f4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -485,7 +486,7 @@ __device__ __forceinline__ void store_tail(const KParams& P, float* __restrict__
         for (int k = 0; k < 4; ++k) v[k] = 4 * g + k < OL ? E.obs_prev[4 * g + k] : 0.0f;
         T.st(G_OBSP + g, f4(v[0], v[1], v[2], v[3]));
     }
-    const int fl = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6);
+    const int fl = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6) | (E.props_on << 7);
     T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
 }
 
@@ -902,6 +903,7 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
                             b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
     const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
     E.ep_step = 0;
+    E.props_on = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) E.x[j] = E.xl[j] = 0.0f;
     E.aidx = 0;
@@ -1189,7 +1191,7 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
         float dw = 0.0f;
         if (PHYS == PHYS_BULLET_T && P.num_drones > 1 && P.downwash_on)
             dw = downwash(P, E.p, gid % (uint32_t)P.num_drones);   // mates' positions before this sub-step
-        if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0, dw);
+        if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0 && !E.props_on, dw);
         else simple_substep(P, E, a, on);
         float dummy[17];
         // a sub-step's held measurement reaches an observation only if the final measurement
@@ -1351,7 +1353,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     bool do_reset = false;
     ResetSeed rs;
     __shared__ double s_hjgrid[6 * HJ_PTS];
-    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P, s_hjgrid);     // uniform branch
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     if (P.auto_reset) {
         __syncthreads();     // s_cnt initialised
@@ -1450,6 +1452,44 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 #endif
 }
 
+// One physics sub-step of every env: the physics plugin's step_forward on its own (PyBulletPhysics
+// physics.py:91-124, SimplePhysics :130-200, PybulletPhysicsWithAdversary :213-250): apply_action,
+// force/torque assembly, drag, rigid-body step and readback; no observation, reward or episode
+// counter (cf2_physics_step).  OU normals: Philox block 0 of (rng counter, TAG_PHYS).
+template <bool NOISE, bool DR, int PHYS>
+__global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restrict__ sf, const float* __restrict__ act,
+                                                      const float* __restrict__ dstb, float dt_override) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.N) return;
+    Env E;
+    load_env<NOISE, DR, PHYS>(P, sf, i, E, false, /*with_hist=*/false);
+    const float4 a4 = reinterpret_cast<const float4*>(act)[i];
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+    float d[3] = {0.0f, 0.0f, 0.0f};
+    if (dstb) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) d[k] = dstb[(size_t)i * 3 + k];
+    }
+    if (dt_override > 0.0f) E.dt = dt_override;
+    const Keys K = make_keys(P.key0, P.key1);
+    const Rng g{K, E.rng, P.gid_off + i, TAG_PHYS};
+    float on[4];
+    normals<4>(g, 0, on);
+    if (PHYS == PHYS_BULLET_T) {
+        bullet_substep(P, E, a, d, on, E.ep_step == 0 && !E.props_on);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.wb[k] = E.w[k];
+        simple_substep(P, E, a, on);
+    }
+    E.props_on = 1;
+    E.rng += 1;
+    store_core<NOISE, DR, PHYS>(P, sf, i, E);
+    const Tile T(sf, P.N, i);
+    const int fl = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6) | (E.props_on << 7);
+    T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
+}
+
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __global__ void __launch_bounds__(256) reset_kernel(KParams P0, float* __restrict__ sf,
                                                     const uint8_t* __restrict__ mask, float* __restrict__ obs) {
@@ -1538,10 +1578,12 @@ __global__ void state_convert_kernel(uint32_t N, float* __restrict__ sf, float* 
     }
 }
 
-__global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* __restrict__ states, uint32_t n,
-                          float level, float* __restrict__ dstb, float* __restrict__ uopt) {
+// the grid nodes arrive by value in the kernarg segment (720 B): the stand-alone call needs no
+// device table, allocation or host synchronisation
+__global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, const float* __restrict__ states,
+                          uint32_t n, float level, float* __restrict__ dstb, float* __restrict__ uopt) {
     __shared__ double s_grid[6 * HJ_PTS];
-    stage_hj_grid(P, s_grid);
+    stage_hj_grid(G.p, s_grid);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double st[6];
@@ -1550,7 +1592,7 @@ __global__ void hj_kernel(KParams P, const float* __restrict__ V, const float* _
     const unsigned bits = hj_signs(V, st, s_grid);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double um = P.umax_d[k];
+        const double um = k == 0 ? umax.x : (k == 1 ? umax.y : umax.z);
         const double dm = (double)level * um;
         dstb[(size_t)i * 3 + k] = (float)((bits >> k) & 1u ? -dm : dm);
         if (uopt) uopt[(size_t)i * 3 + k] = (float)((bits >> k) & 1u ? -um : um);
@@ -1639,6 +1681,26 @@ hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     CF2_DISPATCH(launch_reset_t, P, sf, mask, obs, s);
 }
+template <bool NOISE, bool DR, int PHYS>
+static hipError_t launch_physics_t(const KParams& P, float* sf, const float* act, const float* dstb, float dt_override,
+                                   hipStream_t s) {
+    const dim3 grid((P.N + 255) / 256), block(256);
+    hipLaunchKernelGGL((physics_kernel<NOISE, DR, PHYS>), grid, block, 0, s, P, sf, act, dstb, dt_override);
+    return hipGetLastError();
+}
+hipError_t launch_physics(const KParams& P, float* sf, const float* act, const float* dstb, float dt_override,
+                          hipStream_t s) {
+    switch ((P.noise ? 4 : 0) | (P.dr ? 2 : 0) | (P.phys == PHYS_SIMPLE_T ? 1 : 0)) {
+    case 0: return launch_physics_t<false, false, PHYS_BULLET_T>(P, sf, act, dstb, dt_override, s);
+    case 1: return launch_physics_t<false, false, PHYS_SIMPLE_T>(P, sf, act, dstb, dt_override, s);
+    case 2: return launch_physics_t<false, true, PHYS_BULLET_T>(P, sf, act, dstb, dt_override, s);
+    case 3: return launch_physics_t<false, true, PHYS_SIMPLE_T>(P, sf, act, dstb, dt_override, s);
+    case 4: return launch_physics_t<true, false, PHYS_BULLET_T>(P, sf, act, dstb, dt_override, s);
+    case 5: return launch_physics_t<true, false, PHYS_SIMPLE_T>(P, sf, act, dstb, dt_override, s);
+    case 6: return launch_physics_t<true, true, PHYS_BULLET_T>(P, sf, act, dstb, dt_override, s);
+    default: return launch_physics_t<true, true, PHYS_SIMPLE_T>(P, sf, act, dstb, dt_override, s);
+    }
+}
 hipError_t launch_state_convert(const KParams& P, float* sf, float* state_f, int32_t* state_i, int to_public,
                                 hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
@@ -1650,11 +1712,12 @@ hipError_t launch_init(const KParams& P, float* sf, hipStream_t s) {
     hipLaunchKernelGGL(init_kernel, grid, block, 0, s, P, sf);
     return hipGetLastError();
 }
-hipError_t launch_hj(const KParams& P, const float* V, const float* states, uint32_t n, float level, float* dstb,
-                     float* uopt, hipStream_t s) {
+hipError_t launch_hj(const HjGrid& G, const double umax[3], const float* V, const float* states, uint32_t n,
+                     float level, float* dstb, float* uopt, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const dim3 grid((n + 255) / 256), block(256);
-    hipLaunchKernelGGL(hj_kernel, grid, block, 0, s, P, V, states, n, level, dstb, uopt);
+    const double3 um = make_double3(umax[0], umax[1], umax[2]);
+    hipLaunchKernelGGL(hj_kernel, grid, block, 0, s, G, um, V, states, n, level, dstb, uopt);
     return hipGetLastError();
 }
 

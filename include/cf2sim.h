@@ -208,6 +208,16 @@ int  cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev,
               float* obs_dev, float* rew_dev, uint8_t* done_dev, uint8_t* trunc_dev,
               float* cost_dev, float* level_dev, float* final_obs_dev, void* stream);
 
+/* One physics sub-step of every env, without the env-step around it: the physics plugin's
+ * step_forward (PyBulletPhysics.step_forward physics.py:91-124, SimplePhysics :130-200,
+ * PybulletPhysicsWithAdversary.step_forward :213-250; plugin construction envs/base.py:223-232):
+ * apply_action (latency ring, PWM, OU thrust noise, motor dynamics), motor forces + yaw torque,
+ * adversary torques dstb[0], dstb[1] (dstb_dev [N,3] or NULL = none), drag, the rigid-body step
+ * and update_information.  No observation, reward, TimeLimit or auto-reset.  time_step > 0
+ * overrides every env's dt for this call (BasePhysics.set_parameters physics.py:60-68); <= 0
+ * uses the per-env dt (domain randomisation).  act_dev [N,4] 16-B aligned. */
+int  cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float time_step, void* stream);
+
 /* K consecutive env-steps with actions act_dev[k] = act_dev + k*N*4 (rollout mode); outputs
  * are those of the last step.  Equivalent to K cf2_step calls; one launch per step. */
 int  cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems,

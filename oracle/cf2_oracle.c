@@ -69,7 +69,7 @@ void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint3
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-enum { TAG_STEP = 1, TAG_RESET = 2 };
+enum { TAG_STEP = 1, TAG_RESET = 2, TAG_PHYS = 3 };
 
 typedef struct { uint32_t key[2]; uint32_t gid, ctr, tag; } rng_t;
 
@@ -229,6 +229,7 @@ typedef struct {
     int aidx;
     REAL last_action[4];
     int last_action_is_view;            /* drone.last_action aliases action_buffer[-1] */
+    int props_on;                       /* a physics sub-step ran since the reset (prop joints spin) */
     /* per-env params (DR) */
     REAL dt, m, J[3], k0, k1, A[4], B[4], K[4];
     /* sensor */
@@ -679,6 +680,7 @@ static void reset_env(orc_ctx* X, int i, REAL* obs) {
 
     E->iteration = 0;
     E->ep_step = 0;
+    E->props_on = 0;
     /* drone.reset() agents.py:377-386 */
     for (int j = 0; j < 4; ++j) E->x[j] = E->xl[j] = R(0.0);
     E->aidx = 0;
@@ -921,7 +923,7 @@ void orc_step(void* h, const float* act, const double* dstb_ext, double* obs, do
           const REAL dw = (M > 1 && c->downwash_on) ? orc_downwash(c, pos[m], (const REAL(*)[3])pos, M, m) : R(0.0);
           REAL ou_n[4];
           rng_normals(&g_g[m], 1 + (uint32_t)s, 4, ou_n);
-          if (c->physics == CF2_PHYS_BULLET) bullet_substep(X, E, a_g[m], d_g[m], ou_n, E->ep_step == 0 && s == 0, dw);
+          if (c->physics == CF2_PHYS_BULLET) bullet_substep(X, E, a_g[m], d_g[m], ou_n, E->ep_step == 0 && s == 0 && !E->props_on, dw);
           else simple_substep(X, E, a_g[m], ou_n);
           REAL dummy[17];
           compute_observation(X, E, &g_g[m], 8 + 8 * (uint32_t)s, dummy);
@@ -959,6 +961,32 @@ void orc_step(void* h, const float* act, const double* dstb_ext, double* obs, do
     }
 }
 
+/* One physics sub-step of every env: the physics plugin's step_forward on its own
+ * (PyBulletPhysics physics.py:91-124, SimplePhysics :130-200, PybulletPhysicsWithAdversary
+ * :213-250), i.e. apply_action + force/torque assembly + drag + rigid-body step + readback, with no
+ * observation, reward or counters around it (cf2_physics_step).  OU normals: Philox block 0 of
+ * (rng counter, TAG_PHYS); the counter advances once per call.  dt_override > 0 replaces the
+ * per-env time step for this call (BasePhysics.set_parameters physics.py:60-68). */
+void orc_physics_step(void* h, const float* act, const double* dstb, double dt_override) {
+    orc_ctx* X = (orc_ctx*)h;
+    const cf2_config* c = &X->cfg;
+    for (int i = 0; i < X->n; ++i) {
+        orc_env* E = &X->e[i];
+        rng_t g = mk_rng(X, i, TAG_PHYS);
+        REAL a[4], d[3] = {R(0.0), R(0.0), R(0.0)}, ou_n[4];
+        for (int k = 0; k < 4; ++k) a[k] = R(act[(size_t)i * 4 + k]);
+        if (dstb) for (int k = 0; k < 3; ++k) d[k] = R(dstb[(size_t)i * 3 + k]);
+        const REAL dt_saved = E->dt;
+        if (dt_override > 0.0) E->dt = R(dt_override);
+        rng_normals(&g, 0, 4, ou_n);
+        if (c->physics == CF2_PHYS_BULLET) bullet_substep(X, E, a, d, ou_n, E->ep_step == 0 && !E->props_on, R(0.0));
+        else simple_substep(X, E, a, ou_n);
+        E->dt = dt_saved;
+        E->props_on = 1;
+        E->rng_ctr += 1;
+    }
+}
+
 /* SoA snapshot in the HIP kernel's layout (DESIGN.md "State layout"). */
 #define NF 108
 #define NI 5
@@ -992,7 +1020,7 @@ void orc_get_state(void* h, double* sf, int32_t* si) {
         for (int k = 0; k < NF; ++k) sf[(size_t)k * N + i] = f[k];
         si[0 * N + i] = E->ep_step;
         si[1 * N + i] = (int32_t)E->rng_ctr;
-        si[2 * N + i] = (E->aidx & 15) | (E->halias[0] << 4) | (E->halias[1] << 5) | (E->last_action_is_view << 6);
+        si[2 * N + i] = (E->aidx & 15) | (E->halias[0] << 4) | (E->halias[1] << 5) | (E->last_action_is_view << 6) | (E->props_on << 7);
         si[3 * N + i] = E->level_idx;
         si[4 * N + i] = E->gust_left;
     }
@@ -1040,6 +1068,7 @@ void orc_set_state(void* h, const double* sf, const int32_t* si) {
         E->halias[0] = (fl >> 4) & 1;
         E->halias[1] = (fl >> 5) & 1;
         E->last_action_is_view = (fl >> 6) & 1;
+        E->props_on = (fl >> 7) & 1;
         for (int k = 0; k < 4; ++k) E->last_action[k] = E->abuf[c->buf_size - 1][k];
         E->level_idx = si[3 * N + i];
         E->gust_left = si[4 * N + i];

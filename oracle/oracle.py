@@ -46,6 +46,7 @@ class _Lib:
             lib.orc_set_threads.argtypes = [_P, ctypes.c_int]
             lib.orc_reset.argtypes = [_P, _u8p, _dp]
             lib.orc_step.argtypes = [_P, _fp, _dp, _dp, _dp, _u8p, _u8p, _dp, _dp, _dp]
+            lib.orc_physics_step.argtypes = [_P, _fp, _dp, ctypes.c_double]
             lib.orc_get_state.argtypes = [_P, _dp, _ip]
             lib.orc_set_state.argtypes = [_P, _dp, _ip]
             lib.orc_bind_tables.argtypes = [_P, _fp, ctypes.c_int, _ip]
@@ -141,6 +142,12 @@ class OracleEnv:
         if want_final:
             info["final_obs"] = fin
         return obs, rew, done.astype(bool), info
+
+    def physics_step(self, act, dstb=None, time_step=0.0):
+        """One physics sub-step of every env (orc_physics_step; the plugin's step_forward)."""
+        act = np.ascontiguousarray(act, dtype=np.float32).reshape(self.n, 4)
+        d = None if dstb is None else np.ascontiguousarray(dstb, dtype=np.float64).reshape(self.n, 3)
+        self.lib.orc_physics_step(self.h, _ptr(act, _fp), _ptr(d, _dp), float(time_step))
 
     def get_state(self):
         sf = np.zeros((NF, self.n), np.float64)

@@ -84,3 +84,33 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     ref_obs, ref_rew = _single_process()
     np.testing.assert_array_equal(got["obs"], ref_obs)
     np.testing.assert_array_equal(got["rew"], ref_rew)
+
+
+def _gather_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "disturbance-crazyfile-simulation_amd"))
+    from cf2sim.dist import exchange_sizes, gather_rows
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sizes = exchange_sizes(3, None)                       # once per layout
+    out = None
+    res = []
+    for t in range(4):                                    # per step: no size exchange, buffer reused
+        x = torch.full((3, 2), float(10 * rank + t))
+        out = gather_rows(x, sizes=sizes, out=out)
+        res.append(out.clone())
+    if rank == 0:
+        np.save(os.path.join(out_dir, "g.npy"), torch.stack(res).numpy())
+    with pytest.raises(ValueError):
+        gather_rows(torch.zeros(2, 2), sizes=sizes)       # sizes that do not match the tensor
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_rows_with_cached_sizes(tmp_path):
+    mp.spawn(_gather_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    g = np.load(tmp_path / "g.npy")
+    for t in range(4):
+        np.testing.assert_array_equal(g[t, :3], t)
+        np.testing.assert_array_equal(g[t, 3:], 10 + t)

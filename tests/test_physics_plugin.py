@@ -1,0 +1,111 @@
+"""The physics-plugin contract: the reference builds its physics by
+name around the env's drone (envs/base.py:223-232) and drives it with step_forward(action[, dstb])
+and set_parameters(time_step, number_solver_iterations) (envs/physics.py:8-76, 79-124, 127-200,
+202-250).  cf2sim.physics mirrors that contract over the HIP physics kernel (cf2_physics_step);
+the GPU tests step it through the reference's getattr lookup against the CPU restatement's
+orc_physics_step (same sub-step, same Philox OU draws)."""
+import inspect
+
+import numpy as np
+import pytest
+
+import oracle as O
+from cf2sim.config import build_config
+
+NAMES = ["PyBulletPhysics", "PybulletPhysicsWithAdversary", "SimplePhysics", "HipBatchedPhysics"]
+
+
+def test_plugin_classes_resolve_by_name_with_reference_signatures():
+    import cf2sim.physics as phoenix_physics
+    for name in NAMES:
+        assert hasattr(phoenix_physics, name)                     # base.py:224-225
+        cls = getattr(phoenix_physics, name)                      # base.py:226
+        params = list(inspect.signature(cls.__init__).parameters)
+        assert params[:4] == ["self", "drone", "bc", "time_step"]  # physics.py:11-19
+        assert {"gravity", "number_solver_iterations", "use_ground_effect"} <= set(params)
+        assert list(inspect.signature(cls.set_parameters).parameters)[:3] == ["self", "time_step",
+                                                                            "number_solver_iterations"]
+        assert callable(cls.step_forward)
+    with pytest.raises(AssertionError, match="not found"):
+        phoenix_physics.resolve_physics("MuJoCoPhysics", 0)
+    with pytest.raises(TypeError):
+        phoenix_physics.PyBulletPhysics(object(), None, time_step=0.005)
+
+
+def _pair(env_id, n, seed, kw):
+    from cf2sim.physics import BatchedDrone
+    drone = BatchedDrone(num_drones=n, seed=seed, env_id=env_id, **kw)
+    ref = O.OracleEnv(build_config(env_id, n, seed=seed, auto_reset=False, max_episode_steps=0, **kw), "f32")
+    return drone, ref
+
+
+def _err(g, r):
+    return float((np.abs(g - r) / (1.0 + np.abs(r))).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,env_id,kw,time_step", [
+    ("PybulletPhysicsWithAdversary", "DroneHoverBulletFreeEnvWithoutAdversary-v0", {}, None),
+    ("PyBulletPhysics", "DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(domain_randomization=-1), 0.005),
+    ("SimplePhysics", "DroneHoverSimpleEnv-v0", {}, None),
+    ("HipBatchedPhysics", "DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(latency=0.0), 0.004),
+])
+def test_plugin_step_forward_matches_restatement(gpu, name, env_id, kw, time_step):
+    """getattr(cf2sim.physics, name)(drone, bc, time_step=...) stepped 60 sub-steps with random
+    actions (and adversary torques where the class takes them) vs the fp32 restatement: state
+    within 2e-5 mixed abs/rel (the fused-FMA / approximate-transcendental differences of the
+    kernel), counters exact."""
+    import torch
+    import cf2sim.physics as phoenix_physics
+    n, seed = 256, 5
+    drone, ref = _pair(env_id, n, seed, kw)
+    phys = getattr(phoenix_physics, name)(drone, None, time_step=time_step)
+    phys.set_parameters(time_step=time_step, number_solver_iterations=5)
+    drone.reset()
+    ref.reset()
+    rng = np.random.default_rng(1)
+    takes_dstb = name in ("PybulletPhysicsWithAdversary", "HipBatchedPhysics")
+    for _ in range(60):
+        a = (rng.uniform(-1, 1, (n, 4)) * 0.3 + 0.1111).astype(np.float32)
+        d = (rng.uniform(-1, 1, (n, 3)) * 2e-4).astype(np.float32) if takes_dstb else None
+        at = torch.from_numpy(a).cuda()
+        if takes_dstb:
+            phys.step_forward(at, torch.from_numpy(d).cuda())
+        else:
+            phys.step_forward(at)
+        ref.physics_step(a, d, time_step or 0.0)
+    gsf, gsi = drone.env.get_state()
+    rsf, rsi = ref.get_state()
+    gsf, gsi = gsf.cpu().numpy(), gsi.cpu().numpy()
+    L = drone.env.layout
+    fields = list(range(0, 13)) + list(range(L.f_motor, L.f_motor + 8))
+    assert _err(gsf[fields], rsf[fields]) < 2e-5
+    np.testing.assert_array_equal(gsi[:3], rsi[:3])        # episode step, RNG counter, flags
+    # the agent attributes read back from the snapshot
+    np.testing.assert_allclose(drone.xyz.cpu().numpy(), rsf[0:3].T, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(drone.quaternion.cpu().numpy(), rsf[3:7].T, rtol=0, atol=2e-5)
+    if name != "SimplePhysics":
+        rpy = drone.rpy.cpu().numpy()
+        q = rsf[3:7].T
+        x, y, z, w = q.T
+        roll = np.arctan2(2 * (y * z + w * x), w * w - x * x - y * y + z * z)
+        np.testing.assert_allclose(rpy[:, 0], roll, atol=1e-4)
+    drone.close()
+    ref.close()
+
+
+@pytest.mark.gpu
+def test_plugin_rejects_mismatched_drone_and_bad_inputs(gpu):
+    import torch
+    import cf2sim.physics as phoenix_physics
+    drone = phoenix_physics.BatchedDrone("cf21x_bullet", num_drones=8)
+    with pytest.raises(ValueError):
+        phoenix_physics.SimplePhysics(drone, None, time_step=0.005)
+    phys = phoenix_physics.PybulletPhysicsWithAdversary(drone, None, time_step=0.005)
+    with pytest.raises(ValueError):
+        phys.step_forward(torch.zeros(8, 3, device="cuda"), torch.zeros(8, 3, device="cuda"))
+    with pytest.raises(ValueError):
+        phys.step_forward(torch.zeros(8, 4, device="cuda"), torch.zeros(8, device="cuda"))
+    with pytest.raises(NotImplementedError):
+        phoenix_physics.PyBulletPhysics(drone, None, time_step=0.005, use_ground_effect=True)
+    drone.close()

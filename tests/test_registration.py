@@ -29,12 +29,12 @@ def test_unknown_id_raises():
 
 
 def test_physics_plugin_names():
-    assert R.HipBatchedPhysics.resolve(None, PHYS_BULLET) == PHYS_BULLET
-    assert R.HipBatchedPhysics.resolve("HipBatchedPhysics", PHYS_SIMPLE) == PHYS_SIMPLE
-    assert R.HipBatchedPhysics.resolve("SimplePhysics", PHYS_BULLET) == PHYS_SIMPLE
-    assert R.HipBatchedPhysics.resolve("PybulletPhysicsWithAdversary", PHYS_SIMPLE) == PHYS_BULLET
+    assert R.resolve_physics(None, PHYS_BULLET) == PHYS_BULLET
+    assert R.resolve_physics("HipBatchedPhysics", PHYS_SIMPLE) == PHYS_SIMPLE
+    assert R.resolve_physics("SimplePhysics", PHYS_BULLET) == PHYS_SIMPLE
+    assert R.resolve_physics("PybulletPhysicsWithAdversary", PHYS_SIMPLE) == PHYS_BULLET
     with pytest.raises(AssertionError):                 # envs/base.py:224-225
-        R.HipBatchedPhysics.resolve("MuJoCoPhysics", PHYS_BULLET)
+        R.resolve_physics("MuJoCoPhysics", PHYS_BULLET)
 
 
 def test_make_without_gpu_fails_loudly():

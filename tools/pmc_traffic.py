@@ -38,6 +38,7 @@ res = {
     "calibration": {"kernel": "tools/membench.hip SoA R84 W72 +obs34 (4 B/lane)", "known_read_bytes": calib_rd,
                     "known_write_bytes": calib_wr, "FETCH_SIZE_bytes": c_f, "WRITE_SIZE_bytes": c_w,
                     "read_factor": kr, "write_factor": kw},
+    "library_stamp": open(os.path.join(ROOT, "disturbance-crazyfile-simulation_amd", "cf2sim", "libcf2sim.so.stamp")).read().strip(),
     "note": "FETCH_SIZE/WRITE_SIZE count L2 memory-side requests; Infinity-Cache hits are counted "
             "(MI355X_MICROARCH.md HBM section), so this is L2->fabric traffic.",
 }
