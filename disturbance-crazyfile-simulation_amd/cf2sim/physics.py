@@ -49,8 +49,15 @@ class BatchedDrone:
     agents (DroneBaseEnv.reset envs/base.py:420-464 incl. task reset and domain randomisation)."""
 
     def __init__(self, drone_model: str = "cf21x_bullet", num_drones: int = 1, seed: int = 0, device=None,
-                 env_id: str | None = None, **env_kwargs):
+                 env_id: str | None = None, config=None, **env_kwargs):
+        """config: a full cf2sim.config.CF2Config (num_envs = the number of drones) instead of the
+        env id's defaults plus env_kwargs."""
         from .vec_env import BatchedCrazyflieEnv
+        if config is not None:
+            self.env = BatchedCrazyflieEnv(env_id or "", int(config.num_envs), device=device, config=config)
+            self.drone_model = "cf21x_bullet" if self.physics_type == PHYS_BULLET else "cf21x_sys_eq"
+            self.num_drones = self.env.num_envs
+            return
         if env_id is None:
             if drone_model not in _DRONE_MODEL_ENV:
                 raise NotImplementedError(f"drone_model={drone_model}")   # envs/base.py:214

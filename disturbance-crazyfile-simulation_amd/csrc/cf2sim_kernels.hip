@@ -563,7 +563,10 @@ __device__ __forceinline__ void apply_action(const KParams& P, Env& E, const flo
         } else {
             noisy = (1.0f + E.ou[j]) * tn;
         }
-        f[j] = E.K[j] * clampf(noisy, 0.0f, 1.0f);
+        // rounded on its own (no FMA contraction into the mixer sums below): equal motor forces then
+        // cancel exactly in the roll/pitch torques, as in the reference; a contracted product would
+        // leave a one-sided ulp torque every sub-step (a systematic attitude drift in hover)
+        f[j] = opaque(E.K[j] * clampf(noisy, 0.0f, 1.0f));
     }
     float t[4];
 #pragma unroll
