@@ -74,7 +74,8 @@ def load() -> ctypes.CDLL:
     lib.cf2_policy_weights_count.argtypes = [u32]
     lib.cf2_policy_forward.argtypes = [vp, u32, u32, vp, ctypes.c_uint64, u32, u32, ctypes.c_int, vp, vp, vp, vp]
     lib.cf2_value_forward_masked.argtypes = [vp, u32, u32, vp, vp, vp, vp]
-    lib.cf2_gae.argtypes = [u32, u32, vp, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float, vp, vp, vp]
+    lib.cf2_gae.argtypes = [u32, u32, vp, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp,
+                            vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
                         "cf2_policy_weights_count"):

@@ -12,7 +12,14 @@ Reference behaviour restated (paths relative to phoenix_drone_simulation/):
   last_val = 0 on a terminal state and V(s) on a time-out or at the end of the epoch.
 * ``finish_path`` / ``calculate_adv_and_value_targets`` (algs/core.py:459-535): GAE
   A_t = sum_k (gamma*lam)^k delta_{t+k}, delta_t = r_t + gamma V_{t+1} - V_t, value targets
-  A_t + V_t, over each episode slice.
+  A_t + V_t, over each episode slice; with reward scaling (IWPG default use_reward_scaling=True,
+  algs/iwpg/iwpg.py:56) the rewards entering delta are clip(r / (ret_std + 1e-5), -10, 10)
+  (core.py:522-529) and the unscaled discounted returns feed the return statistics.
+* Observation standardisation (IWPG default use_standardized_obs=True, iwpg.py:59):
+  ``ActorCritic.step`` feeds (obs - mean) / (std + 1e-5) to both networks (core.py:383-388);
+  the statistics are ``OnlineMeanStd`` (utils/online_mean_std.py), updated once per epoch by
+  ``update_running_statistics`` (iwpg.py:412-420).  The fused kernel takes the standardisation
+  folded into the first layer of each network (pack_policy_weights).
 
 Here N envs run in lock step with on-device auto-reset, so episode boundaries differ per env.
 ``gae`` evaluates the same recursion over a [T, N] buffer with per-env masks:
@@ -43,15 +50,76 @@ def _mlp(sizes, activation, output_activation=nn.Identity):
 _ACT = {"relu": nn.ReLU, "tanh": nn.Tanh, "identity": nn.Identity}
 
 
+class OnlineMeanStd(nn.Module):
+    """Running mean / standard deviation (utils/online_mean_std.py): the incremental update of
+    Chan et al. over batches, single process (the reference's MPI averages are the identity with
+    one process; across GPUs, batches of every rank can be concatenated before update())."""
+
+    def __init__(self, epsilon: float = 1e-5, shape=()):
+        super().__init__()
+        self.register_buffer("mean", torch.zeros(*shape))
+        self.register_buffer("std", torch.ones(*shape))
+        self.register_buffer("count", torch.zeros(1))
+        self.eps = epsilon
+        self.bound = 10
+        self.shape = tuple(shape)
+
+    def forward(self, x, subtract_mean: bool = True, clip: bool = False):
+        x_new = (x - self.mean) / (self.std + self.eps) if subtract_mean else x / (self.std + self.eps)
+        return torch.clamp(x_new, -self.bound, self.bound) if clip else x_new
+
+    @torch.no_grad()
+    def update(self, x: torch.Tensor) -> None:
+        x = torch.as_tensor(x, dtype=torch.float32, device=self.mean.device)
+        if self.shape[0] == 1:
+            if x.dim() != 1:
+                raise ValueError(f"expected a 1-d batch, got {tuple(x.shape)}")
+            x = x.view(-1, 1)
+        elif x.dim() != 2 or x.shape[1] != self.shape[0]:
+            raise ValueError(f"expected [B, {self.shape[0]}], got {tuple(x.shape)}")
+        n_b = x.shape[0]
+        n_a = self.count.clone()
+        n_ab = self.count + n_b
+        delta = x.mean(dim=0) - self.mean
+        mean_new = self.mean + delta * n_b / n_ab
+        batch_var = torch.mean((x - mean_new) ** 2, dim=0)
+        m2_ab = n_a * torch.square(self.std) + n_b * batch_var + delta ** 2 * (n_a * n_b / n_ab)
+        self.mean.copy_(mean_new)
+        self.count.copy_(n_ab)
+        self.std.copy_(torch.sqrt(m2_ab / n_ab))
+
+
 class MLPActorCritic(nn.Module):
-    """Gaussian MLP policy + MLP value function with the reference's PPO defaults."""
+    """Gaussian MLP policy + MLP value function with the reference's PPO defaults, the
+    observation standardisation and the return statistics of reward scaling."""
 
     def __init__(self, obs_dim: int = 34, act_dim: int = 4, pi_hidden=(50, 50), pi_activation="relu",
-                 v_hidden=(64, 64), v_activation="tanh", log_std: float = math.log(0.5)):
+                 v_hidden=(64, 64), v_activation="tanh", log_std: float = math.log(0.5),
+                 use_standardized_obs: bool = True, use_scaled_rewards: bool = True):
         super().__init__()
         self.pi_net = _mlp([obs_dim, *pi_hidden, act_dim], _ACT[pi_activation])
         self.v_net = _mlp([obs_dim, *v_hidden, 1], _ACT[v_activation])
         self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std)), requires_grad=False)
+        self.obs_oms = OnlineMeanStd(shape=(obs_dim,)) if use_standardized_obs else None
+        self.ret_oms = OnlineMeanStd(shape=(1,)) if use_scaled_rewards else None
+
+    def load_reference_state_dict(self, sd: dict):
+        """Load a state_dict of the reference's ActorCritic (keys pi.net.{0,2,4}.*, pi.log_std,
+        v.net.{0,2,4}.*, obs_oms.*, ret_oms.*; algs/core.py:314-364)."""
+        def t(k):
+            return torch.as_tensor(sd[k], dtype=torch.float32)
+        with torch.no_grad():
+            for mine, ref in ((self.pi_net, "pi.net"), (self.v_net, "v.net")):
+                for i in (0, 2, 4):
+                    mine[i].weight.copy_(t(f"{ref}.{i}.weight"))
+                    mine[i].bias.copy_(t(f"{ref}.{i}.bias"))
+            self.log_std.copy_(t("pi.log_std"))
+            for name, oms in (("obs_oms", self.obs_oms), ("ret_oms", self.ret_oms)):
+                if oms is not None and f"{name}.mean" in sd:
+                    oms.mean.copy_(t(f"{name}.mean")); oms.std.copy_(t(f"{name}.std")); oms.count.copy_(t(f"{name}.count"))
+
+    def normalize(self, obs: torch.Tensor) -> torch.Tensor:
+        return self.obs_oms(obs) if self.obs_oms is not None else obs
 
     def set_log_std(self, frac: float):
         """Exploration-noise annealing of core.py:274-281 (std 0.5 -> 0.01 as frac goes 1 -> 0)."""
@@ -62,6 +130,7 @@ class MLPActorCritic(nn.Module):
     @torch.no_grad()
     def step(self, obs: torch.Tensor, generator: torch.Generator | None = None, deterministic: bool = False):
         """(action, value, log_prob) for a batch of observations (core.py:371-395)."""
+        obs = self.normalize(obs)
         mu = self.pi_net(obs)
         v = self.v_net(obs).squeeze(-1)
         if deterministic:
@@ -75,12 +144,42 @@ class MLPActorCritic(nn.Module):
 
     @torch.no_grad()
     def value(self, obs: torch.Tensor) -> torch.Tensor:
-        return self.v_net(obs).squeeze(-1)
+        return self.v_net(self.normalize(obs)).squeeze(-1)
+
+    @torch.no_grad()
+    def log_prob(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
+        """Normal(mu(obs), std).log_prob(act).sum(-1) (core.py:253-259)."""
+        mu = self.pi_net(self.normalize(obs))
+        return torch.distributions.Normal(mu, self.log_std.exp()).log_prob(act).sum(-1)
+
+
+def update_running_statistics(ac: MLPActorCritic, rollout: "Rollout", fused: "FusedActorCritic | None" = None):
+    """IWPGAlgorithm.update_running_statistics (iwpg.py:412-420) on a whole batched rollout: the raw
+    observations update the observation statistics, the discounted returns the return statistics.
+    A FusedActorCritic over `ac` is re-synced (its first layers carry the folded standardisation)."""
+    if ac.obs_oms is not None:
+        ac.obs_oms.update(rollout.obs.reshape(-1, rollout.obs.shape[-1]))
+    if ac.ret_oms is not None:
+        ac.ret_oms.update(rollout.discounted_ret.reshape(-1))
+    if fused is not None:
+        fused.sync()
+
+
+def _folded_first_layer(lin: nn.Linear, oms: OnlineMeanStd | None):
+    """W' x + b' == W ((x - mean) / (std + eps)) + b: the observation standardisation folded into
+    a first layer (fp64 on the host, then fp32)."""
+    W, b = lin.weight.detach().double(), lin.bias.detach().double()
+    if oms is None:
+        return W, b
+    den = oms.std.detach().double() + oms.eps
+    Wf = W / den[None, :]
+    return Wf, b - Wf @ oms.mean.detach().double()
 
 
 def pack_policy_weights(ac: MLPActorCritic) -> torch.Tensor:
     """Flatten an MLPActorCritic with the default shapes into the weight block of
-    cf2_policy_forward (input-major matrices: pi W1 b1 W2 b2 W3 b3 log_std, then v W1 b1 W2 b2 W3 b3)."""
+    cf2_policy_forward (input-major matrices: pi W1 b1 W2 b2 W3 b3 log_std, then v W1 b1 W2 b2 W3 b3).
+    The observation standardisation is folded into pi W1/b1 and v W1/b1."""
     lin_pi = [m for m in ac.pi_net if isinstance(m, nn.Linear)]
     lin_v = [m for m in ac.v_net if isinstance(m, nn.Linear)]
     shapes = [(m.out_features, m.in_features) for m in lin_pi] + [(m.out_features, m.in_features) for m in lin_v]
@@ -88,11 +187,13 @@ def pack_policy_weights(ac: MLPActorCritic) -> torch.Tensor:
     if shapes != [(50, d), (50, 50), (4, 50), (64, d), (64, 64), (1, 64)] or d not in (34, 42):
         raise ValueError(f"the fused kernel implements the PPO default networks only, got {shapes}")
     parts = []
-    for m in lin_pi:
-        parts += [m.weight.detach().t().reshape(-1), m.bias.detach()]
-    parts.append(ac.log_std.detach())
-    for m in lin_v:
-        parts += [m.weight.detach().t().reshape(-1), m.bias.detach()]
+    for lins in (lin_pi, lin_v):
+        W1, b1 = _folded_first_layer(lins[0], ac.obs_oms)
+        parts += [W1.t().reshape(-1), b1]
+        for m in lins[1:]:
+            parts += [m.weight.detach().t().reshape(-1), m.bias.detach()]
+        if lins is lin_pi:
+            parts.append(ac.log_std.detach())
     return torch.cat([p.float().reshape(-1) for p in parts]).contiguous()
 
 
@@ -153,7 +254,8 @@ class FusedActorCritic:
         return self.step(obs, deterministic=True)[1]
 
 
-def gae(rew, val, done, trunc, last_val, trunc_val, gamma: float = 0.99, lam: float = 0.95):
+def gae(rew, val, done, trunc, last_val, trunc_val, gamma: float = 0.99, lam: float = 0.95,
+        rew_den: float | None = None, with_discounted: bool = False):
     """Batched GAE over [T, N] buffers with per-env episode boundaries.
 
     rew, val:   [T, N] rewards r_t and values V(s_t)
@@ -161,34 +263,46 @@ def gae(rew, val, done, trunc, last_val, trunc_val, gamma: float = 0.99, lam: fl
     trunc:      [T, N] bool, the end was a TimeLimit truncation (bootstrap from trunc_val)
     last_val:   [N]    V(s_T) of the observation after the last step (epoch cut-off)
     trunc_val:  [T, N] V(final_obs_t) where trunc, anything elsewhere
-    Returns (adv [T, N], value_targets [T, N])."""
+    rew_den:    reward scaling (core.py:522-529): delta uses clip(r / rew_den, -10, 10) with
+                rew_den = ret_oms.std + 1e-5; None = unscaled
+    Returns (adv [T, N], value_targets [T, N]) and, with with_discounted, the per-episode
+    discounted returns of the unscaled rewards bootstrapped like finish_path (core.py:519)."""
     T = rew.shape[0]
     adv = torch.empty_like(rew)
+    disc = torch.empty_like(rew) if with_discounted else None
     nxt_adv = torch.zeros_like(last_val)
     nxt_val = last_val
+    nxt_ret = last_val
     for t in range(T - 1, -1, -1):
         d = done[t]
         boot = torch.where(d, torch.where(trunc[t], trunc_val[t], torch.zeros_like(nxt_val)), nxt_val)
-        delta = rew[t] + gamma * boot - val[t]
+        r = rew[t] if rew_den is None else torch.clamp(rew[t] / rew_den, -10.0, 10.0)
+        delta = r + gamma * boot - val[t]
         a = delta + gamma * lam * torch.where(d, torch.zeros_like(nxt_adv), nxt_adv)
         adv[t] = a
+        if disc is not None:
+            disc[t] = rew[t] + gamma * torch.where(d, boot, nxt_ret)
+            nxt_ret = disc[t]
         nxt_adv, nxt_val = a, val[t]
-    return adv, adv + val
+    return (adv, adv + val, disc) if with_discounted else (adv, adv + val)
 
 
-def gae_device(rew, val, done_u8, trunc_u8, last_val, trunc_val, gamma: float = 0.99, lam: float = 0.95):
+def gae_device(rew, val, done_u8, trunc_u8, last_val, trunc_val, gamma: float = 0.99, lam: float = 0.95,
+               rew_den: float | None = None, with_discounted: bool = False):
     """``gae`` as one HIP launch (cf2_gae): one thread per env scans T backward."""
     from . import _native
     T, n = rew.shape
     adv = torch.empty_like(rew)
     ret = torch.empty_like(rew)
+    disc = torch.empty_like(rew) if with_discounted else None
     lib = _native.load()
     _native.check(lib.cf2_gae(T, n, rew.contiguous().data_ptr(), val.contiguous().data_ptr(),
                               done_u8.contiguous().data_ptr(), trunc_u8.contiguous().data_ptr(),
                               trunc_val.contiguous().data_ptr(), last_val.contiguous().data_ptr(), float(gamma),
-                              float(lam), adv.data_ptr(), ret.data_ptr(),
-                              torch.cuda.current_stream(rew.device).cuda_stream), "cf2_gae")
-    return adv, ret
+                              float(lam), float(rew_den) if rew_den is not None else 0.0, adv.data_ptr(),
+                              ret.data_ptr(), _native.ptr(disc), torch.cuda.current_stream(rew.device).cuda_stream),
+                  "cf2_gae")
+    return (adv, ret, disc) if with_discounted else (adv, ret)
 
 
 @dataclasses.dataclass
@@ -205,6 +319,7 @@ class Rollout:
     last_obs: torch.Tensor   # [N, obs_dim] observation after the last step
     last_val: torch.Tensor   # [N] V(last_obs)
     trunc_val: torch.Tensor  # [T, N] V(pre-reset obs), used where trunc
+    discounted_ret: torch.Tensor  # [T, N] per-episode discounted returns (return statistics)
 
 
 @torch.no_grad()
@@ -226,6 +341,8 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
     buf_tr = torch.empty(steps, n, dtype=torch.bool, device=dev)
     trunc_val = torch.zeros(steps, n, device=dev)
     fused = isinstance(ac, FusedActorCritic)
+    module = ac.ac if fused else ac
+    rew_den = float(module.ret_oms.std.item() + module.ret_oms.eps) if module.ret_oms is not None else None
     if fused:
         # zero-copy: the policy and the env write straight into the rollout storage
         obs_buf = torch.empty(steps + 1, n, d, device=dev)
@@ -239,9 +356,9 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
             ac.value_masked(fin, tr8[t], trunc_val[t])              # V(final obs) of the time-outs only
         o = obs_buf[steps]
         last_val = ac.value(o)
-        adv, ret = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam)
+        adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True)
         buf_o, buf_d, buf_tr = obs_buf[:steps], d8.bool(), tr8.bool()
-        return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val)
+        return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val, disc)
     for t in range(steps):
         a, v, lp = ac.step(o, generator=generator)
         buf_o[t] = o
@@ -254,8 +371,9 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         buf_tr[t] = info["truncated"].bool()
         trunc_val[t] = ac.value(info["final_obs"])      # only read where truncated
     last_val = ac.value(o)
-    adv, ret = gae(buf_r, buf_v, buf_d, buf_tr, last_val, trunc_val, gamma, lam)
-    return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val)
+    adv, ret, disc = gae(buf_r, buf_v, buf_d, buf_tr, last_val, trunc_val, gamma, lam, rew_den, True)
+    return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val, disc)
 
 
-__all__ = ["MLPActorCritic", "FusedActorCritic", "pack_policy_weights", "gae", "gae_device", "collect", "Rollout"]
+__all__ = ["OnlineMeanStd", "MLPActorCritic", "FusedActorCritic", "pack_policy_weights", "gae", "gae_device", "collect",
+           "Rollout", "update_running_statistics"]

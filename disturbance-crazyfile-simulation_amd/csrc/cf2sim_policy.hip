@@ -188,25 +188,34 @@ __global__ void __launch_bounds__(256) policy_kernel(const float* __restrict__ W
     if (logp) logp[r] = sample ? lp : 1.0f;
 }
 
-// Batched GAE (algs/core.py:459-480 finish_path per episode slice, with per-env boundaries):
+// Batched GAE (algs/core.py:459-535 finish_path per episode slice, with per-env boundaries):
 // one thread per env scans the [T, N] buffers backward; loads/stores at step t are coalesced
-// over envs.  Bootstraps: terminal 0, time-out trunc_val[t], end of buffer last_val.
+// over envs.  Bootstraps: terminal 0, time-out trunc_val[t], end of buffer last_val.  Reward
+// scaling (core.py:522-529): rew_den > 0 puts clip(r / rew_den, -10, 10) into delta.  disc
+// (optional): the per-episode discounted returns of the unscaled rewards (core.py:519).
 __global__ void __launch_bounds__(256) gae_kernel(uint32_t T, uint32_t n, const float* __restrict__ rew,
                                                   const float* __restrict__ val, const uint8_t* __restrict__ done,
                                                   const uint8_t* __restrict__ trunc, const float* __restrict__ trunc_val,
                                                   const float* __restrict__ last_val, float gamma, float lam,
-                                                  float* __restrict__ adv, float* __restrict__ ret) {
+                                                  float rew_den, float* __restrict__ adv, float* __restrict__ ret,
+                                                  float* __restrict__ disc) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
-    float nxt_adv = 0.0f, nxt_val = last_val[e];
+    float nxt_adv = 0.0f, nxt_val = last_val[e], nxt_ret = last_val[e];
     for (int t = (int)T - 1; t >= 0; --t) {
         const size_t k = (size_t)t * n + e;
         const bool d = done[k] != 0;
         const float boot = d ? (trunc[k] ? trunc_val[k] : 0.0f) : nxt_val;
         const float v = val[k];
-        const float a = (rew[k] + gamma * boot - v) + gamma * lam * (d ? 0.0f : nxt_adv);
+        const float r = rew[k];
+        const float rs = rew_den > 0.0f ? fminf(fmaxf(r / rew_den, -10.0f), 10.0f) : r;
+        const float a = (rs + gamma * boot - v) + gamma * lam * (d ? 0.0f : nxt_adv);
         adv[k] = a;
         ret[k] = a + v;
+        if (disc) {
+            nxt_ret = r + gamma * (d ? boot : nxt_ret);
+            disc[k] = nxt_ret;
+        }
         nxt_adv = a;
         nxt_val = v;
     }
@@ -218,12 +227,13 @@ using namespace cf2;
 
 extern "C" int cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev, const uint8_t* done_dev,
                        const uint8_t* trunc_dev, const float* trunc_val_dev, const float* last_val_dev, float gamma,
-                       float lam, float* adv_dev, float* ret_dev, void* stream) {
+                       float lam, float rew_den, float* adv_dev, float* ret_dev, float* disc_ret_dev, void* stream) {
     if (!rew_dev || !val_dev || !done_dev || !trunc_dev || !trunc_val_dev || !last_val_dev || !adv_dev || !ret_dev)
         return CF2_ERR_INVALID_ARG;
     if (n == 0 || T == 0) return CF2_OK;
     hipLaunchKernelGGL(gae_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, T, n, rew_dev, val_dev,
-                       done_dev, trunc_dev, trunc_val_dev, last_val_dev, gamma, lam, adv_dev, ret_dev);
+                       done_dev, trunc_dev, trunc_val_dev, last_val_dev, gamma, lam, rew_den, adv_dev, ret_dev,
+                       disc_ret_dev);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CF2_OK : CF2_ERR_HIP;
 }

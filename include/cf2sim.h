@@ -250,12 +250,15 @@ int  cf2_policy_forward(const float* weights_dev, uint32_t n, uint32_t obs_dim, 
 int  cf2_value_forward_masked(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
                               const uint8_t* mask_dev, float* val_dev, void* stream);
 
-/* Batched GAE over [T, n] rollout buffers (algs/core.py:459-480 finish_path on every env's
+/* Batched GAE over [T, n] rollout buffers (algs/core.py:459-535 finish_path on every env's
  * episode slices): done/trunc uint8 (terminal -> bootstrap 0, time-out -> trunc_val), the end of
- * the buffer bootstraps last_val [n].  Outputs adv [T, n], ret = adv + val [T, n]. */
+ * the buffer bootstraps last_val [n].  rew_den > 0: reward scaling, delta uses
+ * clip(r / rew_den, -10, 10) with rew_den = ret_oms.std + 1e-5 (core.py:522-529); <= 0: none.
+ * Outputs adv [T, n], ret = adv + val [T, n] and, if disc_ret_dev is not NULL, the per-episode
+ * discounted returns of the unscaled rewards (core.py:519, the return statistics' input). */
 int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev, const uint8_t* done_dev,
              const uint8_t* trunc_dev, const float* trunc_val_dev, const float* last_val_dev, float gamma,
-             float lam, float* adv_dev, float* ret_dev, void* stream);
+             float lam, float rew_den, float* adv_dev, float* ret_dev, float* disc_ret_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,9 +20,12 @@ def discount_cumsum(x, discount):
     return out
 
 
-def reference_gae(rew, val, done, trunc, trunc_val, last_val, gamma, lam):
+def reference_gae(rew, val, done, trunc, trunc_val, last_val, gamma, lam, rew_den=None):
     """roll_out + finish_path on one env's stream: an episode slice ends at done (bootstrap
-    V(final obs) on a time-out, 0 on a terminal state) or at the end of the epoch (V(s_T))."""
+    V(final obs) on a time-out, 0 on a terminal state) or at the end of the epoch (V(s_T)).
+    rew_den: reward scaling, rewards clip(r / rew_den, -10, 10) (core.py:522-529)."""
+    if rew_den is not None:
+        rew = np.clip(np.asarray(rew, np.float64) / rew_den, -10.0, 10.0)
     T = len(rew)
     adv = np.zeros(T)
     start = 0
@@ -65,10 +68,10 @@ def test_actor_critic_matches_reference_definitions():
     obs = torch.randn(128, 34)
     g = torch.Generator().manual_seed(1)
     a, v, logp = ac.step(obs, generator=g)
-    mu = ac.pi_net(obs).detach()
+    mu = ac.pi_net(ac.normalize(obs)).detach()
     ref = torch.distributions.Normal(mu, torch.exp(ac.log_std)).log_prob(a).sum(-1)
     torch.testing.assert_close(logp, ref, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(v, ac.v_net(obs).squeeze(-1).detach())
+    torch.testing.assert_close(v, ac.v_net(ac.normalize(obs)).squeeze(-1).detach())
     assert math.isclose(float(ac.log_std.exp()[0]), 0.5, rel_tol=1e-6)        # core.py:238
     ac.set_log_std(0.0)
     assert math.isclose(float(ac.log_std.exp()[0]), 0.01, rel_tol=1e-5)        # core.py:278
@@ -94,8 +97,9 @@ def test_collect_on_gpu_matches_reference_gae(gpu):
     adv = ro.adv.double().cpu().numpy()
     last_val, trunc_val = ro.last_val.double().cpu().numpy(), ro.trunc_val.double().cpu().numpy()
     torch.testing.assert_close(ro.last_val, ac.value(ro.last_obs))
+    den = float(ac.ret_oms.std.item()) + 1e-5                         # reward scaling (IWPG default)
     for k in range(0, n, 7):
-        ra, rr = reference_gae(rew[:, k], val[:, k], d[:, k], tr[:, k], trunc_val[:, k], last_val[k], 0.99, 0.95)
+        ra, rr = reference_gae(rew[:, k], val[:, k], d[:, k], tr[:, k], trunc_val[:, k], last_val[k], 0.99, 0.95, den)
         np.testing.assert_allclose(adv[:, k], ra, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(ro.ret[:, k].double().cpu().numpy(), rr, rtol=1e-4, atol=1e-4)
     envs.close()
@@ -114,12 +118,13 @@ def test_fused_policy_matches_torch_networks(gpu, obs_dim):
     for m in ac.modules():                       # non-trivial biases
         if isinstance(m, torch.nn.Linear):
             torch.nn.init.uniform_(m.bias, -0.3, 0.3)
-    fused = FusedActorCritic(ac, seed=1234)
+    ac.obs_oms.update(torch.randn(5000, obs_dim, device=gpu) * torch.rand(obs_dim, device=gpu) * 4 + 1.0)
+    fused = FusedActorCritic(ac, seed=1234)       # standardisation folded into the first layers
     n = 3000                                      # ragged last block
     obs = torch.randn(n, obs_dim, device=gpu) * 3
     with torch.no_grad():
-        mu_ref = ac.pi_net(obs)
-        v_ref = ac.v_net(obs).squeeze(-1)
+        mu_ref = ac.pi_net(ac.normalize(obs))
+        v_ref = ac.v_net(ac.normalize(obs)).squeeze(-1)
     a_det, v, _ = fused.step(obs, deterministic=True)
     err = lambda g, r: float(((g - r).abs() / (1 + r.abs())).max())
     assert err(a_det, mu_ref) < 2e-5 and err(v, v_ref) < 2e-5
@@ -150,7 +155,7 @@ def test_fused_value_masked_and_collect(gpu):
     out = torch.full((700,), -7.0, device=gpu)
     fused.value_masked(obs, mask, out)
     with torch.no_grad():
-        v_ref = ac.v_net(obs).squeeze(-1)
+        v_ref = ac.value(obs)
     assert torch.all(out[~mask] == -7.0)
     assert float(((out[mask] - v_ref[mask]).abs() / (1 + v_ref[mask].abs())).max()) < 2e-5
     n, T = 512, 48
@@ -162,8 +167,9 @@ def test_fused_value_masked_and_collect(gpu):
     rew, val = ro.rew.double().cpu().numpy(), ro.val.double().cpu().numpy()
     last_val, trunc_val = ro.last_val.double().cpu().numpy(), ro.trunc_val.double().cpu().numpy()
     # the time-out bootstraps equal the torch value of the pre-reset observation
+    den = float(ac.ret_oms.std.item()) + 1e-5
     for k in range(0, n, 11):
-        ra, _ = reference_gae(rew[:, k], val[:, k], d[:, k], tr[:, k], trunc_val[:, k], last_val[k], 0.99, 0.95)
+        ra, _ = reference_gae(rew[:, k], val[:, k], d[:, k], tr[:, k], trunc_val[:, k], last_val[k], 0.99, 0.95, den)
         np.testing.assert_allclose(ro.adv[:, k].double().cpu().numpy(), ra, rtol=1e-4, atol=1e-4)
     envs.close()
 
