@@ -66,7 +66,7 @@ def load() -> ctypes.CDLL:
     lib.cf2_reset.argtypes = [vp, vp, vp, vp]
     lib.cf2_step.argtypes = [vp] * 11
     lib.cf2_physics_step.argtypes = [vp, vp, vp, ctypes.c_float, vp]
-    lib.cf2_rollout.argtypes = [vp, ctypes.c_int, vp, ctypes.c_size_t, vp, vp, vp, vp]
+    lib.cf2_rollout.argtypes = [vp, ctypes.c_int, vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.cf2_get_state.argtypes = [vp, vp, vp, vp]
     lib.cf2_set_state.argtypes = [vp, vp, vp, vp]
     lib.cf2_hj_disturbance.argtypes = [P(CF2Config), vp, vp, ctypes.c_uint32, ctypes.c_float, vp, vp, vp]

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .config import ENV_SPECS, PHYS_BULLET, PHYS_SIMPLE, REFERENCE_IDS, spec_for_id
+from .config import ENV_SPECS, PHYS_BULLET, PHYS_SIMPLE, REFERENCE_IDS, spec_for_id  # noqa: F401
 
 PHYSICS_PLUGINS = {
     "PybulletPhysicsWithAdversary": PHYS_BULLET,   # envs/physics.py:202
@@ -75,6 +75,11 @@ class CrazyflieEnv:
         self.action_space = self._env.action_space
         self._t = 0
         self._needs_reset = True
+        self._last_action = np.zeros(4, np.float32)
+        # penalty terms of the last compute_reward (envs/hover_free.py:61-66, 227-232), read by the
+        # reference's learner for logging (algs/iwpg/iwpg.py:531-532)
+        self.penalty_log = self.penalty_rpy_log = self.penalty_crash_log = 0.0
+        self.penalty_z_log = self.penalty_rpy_dot_log = self.penalty_velocity_log = 0.0
 
     @property
     def disturbance_level(self) -> float:        # read by iwpg.py:408
@@ -90,6 +95,9 @@ class CrazyflieEnv:
         obs = self._env.reset()
         self._t = 0
         self._needs_reset = False
+        sf, si = self._env.get_state()
+        L = self._env.layout
+        self._last_action = sf[L.f_abuf + 4 * (int(self._env.cfg.buf_size) - 1):][:4, 0].cpu().numpy()
         return obs[0].double().cpu().numpy()
 
     def step(self, action):
@@ -100,6 +108,7 @@ class CrazyflieEnv:
         obs, rew, done, info = self._env.step(a)
         self._t += 1
         terminal = bool(done[0].item())
+        self._log_penalties(np.asarray(action, np.float32).reshape(4), terminal)
         info_out = {"cost": float(info["cost"][0].item()),
                     "disturbance_level": float(info["disturbance_level"][0].item())}
         truncated = self._t >= self.max_episode_steps > 0
@@ -109,6 +118,37 @@ class CrazyflieEnv:
         if d:
             self._needs_reset = True
         return obs[0].double().cpu().numpy(), float(rew[0].item()), d, info_out
+
+    def _log_penalties(self, action, terminal: bool):
+        """The individual terms of compute_reward (hover_free.py:206-235) from the env's state after
+        the step (host-side, single-env adapter only; the batched kernel computes the reward)."""
+        c = self._env.cfg
+        sf = self._env.get_state()[0][:, 0].double().cpu().numpy()
+        L = self._env.layout
+        p, q, v, w = sf[L.f_pos:L.f_pos + 3], sf[L.f_quat:L.f_quat + 4], sf[L.f_vel:L.f_vel + 3], sf[L.f_omega:L.f_omega + 3]
+        if int(c.physics) == PHYS_SIMPLE:
+            rpy, rpy_dot = sf[L.f_rpy:L.f_rpy + 3], w
+        else:
+            x, y, z, qw = q
+            sarg = min(max(-2.0 * (x * z - qw * y), -1.0), 1.0)
+            rpy = np.array([np.arctan2(2 * (y * z + qw * x), qw * qw - x * x - y * y + z * z), np.arcsin(sarg),
+                            np.arctan2(2 * (x * y + qw * z), qw * qw + x * x - y * y - z * z)])
+            s2 = 2.0 / float(q @ q)
+            R = np.array([[1 - s2 * (y * y + z * z), s2 * (x * y - qw * z), s2 * (x * z + qw * y)],
+                          [s2 * (x * y + qw * z), 1 - s2 * (x * x + z * z), s2 * (y * z - qw * x)],
+                          [s2 * (x * z - qw * y), s2 * (y * z + qw * x), 1 - s2 * (x * x + y * y)]])
+            rpy_dot = R.T @ w
+        tgt_rpy, tgt_rate, tgt_pos = np.array(c.target_rpy[:]), np.array(c.target_rate[:]), np.array(c.target_pos[:])
+        pen_action = c.penalty_action * np.linalg.norm(0.5 * (np.clip(action, -1, 1) + 1))
+        pen_arp = c.penalty_arp * np.linalg.norm(action - self._last_action)
+        self.penalty_rpy_log = c.penalty_angle * np.linalg.norm(rpy - tgt_rpy)
+        self.penalty_rpy_dot_log = c.penalty_spin * np.linalg.norm(rpy_dot - tgt_rate)
+        self.penalty_crash_log = c.penalty_terminal if terminal else 0.0
+        self.penalty_velocity_log = c.penalty_velocity * np.linalg.norm(v)
+        self.penalty_log = (self.penalty_rpy_log + pen_arp + self.penalty_rpy_dot_log + self.penalty_velocity_log
+                            + pen_action + self.penalty_crash_log)
+        self.penalty_z_log = c.penalty_z * abs(p[2] - tgt_pos[2])
+        self._last_action = action
 
     def render(self, mode="human"):
         raise NotImplementedError("rendering is outside the accelerated path (DESIGN.md 'Out of scope')")

@@ -170,6 +170,41 @@ class BatchedCrazyflieEnv:
             self._ctx, actions.data_ptr(), None, obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
             _native.ptr(trunc_out), _native.ptr(cost_out), None, _native.ptr(final_obs_out), self.stream), "cf2_step")
 
+    def rollout(self, actions: torch.Tensor, obs_out: torch.Tensor | None = None, rew_out=None, done_out=None,
+                trunc_out=None, cost_out=None, level_out=None, final_obs_out=None):
+        """K env-steps in one fused launch (cf2_rollout): actions [K, N, 4]; returns (obs [K, N, D],
+        rew [K, N], done [K, N], info with truncated / cost / disturbance_level [K, N] and
+        final_obs [K, N, D] when the env keeps final observations).  Identical to K step() calls
+        with the same actions; the state stays in registers across the K steps."""
+        K = int(actions.shape[0])
+        n, od, dev = self.num_envs, self.obs_dim, self.device
+        _check_buf(actions, "actions", (K, n, 4), torch.float32, dev, 16)
+        obs_out = obs_out if obs_out is not None else torch.empty(K, n, od, device=dev)
+        rew_out = rew_out if rew_out is not None else torch.empty(K, n, device=dev)
+        done_out = done_out if done_out is not None else torch.empty(K, n, dtype=torch.uint8, device=dev)
+        trunc_out = trunc_out if trunc_out is not None else torch.empty(K, n, dtype=torch.uint8, device=dev)
+        cost_out = cost_out if cost_out is not None else torch.empty(K, n, device=dev)
+        level_out = level_out if level_out is not None else torch.empty(K, n, device=dev)
+        if final_obs_out is None and self.want_final_obs:
+            final_obs_out = torch.empty(K, n, od, device=dev)
+        _check_buf(obs_out, "obs_out", (K, n, od), torch.float32, dev, 8)
+        _check_buf(rew_out, "rew_out", (K, n), torch.float32, dev)
+        _check_buf(done_out, "done_out", (K, n), torch.uint8, dev, 1)
+        _check_buf(trunc_out, "trunc_out", (K, n), torch.uint8, dev, 1)
+        _check_buf(cost_out, "cost_out", (K, n), torch.float32, dev)
+        _check_buf(level_out, "level_out", (K, n), torch.float32, dev)
+        _check_buf(final_obs_out, "final_obs_out", (K, n, od), torch.float32, dev, 8)
+        if self.cfg.disturbance == DSTB_HJ and self._tables is None:
+            raise _native.CF2Error("HJ-adversary env: bind value tables with bind_hj_tables() first")
+        _native.check(self.lib.cf2_rollout(
+            self._ctx, K, actions.data_ptr(), n * 4, obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
+            trunc_out.data_ptr(), cost_out.data_ptr(), level_out.data_ptr(), _native.ptr(final_obs_out), self.stream),
+            "cf2_rollout")
+        info = {"cost": cost_out, "truncated": trunc_out, "disturbance_level": level_out}
+        if final_obs_out is not None:
+            info["final_obs"] = final_obs_out
+        return obs_out, rew_out, done_out, info
+
     def step_raw(self, act_ptr: int, obs_ptr: int | None = None, full_info: bool = True):
         """Launch one env-step with a raw device pointer to [N, 4] float32 actions (benchmark /
         graph-capture helper; the pointer is not checked).  full_info: also write the truncation,

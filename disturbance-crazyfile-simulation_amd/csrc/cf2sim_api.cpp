@@ -267,15 +267,19 @@ int cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, 
 }
 
 int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems, float* obs_dev, float* rew_dev,
-                uint8_t* done_dev, void* stream) {
-    if (!ctx || K < 1 || !act_dev) return CF2_ERR_INVALID_ARG;
-    if (act_stride_elems < (size_t)ctx->cfg.num_envs * 4 && K > 1) return CF2_ERR_INVALID_ARG;
-    for (int k = 0; k < K; ++k) {
-        const int r = cf2_step(ctx, act_dev + (size_t)k * act_stride_elems, nullptr, obs_dev, rew_dev, done_dev,
-                               nullptr, nullptr, nullptr, nullptr, stream);
-        if (r) return r;
-    }
-    return CF2_OK;
+                uint8_t* done_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, float* final_obs_dev,
+                void* stream) {
+    if (!ctx || K < 1 || !act_dev || !obs_dev || !rew_dev || !done_dev) return CF2_ERR_INVALID_ARG;
+    const size_t n = ctx->cfg.num_envs;
+    if (K > 1 && act_stride_elems < n * 4) return CF2_ERR_INVALID_ARG;
+    if ((act_stride_elems & 3u) != 0 || ((uintptr_t)act_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
+    if (((uintptr_t)obs_dev & 7u) != 0 || (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0))
+        return CF2_ERR_INVALID_ARG;
+    if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL) return CF2_ERR_UNSUPPORTED;   // one dstb tensor per step
+    if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
+    StepIO io{ctx->sf, act_dev, nullptr, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev, final_obs_dev};
+    const hipError_t e = launch_rollout(ctx->P, io, (uint32_t)K, (uint32_t)act_stride_elems, (hipStream_t)stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
 int cf2_get_state(const cf2_ctx* ctx, float* state_f_dev, int32_t* state_i_dev, void* stream) {

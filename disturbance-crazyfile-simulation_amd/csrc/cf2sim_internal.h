@@ -78,6 +78,7 @@ enum : uint32_t { TAG_STEP = 1, TAG_RESET = 2, TAG_PHYS = 3 };
 struct KParams {
     uint32_t N, gid_off, key0, key1;
     uint32_t late_block;          // step kernel: first block index past one residency round (set per launch)
+    uint32_t out_stride;          // rollout kernel: rows per per-step output slab (set per launch)
     int32_t agg, obs_rate, buf_size, use_latency, use_motor_dyn, max_steps, auto_reset, reset_dist;
     int32_t dstb_mode, level_mode, num_levels, gust_dur, noise, dr, phys, held_persistent, need_level;
     float time_step, mass, ixx, iyy, izz, ft0, ft1, K, A, B, hover_x, hover_action, ou_sigma;
@@ -120,6 +121,8 @@ struct StepIO {
 };
 
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
+// K fused env-steps (state in registers); outputs [K][N][...] slabs, actions at act + k * act_stride
+hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s);
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s);
 hipError_t launch_init(const KParams& P, float* sf, hipStream_t s);
 // one physics sub-step of every env (physics plugin step_forward); dt_override <= 0: per-env dt

@@ -1083,15 +1083,13 @@ struct ResetSeed {
 };
 enum { SEED_WORDS = 13 };
 
-template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
-                                         ResetSeed& rs, const double* hj_grid) {
+// The env-step on a loaded Env.  STORE: write the state back (the one-step kernel: the physics
+// state as soon as it is final, the rest at the end); the fused rollout keeps it in registers.
+template <bool NOISE, bool DR, int PHYS, bool STORE>
+__device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
+                                              float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
-    Env E;
-    // every state load is issued up front: on gfx9 vmcnt also counts stores, so a load issued
-    // after the state stores would wait for the whole store burst to drain
-    load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/true);
     const uint32_t gid = P.gid_off + i;
     const float4 a4 = reinterpret_cast<const float4*>(io.act)[i];
     TREADY("v"(E.p[0]), "v"(E.obs_prev[OL - 1]), "v"(E.hact[1][3]), "v"(E.K[3]), "v"(a4.w), "v"(E.rng));
@@ -1212,7 +1210,7 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     }
     // the physics state is final now (an auto-reset below overwrites it): store it early so
     // its registers free up before the epilogue
-    store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
+    if (STORE) store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
     const bool term = compute_done(P, E);
     const float r = compute_reward(P, E, a, term);
     const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
@@ -1245,9 +1243,19 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
         rs.ctr = E.rng;
     }
     E.rng += 1;
-    store_tail<NOISE>(P, io.sf, i, E);
+    if (STORE) store_tail<NOISE>(P, io.sf, i, E);
     TSTAMP(3);   // epilogue issued
     return do_reset;
+}
+
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
+                                         ResetSeed& rs, const double* hj_grid) {
+    Env E;
+    // every state load is issued up front: on gfx9 vmcnt also counts stores, so a load issued
+    // after the state stores would wait for the whole store burst to drain
+    load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/true);
+    return step_env_body<NOISE, DR, PHYS, true>(P, io, i, E, obs_row, rs, hj_grid);
 }
 
 // Reset one env in place: reads only what a reset consumes from the finished episode (the
@@ -1310,54 +1318,14 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
     TSTAMP(8);   // reset stores issued
 }
 
-#ifndef CF2_STEP_MIN_WAVES
-#define CF2_STEP_MIN_WAVES 3   // waves per SIMD: <= 168 VGPRs (and <= 53 KB LDS per block)
-#endif
-// Step kernel: one lane per env.  Auto-reset is compacted per block: with random actions a few
-// % of envs finish per step, so nearly every wave would hold one and run the whole reset path
-// divergently.  Finished envs are listed in LDS and reset by the fewest waves after a block
-// barrier; their state rows were just written by this block and are still in L2, so the reset's
-// scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
-// 4-byte field access for them).
-template <bool NOISE, bool DR, int PHYS, int SPEC>
-#ifndef CF2_STEP_BLOCK
-#define CF2_STEP_BLOCK 256     // envs per block = auto-reset compaction group
-#endif
-__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
-    const KParams P = shape_view<SPEC>(P0);
-    // Issue priority: the blocks that start only after the first residency round (the partial
-    // last round at 262 144 envs) run mostly alone on their SIMDs and end the kernel; their waves
-    // get the issue slots first, so they overlap the tail of the first round (-1 us measured).
-    if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(1);
-#ifdef CF2_TIMING
-    if (uint64_t* r = timing_row()) {
-        if ((threadIdx.x & 63) == 0) {
-            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_ID
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // XCC_ID
-            r[0] = ((uint64_t)xcc << 32) | hw;
-            r[1] = __builtin_amdgcn_s_memrealtime();
-            r[3] = __builtin_amdgcn_s_memtime();
-        }
-    }
-#endif
+// End of a block's env-step: list the finished envs (wave ballot + one LDS atomic per wave), reset
+// them block-cooperatively (see step_kernel) and write the block's obs rows out coalesced.  Every
+// thread of the block calls it; s_cnt must be 0 on entry (set before a barrier the caller passed).
+template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C>
+__device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& io, uint32_t base, uint32_t tid,
+                                               bool do_reset, const ResetSeed& rs, float* s_obs, uint32_t* s_list,
+                                               uint32_t* s_rand, uint32_t* s_cnt) {
     constexpr int OD = NOISE ? 34 : 42;
-    constexpr uint32_t B = CF2_STEP_BLOCK;
-    __shared__ __align__(16) float s_obs[B * OD];          // the block's obs rows, global layout
-    __shared__ uint32_t s_list[B];                         // queue: block-local env index
-#ifndef CF2_RESET_CHUNK
-#define CF2_RESET_CHUNK 32
-#endif
-    constexpr uint32_t C = CF2_RESET_CHUNK;                // auto-resets per chunk
-    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
-    __shared__ uint32_t s_cnt;
-    if (threadIdx.x == 0) s_cnt = 0;
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
-    bool do_reset = false;
-    ResetSeed rs;
-    __shared__ double s_hjgrid[6 * HJ_PTS];
-    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     if (P.auto_reset) {
         __syncthreads();     // s_cnt initialised
         const uint64_t m = __ballot(do_reset);
@@ -1365,7 +1333,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
             const int lane = (int)(threadIdx.x & 63);
             const int leader = __ffsll((unsigned long long)m) - 1;
             uint32_t pos = 0;
-            if (lane == leader) pos = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+            if (lane == leader) pos = atomicAdd(s_cnt, (uint32_t)__popcll(m));
             pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
             if (do_reset) s_list[pos] = tid;
         }
@@ -1383,7 +1351,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
         }
         __syncthreads();
         TSTAMP(4);   // block barrier passed
-        const uint32_t cnt = s_cnt;
+        const uint32_t cnt = *s_cnt;
         // Resets run in chunks of C envs.  Their ~26 Philox blocks per env are drawn by every
         // thread of the block in parallel into LDS; then one lane per env runs the reset math
         // on the table.  (On one lane each, the draws made the reset tail, which every wave of
@@ -1438,7 +1406,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     {
         const uint32_t nvalid = P.N - base < B ? P.N - base : B;
         float* dst = io.obs + (size_t)base * OD;
-        if (nvalid == B && (B * OD) % 4 == 0) {
+        if (nvalid == B && (B * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
             const float4* src4 = reinterpret_cast<const float4*>(s_obs);
             float4* dst4 = reinterpret_cast<float4*>(dst);
             for (uint32_t k = tid; k < B * OD / 4; k += B) dst4[k] = src4[k];
@@ -1448,6 +1416,64 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
             for (uint32_t k = tid; k < nvalid * OD / 2; k += B) dst2[k] = src2[k];
         }
     }
+}
+
+#ifndef CF2_STEP_MIN_WAVES
+#define CF2_STEP_MIN_WAVES 3   // waves per SIMD: <= 168 VGPRs (and <= 53 KB LDS per block)
+#endif
+// Step kernel: one lane per env.  Auto-reset is compacted per block: with random actions a few
+// % of envs finish per step, so nearly every wave would hold one and run the whole reset path
+// divergently.  Finished envs are listed in LDS and reset by the fewest waves after a block
+// barrier; their state rows were just written by this block and are still in L2, so the reset's
+// scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
+// 4-byte field access for them).
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+#ifndef CF2_STEP_BLOCK
+#define CF2_STEP_BLOCK 256     // envs per block = auto-reset compaction group
+#endif
+__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
+    const KParams P = shape_view<SPEC>(P0);
+    // Issue priority: the blocks that start only after the first residency round (the partial
+    // last round at 262 144 envs) run mostly alone on their SIMDs and end the kernel; their waves
+    // get the issue slots first, so they overlap the tail of the first round (-1 us measured).
+    if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
+#ifdef CF2_STAGGER
+    // experiment: the g-th block of each CU in the first round starts g * CF2_STAGGER cycles late
+    if (blockIdx.x < P0.late_block) {
+        const uint32_t g = blockIdx.x / (P0.late_block / 3u);
+        for (uint32_t k = 0; k < g * (CF2_STAGGER / 8000); ++k) __builtin_amdgcn_s_sleep(125);
+    }
+#endif
+#ifdef CF2_TIMING
+    if (uint64_t* r = timing_row()) {
+        if ((threadIdx.x & 63) == 0) {
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // XCC_ID
+            r[0] = ((uint64_t)xcc << 32) | hw;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[3] = __builtin_amdgcn_s_memtime();
+        }
+    }
+#endif
+    constexpr int OD = NOISE ? 34 : 42;
+    constexpr uint32_t B = CF2_STEP_BLOCK;
+    __shared__ __align__(16) float s_obs[B * OD];          // the block's obs rows, global layout
+    __shared__ uint32_t s_list[B];                         // queue: block-local env index
+#ifndef CF2_RESET_CHUNK
+#define CF2_RESET_CHUNK 32
+#endif
+    constexpr uint32_t C = CF2_RESET_CHUNK;                // auto-resets per chunk
+    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
+    bool do_reset = false;
+    ResetSeed rs;
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
+    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, &s_cnt);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
     if (uint64_t* r = timing_row())
@@ -1491,6 +1517,114 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
     const Tile T(sf, P.N, i);
     const int fl = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6) | (E.props_on << 7);
     T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
+}
+
+// Fused K-step rollout (cf2_rollout): the env state is loaded once, stays in registers for K
+// env-steps and is stored once.  Step k reads its actions at act + k * act_stride and writes its
+// outputs into the k-th [N, ...] slab of each output (obs, rew, done, trunc, cost, level,
+// final_obs), i.e. exactly what K cf2_step calls would write.  Auto-reset: the block lists its
+// finished envs and draws their reset tables block-parallel as step_kernel does, but each env is
+// then reset in place by its own lane (its state is in that lane's registers); per env-step HBM
+// traffic is the actions and the outputs only (~170 B instead of ~765 B).
+#ifndef CF2_ROLL_MIN_WAVES
+#define CF2_ROLL_MIN_WAVES 2   // the whole state stays live across the loop (~270 registers at peak)
+#endif
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_kernel(KParams P0, StepIO io0, uint32_t K,
+                                                                                  uint32_t act_stride) {
+    const KParams P = shape_view<SPEC>(P0);
+    constexpr int OD = NOISE ? 34 : 42;
+    constexpr uint32_t B = CF2_STEP_BLOCK;
+    constexpr uint32_t C = CF2_RESET_CHUNK;
+    __shared__ __align__(16) float s_obs[B * OD];
+    __shared__ uint32_t s_list[B];
+    __shared__ uint32_t s_ctr[B];                       // rng counter of each listed env's reset
+    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];
+    __shared__ uint32_t s_cnt;
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    const bool live = i < P.N;
+    const bool need_level = P.need_level || io0.level != nullptr;
+    Env E;
+    if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, need_level, /*with_hist=*/true);
+    const size_t n = P0.out_stride;              // rows per output slab (the whole population)
+    float* obs_row = s_obs + tid * OD;
+    for (uint32_t k = 0; k < K; ++k) {
+        if (tid == 0) s_cnt = 0;     // every reader of the previous step passed its last barrier
+        StepIO io = io0;
+        io.act = io0.act + (size_t)k * act_stride;
+        io.rew = io0.rew + (size_t)k * n;
+        io.done = io0.done + (size_t)k * n;
+        if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
+        if (io0.cost) io.cost = io0.cost + (size_t)k * n;
+        if (io0.level) io.level = io0.level + (size_t)k * n;
+        if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+        bool do_reset = false;
+        ResetSeed rs;
+        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false>(P, io, i, E, obs_row, rs, s_hjgrid);
+        __syncthreads();             // s_cnt initialised
+        uint32_t pos = 0;
+        const uint64_t m = __ballot(do_reset);
+        if (m) {
+            const int lane = (int)(threadIdx.x & 63);
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            if (lane == leader) pos = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
+            pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (do_reset) { s_list[pos] = tid; s_ctr[pos] = rs.ctr; }
+        }
+        __syncthreads();
+        const uint32_t cnt = s_cnt;
+        for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
+            const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
+            {
+                const Keys Kk = make_keys(P.key0, P.key1);
+                for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
+                    const uint32_t sl = w / nc, e = w - sl * nc, p2 = c0 + e;
+                    U4 u = philox(Kk, reset_block_of_slot((int)sl), s_ctr[p2], P.gid_off + base + s_list[p2], TAG_RESET);
+                    if (reset_slot_normal_xy((int)sl)) {
+                        float z0, z1;
+                        box_muller(u.x, u.y, z0, z1);
+                        u.x = __float_as_uint(z0); u.y = __float_as_uint(z1);
+                    }
+                    if (reset_slot_normal_zw((int)sl)) {
+                        float z2, z3;
+                        box_muller(u.z, u.w, z2, z3);
+                        u.z = __float_as_uint(z2); u.w = __float_as_uint(z3);
+                    }
+                    uint32_t* q = s_rand + sl * 4 * C + e;
+                    q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
+                }
+            }
+            __syncthreads();
+            if (do_reset && pos >= c0 && pos < c0 + nc) {
+                // in place on this lane's registers: reset_env keeps what a reset inherits from the
+                // finished episode (stale body rates, gyro bias, OU state, level) from E itself
+                float o[OD];
+                const TableRng tg{s_rand + (pos - c0), C};
+                reset_env<NOISE, DR, PHYS>(P, E, tg, P.gid_off + i, o);
+#pragma unroll
+                for (int q = 0; q < OD; q += 2) *reinterpret_cast<float2*>(obs_row + q) = make_float2(o[q], o[q + 1]);
+            }
+            __syncthreads();         // the next chunk reuses s_rand
+        }
+        // coalesced write of the block's obs rows into step k's slab
+        {
+            const uint32_t nvalid = P.N - base < B ? P.N - base : B;
+            float* dst = io0.obs + (size_t)k * n * OD + (size_t)base * OD;
+            if (nvalid == B && (B * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
+                const float4* src4 = reinterpret_cast<const float4*>(s_obs);
+                float4* dst4 = reinterpret_cast<float4*>(dst);
+                for (uint32_t q = tid; q < B * OD / 4; q += B) dst4[q] = src4[q];
+            } else {
+                const float2* src2 = reinterpret_cast<const float2*>(s_obs);
+                float2* dst2 = reinterpret_cast<float2*>(dst);
+                for (uint32_t q = tid; q < nvalid * OD / 2; q += B) dst2[q] = src2[q];
+            }
+        }
+        __syncthreads();             // the write-out read s_obs before the next step's rows
+    }
+    if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
 }
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
@@ -1625,6 +1759,53 @@ static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t 
     return hipGetLastError();
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
+static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
+    // envs are processed in slices that fit one residency round (blocks resident at once =
+    // CUs x blocks per CU): a slice's blocks run all K steps together, so no block waits K steps
+    // for a free slot.  Slices run one after the other on the stream.
+    static int round_blocks = -1;
+    if (round_blocks < 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_kernel<NOISE, DR, PHYS, SPEC>, CF2_STEP_BLOCK, 0);
+        if (e != hipSuccess) return e;
+        round_blocks = cus * (per_cu > 0 ? per_cu : 1);
+    }
+    const uint32_t blocks = (P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK;
+    const uint32_t nslices = (blocks + (uint32_t)round_blocks - 1) / (uint32_t)round_blocks;
+    const uint32_t per = (blocks + nslices - 1) / nslices;           // blocks per slice (balanced)
+    constexpr int OD = NOISE ? 34 : 42;
+    for (uint32_t b0 = 0; b0 < blocks; b0 += per) {
+        const uint32_t nb = blocks - b0 < per ? blocks - b0 : per;
+        const uint32_t e0 = b0 * CF2_STEP_BLOCK;
+        KParams Ps = P;
+        Ps.N = (P.N - e0 < nb * CF2_STEP_BLOCK) ? P.N - e0 : nb * CF2_STEP_BLOCK;
+        Ps.gid_off = P.gid_off + e0;
+        // a slice sees its envs as 0..Ps.N-1: the state view starts at its first tile (e0 is a
+        // multiple of 256, so of 64), each output at its first row; the per-step slab stride
+        // stays that of the whole population (rollout_kernel strides by its own Ps.N, so the
+        // outputs of a sliced launch use an explicit stride below)
+        StepIO ios = io;
+        ios.sf = io.sf + (size_t)(e0 / 64u) * (NG * 256);
+        ios.act = io.act + (size_t)e0 * 4;
+        ios.obs = io.obs + (size_t)e0 * OD;
+        ios.rew = io.rew + e0;
+        ios.done = io.done + e0;
+        if (io.trunc) ios.trunc = io.trunc + e0;
+        if (io.cost) ios.cost = io.cost + e0;
+        if (io.level) ios.level = io.level + e0;
+        if (io.final_obs) ios.final_obs = io.final_obs + (size_t)e0 * OD;
+        Ps.out_stride = P.N;
+        hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s, Ps, ios, K,
+                           act_stride);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_reset_t(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
     hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, sf, mask, obs);
@@ -1681,6 +1862,9 @@ extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
 }
 #endif
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
+hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
+    CF2_DISPATCH(launch_rollout_t, P, io, K, act_stride, s);
+}
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     CF2_DISPATCH(launch_reset_t, P, sf, mask, obs, s);
 }

@@ -218,10 +218,17 @@ int  cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev,
  * uses the per-env dt (domain randomisation).  act_dev [N,4] 16-B aligned. */
 int  cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float time_step, void* stream);
 
-/* K consecutive env-steps with actions act_dev[k] = act_dev + k*N*4 (rollout mode); outputs
- * are those of the last step.  Equivalent to K cf2_step calls; one launch per step. */
+/* K consecutive env-steps fused in one launch (rollout mode; SURVEY section 7 "fused K-step"):
+ * the env state stays in registers across the K steps.  Step k reads actions act_dev + k *
+ * act_stride_elems ([N,4], 16-B aligned, stride a multiple of 4) and writes the k-th [N, ...]
+ * slab of every output: obs_dev [K,N,obs_dim] (8-B aligned), rew_dev [K,N], done_dev [K,N] and,
+ * when not NULL, trunc_dev [K,N], cost_dev [K,N], level_dev [K,N], final_obs_dev [K,N,obs_dim].
+ * Results are identical to K cf2_step calls with the same actions (the reference's
+ * IWPGAlgorithm.roll_out loop algs/iwpg/iwpg.py:372-410 with actions known in advance, e.g.
+ * open-loop or random-action rollouts).  Not for CF2_DSTB_EXTERNAL envs (CF2_ERR_UNSUPPORTED). */
 int  cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems,
-                 float* obs_dev, float* rew_dev, uint8_t* done_dev, void* stream);
+                 float* obs_dev, float* rew_dev, uint8_t* done_dev, uint8_t* trunc_dev,
+                 float* cost_dev, float* level_dev, float* final_obs_dev, void* stream);
 
 /* Whole-state snapshot (device buffers sized by cf2_layout). */
 int  cf2_get_state(const cf2_ctx* ctx, float* state_f_dev, int32_t* state_i_dev, void* stream);

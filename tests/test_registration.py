@@ -88,6 +88,9 @@ def test_make_matches_restatement_and_time_limit(gpu):
         o_r, r_r, d_r, _ = ref.step(a[None])
         assert np.max(np.abs(o_g - o_r[0]) / (1 + np.abs(o_r[0]))) < 5e-4, t
         assert abs(r_g - float(r_r[0])) < 1e-3
+        # the penalty terms the reference logs (hover_free.py:227-232) add up to the reward
+        assert abs(r_g + env.penalty_log + env.penalty_z_log) < 1e-4 * (1 + abs(r_g))
+        assert env.penalty_rpy_log >= 0 and env.penalty_rpy_dot_log >= 0 and env.penalty_velocity_log >= 0
         assert not bool(d_r[0])
         assert d_g == (t == 39)
     assert info.get("TimeLimit.truncated") is True

@@ -1,0 +1,37 @@
+"""Per env-step time of cf2_step launches vs the fused cf2_rollout (K steps per launch) at the
+BASELINE shapes; HIP events on the launch stream.  python tools/fused_bench.py [K]"""
+import os, sys, json
+import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+from cf2sim.vec_env import BatchedCrazyflieEnv
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+res = []
+for env_id, n in [("DroneHoverBulletFreeEnvWithConstWind-v0", 4096), ("DroneHoverBulletFreeEnvWithGust-v0", 32768),
+                  ("DroneHoverBulletFreeEnvWithRandomAdversary-v0", 65536), ("DroneHoverBulletFreeEnvWithGust-v0", 131072),
+                  ("DroneHoverBulletFreeEnvWithGust-v0", 262144)]:
+    env = BatchedCrazyflieEnv(env_id, n, seed=0)
+    env.reset()
+    a = torch.rand(K, n, 4, device="cuda") * 2 - 1
+    obs = torch.empty(K, n, env.obs_dim, device="cuda"); rew = torch.empty(K, n, device="cuda")
+    done = torch.empty(K, n, dtype=torch.uint8, device="cuda"); tr = torch.empty_like(done)
+    cost = torch.empty(K, n, device="cuda"); lv = torch.empty(K, n, device="cuda")
+    s = torch.cuda.current_stream()
+    def steps():
+        for k in range(K):
+            env.step_raw(a[k].data_ptr())
+    def fused():
+        env.rollout(a, obs, rew, done, tr, cost, lv)
+    out = {"env": env_id, "N": n, "K": K}
+    for name, fn in (("step", steps), ("fused", fused)):
+        fn(); torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(3):
+            fn()
+        e1.record(s); torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / (3 * K)
+        out[name + "_us_per_env_step"] = us
+        out[name + "_env_steps_per_s"] = n / us * 1e6
+    print(json.dumps(out), flush=True)
+    env.close()
