@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = (
     "cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
     "cf2_create", "cf2_destroy", "cf2_layout_get", "cf2_bind_hj_tables", "cf2_reset", "cf2_step", "cf2_physics_step",
     "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
-    "cf2_policy_weights_count", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
+    "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
 )
 
 
@@ -56,6 +56,7 @@ def load() -> ctypes.CDLL:
     lib.cf2_abi_version.restype = ctypes.c_int
     lib.cf2_config_sizeof.restype = ctypes.c_size_t
     lib.cf2_policy_weights_count.restype = ctypes.c_size_t
+    lib.cf2_policy_packed_count.restype = ctypes.c_size_t
     lib.cf2_status_string.restype = ctypes.c_char_p
     lib.cf2_status_string.argtypes = [ctypes.c_int]
     lib.cf2_last_hip_error.restype = ctypes.c_int
@@ -72,13 +73,16 @@ def load() -> ctypes.CDLL:
     lib.cf2_hj_disturbance.argtypes = [P(CF2Config), vp, vp, ctypes.c_uint32, ctypes.c_float, vp, vp, vp]
     u32 = ctypes.c_uint32
     lib.cf2_policy_weights_count.argtypes = [u32]
-    lib.cf2_policy_forward.argtypes = [vp, u32, u32, vp, ctypes.c_uint64, u32, u32, ctypes.c_int, vp, vp, vp, vp]
-    lib.cf2_value_forward_masked.argtypes = [vp, u32, u32, vp, vp, vp, vp]
+    lib.cf2_policy_packed_count.argtypes = [u32, ctypes.c_int]
+    lib.cf2_policy_pack.argtypes = [vp, u32, ctypes.c_int, vp, vp]
+    lib.cf2_policy_forward.argtypes = [vp, u32, u32, ctypes.c_int, vp, ctypes.c_uint64, u32, u32, ctypes.c_int, vp, vp,
+                                       vp, vp]
+    lib.cf2_value_forward_masked.argtypes = [vp, u32, u32, ctypes.c_int, vp, vp, vp, vp]
     lib.cf2_gae.argtypes = [u32, u32, vp, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp,
                             vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
-                        "cf2_policy_weights_count"):
+                        "cf2_policy_weights_count", "cf2_policy_packed_count"):
             getattr(lib, name).restype = ctypes.c_int
     if lib.cf2_config_sizeof() != ctypes.sizeof(CF2Config):
         raise CF2Error(f"cf2_config size mismatch: C {lib.cf2_config_sizeof()} vs Python {ctypes.sizeof(CF2Config)}")

@@ -18,8 +18,8 @@ Reference behaviour restated (paths relative to phoenix_drone_simulation/):
 * Observation standardisation (IWPG default use_standardized_obs=True, iwpg.py:59):
   ``ActorCritic.step`` feeds (obs - mean) / (std + 1e-5) to both networks (core.py:383-388);
   the statistics are ``OnlineMeanStd`` (utils/online_mean_std.py), updated once per epoch by
-  ``update_running_statistics`` (iwpg.py:412-420).  The fused kernel takes the standardisation
-  folded into the first layer of each network (pack_policy_weights).
+  ``update_running_statistics`` (iwpg.py:412-420).  The fused kernel standardises the observation
+  in registers before the first layer (pack_policy_weights carries mean and 1 / (std + eps)).
 
 Here N envs run in lock step with on-device auto-reset, so episode boundaries differ per env.
 ``gae`` evaluates the same recursion over a [T, N] buffer with per-env masks:
@@ -156,7 +156,7 @@ class MLPActorCritic(nn.Module):
 def update_running_statistics(ac: MLPActorCritic, rollout: "Rollout", fused: "FusedActorCritic | None" = None):
     """IWPGAlgorithm.update_running_statistics (iwpg.py:412-420) on a whole batched rollout: the raw
     observations update the observation statistics, the discounted returns the return statistics.
-    A FusedActorCritic over `ac` is re-synced (its first layers carry the folded standardisation)."""
+    A FusedActorCritic over `ac` is re-synced (its weight block carries the standardisation)."""
     if ac.obs_oms is not None:
         ac.obs_oms.update(rollout.obs.reshape(-1, rollout.obs.shape[-1]))
     if ac.ret_oms is not None:
@@ -165,21 +165,12 @@ def update_running_statistics(ac: MLPActorCritic, rollout: "Rollout", fused: "Fu
         fused.sync()
 
 
-def _folded_first_layer(lin: nn.Linear, oms: OnlineMeanStd | None):
-    """W' x + b' == W ((x - mean) / (std + eps)) + b: the observation standardisation folded into
-    a first layer (fp64 on the host, then fp32)."""
-    W, b = lin.weight.detach().double(), lin.bias.detach().double()
-    if oms is None:
-        return W, b
-    den = oms.std.detach().double() + oms.eps
-    Wf = W / den[None, :]
-    return Wf, b - Wf @ oms.mean.detach().double()
-
-
 def pack_policy_weights(ac: MLPActorCritic) -> torch.Tensor:
-    """Flatten an MLPActorCritic with the default shapes into the weight block of
-    cf2_policy_forward (input-major matrices: pi W1 b1 W2 b2 W3 b3 log_std, then v W1 b1 W2 b2 W3 b3).
-    The observation standardisation is folded into pi W1/b1 and v W1/b1."""
+    """Flatten an MLPActorCritic with the default shapes into the flat weight block of
+    cf2_policy_pack (input-major matrices: pi W1 b1 W2 b2 W3 b3 log_std, then v W1 b1 W2 b2 W3 b3,
+    then the observation standardisation mean[D] and scale[D] = 1 / (std + eps), computed in fp64;
+    identity without obs_oms).  The kernel standardises the observation before the first layer,
+    as ActorCritic.step does (core.py:383-388)."""
     lin_pi = [m for m in ac.pi_net if isinstance(m, nn.Linear)]
     lin_v = [m for m in ac.v_net if isinstance(m, nn.Linear)]
     shapes = [(m.out_features, m.in_features) for m in lin_pi] + [(m.out_features, m.in_features) for m in lin_v]
@@ -188,33 +179,54 @@ def pack_policy_weights(ac: MLPActorCritic) -> torch.Tensor:
         raise ValueError(f"the fused kernel implements the PPO default networks only, got {shapes}")
     parts = []
     for lins in (lin_pi, lin_v):
-        W1, b1 = _folded_first_layer(lins[0], ac.obs_oms)
-        parts += [W1.t().reshape(-1), b1]
-        for m in lins[1:]:
+        for m in lins:
             parts += [m.weight.detach().t().reshape(-1), m.bias.detach()]
         if lins is lin_pi:
             parts.append(ac.log_std.detach())
+    dev = lin_pi[0].weight.device
+    if ac.obs_oms is not None:
+        parts += [ac.obs_oms.mean.detach(), 1.0 / (ac.obs_oms.std.detach().double() + ac.obs_oms.eps)]
+    else:
+        parts += [torch.zeros(d, device=dev), torch.ones(d, device=dev)]
     return torch.cat([p.float().reshape(-1) for p in parts]).contiguous()
+
+
+POLICY_PRECISIONS = {"fp32": 0, "bf16x3": 1}     # cf2_policy_precision (include/cf2sim.h)
 
 
 class FusedActorCritic:
     """``MLPActorCritic.step`` / ``value`` through the fused HIP kernel (cf2_policy_forward).
     Sampling noise comes from Philox keyed (seed, call counter, row): reproducible, independent
-    of batch geometry.  Call ``sync()`` after changing the torch module's parameters."""
+    of batch geometry.  Call ``sync()`` after changing the torch module's parameters.
 
-    def __init__(self, ac: MLPActorCritic, seed: int = 0):
+    precision: "fp32" -- exact fp32 products on the matrix cores (the result of an fmaf chain);
+    "bf16x3" -- split-bf16 products (x = hi + lo, three bf16 MFMAs): <= ~1.1e-5 relative error
+    per product, fp32 accumulation and activations, ~5x the fp32 matrix rate.  The collected
+    log-probabilities do not depend on it (logp is a function of the drawn noise only)."""
+
+    def __init__(self, ac: MLPActorCritic, seed: int = 0, precision: str = "bf16x3"):
         from . import _native
+        if precision not in POLICY_PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(POLICY_PRECISIONS)}, got {precision!r}")
         self.ac = ac
         self.lib = _native.load()
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.counter = 0
+        self.precision = precision
+        self.prec = POLICY_PRECISIONS[precision]
         self.obs_dim = ac.pi_net[0].in_features
         self.sync()
 
     def sync(self):
+        """Re-pack the weights: the flat block (pack_policy_weights) -> the kernel's MFMA fragment
+        block (cf2_policy_pack, one launch)."""
+        from . import _native
         dev = next(self.ac.parameters()).device
-        self.w = pack_policy_weights(self.ac).to(dev)
-        assert self.w.numel() == self.lib.cf2_policy_weights_count(self.obs_dim)
+        flat = pack_policy_weights(self.ac).to(dev)
+        assert flat.numel() == self.lib.cf2_policy_weights_count(self.obs_dim)
+        self.w = torch.empty(self.lib.cf2_policy_packed_count(self.obs_dim, self.prec), device=dev)
+        _native.check(self.lib.cf2_policy_pack(flat.data_ptr(), self.obs_dim, self.prec, self.w.data_ptr(),
+                                               torch.cuda.current_stream(dev).cuda_stream), "cf2_policy_pack")
 
     @torch.no_grad()
     def step(self, obs: torch.Tensor, deterministic: bool = False, row_offset: int = 0):
@@ -225,7 +237,7 @@ class FusedActorCritic:
         val = torch.empty(n, device=obs.device)
         logp = torch.empty(n, device=obs.device)
         _native.check(self.lib.cf2_policy_forward(
-            self.w.data_ptr(), n, self.obs_dim, obs.data_ptr(), self.seed, self.counter & 0xFFFFFFFF, row_offset,
+            self.w.data_ptr(), n, self.obs_dim, self.prec, obs.data_ptr(), self.seed, self.counter & 0xFFFFFFFF, row_offset,
             0 if deterministic else 1, act.data_ptr(), val.data_ptr(), logp.data_ptr(),
             torch.cuda.current_stream(obs.device).cuda_stream), "cf2_policy_forward")
         self.counter += 1
@@ -235,7 +247,8 @@ class FusedActorCritic:
     def step_into(self, obs: torch.Tensor, act: torch.Tensor, val: torch.Tensor, logp: torch.Tensor):
         from . import _native
         _native.check(self.lib.cf2_policy_forward(
-            self.w.data_ptr(), obs.shape[0], self.obs_dim, obs.data_ptr(), self.seed, self.counter & 0xFFFFFFFF, 0, 1,
+            self.w.data_ptr(), obs.shape[0], self.obs_dim, self.prec, obs.data_ptr(), self.seed,
+            self.counter & 0xFFFFFFFF, 0, 1,
             act.data_ptr(), val.data_ptr(), logp.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream),
             "cf2_policy_forward")
         self.counter += 1
@@ -244,7 +257,7 @@ class FusedActorCritic:
     def value_masked(self, obs: torch.Tensor, mask: torch.Tensor, out: torch.Tensor):
         from . import _native
         _native.check(self.lib.cf2_value_forward_masked(
-            self.w.data_ptr(), obs.shape[0], self.obs_dim, obs.contiguous().data_ptr(),
+            self.w.data_ptr(), obs.shape[0], self.obs_dim, self.prec, obs.contiguous().data_ptr(),
             mask.to(torch.uint8).contiguous().data_ptr(), out.data_ptr(),
             torch.cuda.current_stream(obs.device).cuda_stream), "cf2_value_forward_masked")
         return out

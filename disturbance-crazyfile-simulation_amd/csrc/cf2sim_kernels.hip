@@ -1351,7 +1351,11 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
         }
         __syncthreads();
         TSTAMP(4);   // block barrier passed
+#ifdef CF2_AB_NO_RESET
+        const uint32_t cnt = 0;      // A/B only: measures the auto-reset tail's share
+#else
         const uint32_t cnt = *s_cnt;
+#endif
         // Resets run in chunks of C envs.  Their ~26 Philox blocks per env are drawn by every
         // thread of the block in parallel into LDS; then one lane per env runs the reset math
         // on the table.  (On one lane each, the draws made the reset tail, which every wave of
@@ -1383,7 +1387,11 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
             // the resetting wave rotates with the block index, so that the resets of the blocks
             // sharing a CU do not all queue on one SIMD
             const uint32_t rl = tid - 64u * (blockIdx.x % (B / 64u));
+#ifdef CF2_AB_NO_RESET_MATH
+            if (rl < nc && P.N == 0u) {   // A/B only: draws kept, reset math skipped
+#else
             if (rl < nc) {
+#endif
                 const uint32_t pos = c0 + rl, t = s_list[pos];
                 const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
                 ResetSeed q;

@@ -7,15 +7,34 @@
 //       logp = Normal(mu, std).log_prob(a).sum(-1)                           (core.py:228-291)
 //   v:  obs -> Linear(64) -> tanh -> Linear(64) -> tanh -> Linear(1)      (MLPCritic)
 // As torch runs it, each layer is a separate GEMM plus an activation kernel, with 50- and 64-wide
-// activations round-tripping through HBM (~0.6 ms per step at 262k rows).  Here one lane owns
-// one row end to end: the obs row is staged through LDS (a block's rows are contiguous), the
-// activations never leave VGPRs, and the weights -- identical for every lane -- are scalar loads
-// (SGPR operands of packed v_pk_fma_f32, two output neurons per instruction).  fp32 throughout:
-// on gfx950 fp32 MFMA issues at the plain-VALU FMA rate, packed VALU at twice it.
+// activations round-tripping through HBM (~0.6 ms per step at 262k rows).  Here the whole network
+// runs on the matrix cores in one launch, fp32 activations and fp32 accumulation, in one of two
+// product precisions (cf2_policy_precision in include/cf2sim.h):
+//   CF2_POLICY_F32     v_mfma_f32_16x16x4_f32: exact fp32 (the result of an fmaf chain over k);
+//   CF2_POLICY_BF16X3  v_mfma_f32_16x16x32_bf16 on split operands, x = hi + lo (two bf16 words),
+//                      x*w ~ hi_x*hi_w + hi_x*lo_w + lo_x*hi_w: 16 significant bits per operand,
+//                      <= ~3 * 2^-18 relative error per product (1.1e-5, typically a few 1e-6),
+//                      at 3 bf16 MFMAs per 32-k block = 16/3 the fp32 rate.
 //
-// Weight block (floats, all matrices input-major so output neurons are contiguous):
+// Transposed formulation: every layer computes out^T[neuron][row] = W[neuron][k] * in^T[k][row],
+// weights as the A operand (16 neurons x k), activations as the B operand (k x 16 batch rows).
+// The accumulator of an n-tile t holds, in lane l and register i, neuron 16t + 4(l>>4) + i of
+// batch row l & 15.  Read as a B operand, that is a k-step whose k slot of lane group g = l >> 4
+// is neuron 16t + 4g + i (fp32: one register per k-step of 4; bf16: two tiles' 8 registers per
+// k-block of 32, slot (g, j) = neuron 16 t_{j/4} + 4g + (j % 4)).  The next layer's weights are
+// packed in that permuted k order (cf2_policy_pack), so activations go from layer to layer in
+// registers, with no LDS round trip and no cross-lane move.  Biases initialise the accumulators.
+//
+// Work split: persistent blocks of 4 waves; each wave runs chunks of 32 rows (2 row tiles, so
+// each weight fragment read from LDS feeds two MFMAs) and prefetches the next chunk's
+// observations while the current one runs.  The packed block (A-operand fragments, lane-ordered:
+// conflict-free ds_read_b32 / ds_read_b128) is staged into LDS once per block.
+//
+// Flat weight block (cf2_policy_weights_count floats; input-major so output neurons are contiguous):
 //   pi: W1[D][50] b1[50] W2[50][50] b2[50] W3[50][4] b3[4] log_std[4]
 //   v:  W1[D][64] b1[64] W2[64][64] b2[64] W3[64]    b3[1]
+//   obs standardisation (core.py:383-388, OnlineMeanStd): mean[D], scale[D] = 1 / (std + 1e-5);
+//   both networks see (obs - mean) * scale (identity: mean 0, scale 1)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "cf2sim_rng.h"
@@ -23,10 +42,8 @@
 
 namespace cf2 {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-// weights are read through the constant address space: scalar loads, and provably no alias of
-// the private activation arrays (a generic pointer laundered by asm would pin those to scratch)
-typedef const __attribute__((address_space(4))) float* cptr;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
 
 template <int D>
 struct PolicyLayout {
@@ -34,67 +51,189 @@ struct PolicyLayout {
                          P_B3 = P_W3 + 50 * 4, P_LOGSTD = P_B3 + 4;
     static constexpr int V_W1 = P_LOGSTD + 4, V_B1 = V_W1 + D * 64, V_W2 = V_B1 + 64, V_B2 = V_W2 + 64 * 64,
                          V_W3 = V_B2 + 64, V_B3 = V_W3 + 64;
-    static constexpr int TOTAL = V_B3 + 1;
+    static constexpr int O_MEAN = V_B3 + 1, O_SCALE = O_MEAN + D;     // observation standardisation
+    static constexpr int TOTAL = O_SCALE + D;
 };
 
-struct W16 { float w[16]; };
-__device__ __forceinline__ W16 load16(cptr p, int n) {
-    W16 r;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) r.w[k] = k < n ? p[k] : 0.0f;
-    return r;
+// fp32 k-steps over a C-layout activation of 4 tiles with V valid neurons: step (t, i) holds
+// neurons 16t + 4g + i (g = 0..3); steps with no valid neuron are skipped (pi: 50 -> 14, v: 16)
+constexpr int ksteps(int V) {
+    int n = 0;
+    for (int t = 0; t < 4; ++t)
+        for (int i = 0; i < 4; ++i) n += (16 * t + i < V) ? 1 : 0;
+    return n;
+}
+constexpr int kstep_t(int V, int s) {
+    for (int t = 0; t < 4; ++t)
+        for (int i = 0; i < 4; ++i)
+            if (16 * t + i < V && s-- == 0) return t;
+    return -1;
+}
+constexpr int kstep_i(int V, int s) {
+    for (int t = 0; t < 4; ++t)
+        for (int i = 0; i < 4; ++i)
+            if (16 * t + i < V && s-- == 0) return i;
+    return -1;
 }
 
-// y[OUT] = b + sum_i W[i][.] x[i]  (W input-major); two outputs per v_pk_fma_f32 with the weight
-// pair as an SGPR operand.  The flattened weights are walked in chunks of 16 (one
-// s_load_dwordx16), software-pipelined by hand: chunk c+1 is requested before chunk c's FMAs and
-// scheduling barriers keep the compiler from hoisting every load of the layer to the top (which
-// needs thousands of SGPRs and spills them to VGPR lanes).  A weight pair never straddles an
-// input row (OUT is even, chunks start at even flat indices).
-#ifndef CF2_POLICY_PREFETCH
-#define CF2_POLICY_PREFETCH 3   // chunks of 16 weights in flight ahead of the FMAs (16 SGPRs each)
-#endif
-constexpr int PF = CF2_POLICY_PREFETCH;
+// Neuron-level weights of the four GEMMs (0 for padding).  Layer 1 is the 128-wide [pi | v]
+// layer (rows 0..49 pi, 64..127 v); layer 3 has rows 0..3 = mu, row 4 = v over the 128-wide
+// [pi h2 | v h2] input (pi inputs 0..63, v inputs 64..127).
+template <int D>
+__device__ float w_l1(const float* __restrict__ W, int n, int in) {
+    using L = PolicyLayout<D>;
+    if (in >= D) return 0.0f;
+    if (n < 64) return n < 50 ? W[L::P_W1 + in * 50 + n] : 0.0f;
+    return W[L::V_W1 + in * 64 + (n - 64)];
+}
+template <int D>
+__device__ float w_l2p(const float* __restrict__ W, int n, int in) {
+    return (n < 50 && in < 50) ? W[PolicyLayout<D>::P_W2 + in * 50 + n] : 0.0f;
+}
+template <int D>
+__device__ float w_l2v(const float* __restrict__ W, int n, int in) { return W[PolicyLayout<D>::V_W2 + in * 64 + n]; }
+template <int D>
+__device__ float w_l3(const float* __restrict__ W, int n, int in) {
+    using L = PolicyLayout<D>;
+    if (in < 64) return (n < 4 && in < 50) ? W[L::P_W3 + in * 4 + n] : 0.0f;
+    return n == 4 ? W[L::V_W3 + in - 64] : 0.0f;
+}
 
-// one chunk of 16 flattened weights; recursion (not a loop) guarantees full unrolling, so the
-// input / accumulator indices are compile-time and x[] / acc[] stay in registers.  ring[k] holds
-// chunk C + k; the load of chunk C + PF is issued before chunk C's FMAs.
-template <int C, int NC, int IN, int OUT>
-struct Chunks {
-    static __device__ __forceinline__ void run(cptr W, const float* x, f2* acc, const W16 (&ring)[PF]) {
-        constexpr int TOT = IN * OUT;
-        W16 nring[PF];
-#pragma unroll
-        for (int k = 0; k + 1 < PF; ++k) nring[k] = ring[k + 1];
-        if constexpr (C + PF < NC) nring[PF - 1] = load16(W + 16 * (C + PF), TOT - 16 * (C + PF) < 16 ? TOT - 16 * (C + PF) : 16);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k = 0; k < 16; k += 2) {
-            const int f = 16 * C + k;
-            if (f < TOT) {
-                const int i = f / OUT, j = f % OUT;
-                acc[j / 2] = __builtin_elementwise_fma(f2{ring[0].w[k], ring[0].w[k + 1]}, f2{x[i], x[i]}, acc[j / 2]);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (C + 1 < NC) Chunks<C + 1, NC, IN, OUT>::run(W, x, acc, nring);
-    }
+// Packed block layout (floats).  fp32 fragments: 64 floats (lane l: A[16nt + (l&15)][k slot l>>4]).
+// bf16 fragments: 512 floats = hi[64 lanes][8 bf16] then lo[64 lanes][8 bf16] (lane l: k slots
+// 8(l>>4) .. 8(l>>4)+7).  Layer 1 in bf16x3 mode: D/32 bf16 blocks + fp32 k-steps for the rest.
+template <int D, int PREC>
+struct Packed {
+    static constexpr bool BF = PREC == CF2_POLICY_BF16X3;
+    static constexpr int KS1 = BF ? (D % 32 + 3) / 4 : (D + 3) / 4;     // fp32 k-steps of layer 1
+    static constexpr int KB1 = BF ? D / 32 : 0;                          // bf16 k-blocks of layer 1
+    static constexpr int K1R = 32 * KB1;                                 // first fp32 input of layer 1
+    static constexpr int KSP = ksteps(50), KSV = ksteps(64);
+    static constexpr int FB = 512, FF = 64;
+    static constexpr int O_L1B = 0, O_L1F = O_L1B + KB1 * 8 * FB, O_L2P = O_L1F + KS1 * 8 * FF;
+    static constexpr int N_L2 = BF ? 2 * 4 * FB : 0;
+    static constexpr int O_L2V = O_L2P + (BF ? N_L2 : KSP * 4 * FF);
+    static constexpr int O_L3 = O_L2V + (BF ? N_L2 : KSV * 4 * FF);
+    static constexpr int O_BIAS = O_L3 + (BF ? 4 * FB : (KSP + KSV) * FF);
+    static constexpr int B_L1 = 0, B_L2P = 128, B_L2V = 192, B_L3 = 256, NB = 272;   // neuron-ordered biases
+    static constexpr int O_LOGSTD = O_BIAS + NB, O_MEAN = O_LOGSTD + 4, O_SCALE = O_MEAN + D;
+    static constexpr int TOTAL = (O_SCALE + D + 3) / 4 * 4;
 };
 
-template <int IN, int OUT>
-__device__ __forceinline__ void dense(cptr W, cptr b, const float* x, float* y) {
-    static_assert(OUT % 2 == 0, "pairs of outputs");
-    constexpr int TOT = IN * OUT, NC = (TOT + 15) / 16;
-    f2 acc[OUT / 2];
+template <int D>
+__device__ float bias_value(const float* __restrict__ W, int k) {
+    using L = PolicyLayout<D>;
+    if (k < 128) return k < 50 ? W[L::P_B1 + k] : (k < 64 ? 0.0f : W[L::V_B1 + k - 64]);
+    if (k < 192) { const int n = k - 128; return n < 50 ? W[L::P_B2 + n] : 0.0f; }
+    if (k < 256) return W[L::V_B2 + k - 192];
+    const int n = k - 256;
+    return n < 4 ? W[L::P_B3 + n] : (n == 4 ? W[L::V_B3] : 0.0f);
+}
+
+// bf16 k-block element: fragment (layer, kb, nt), lane l, slot j -> weight
+template <int D>
+__device__ float bf16_weight(const float* __restrict__ W, int layer, int kb, int nt, int l, int j) {
+    const int n = 16 * nt + (l & 15), g = l >> 4;
+    if (layer == 1) return w_l1<D>(W, n, 32 * kb + 8 * g + j);
+    const int in = 16 * (2 * kb + (j >> 2)) + 4 * g + (j & 3);      // C-layout input, two tiles per block
+    if (layer == 2) return w_l2p<D>(W, n, in);
+    if (layer == 3) return w_l2v<D>(W, n, in);
+    return w_l3<D>(W, n, in);                                          // kb 0,1: pi h2; 2,3: v h2 (+64)
+}
+
+__device__ __forceinline__ uint32_t bf16_bits(float x) {
+    const __bf16 h = (__bf16)x;
+    return (uint32_t)__builtin_bit_cast(uint16_t, h);
+}
+
+// one packed word per thread
+template <int D, int PREC>
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, float* __restrict__ out) {
+    using P = Packed<D, PREC>;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= P::TOTAL) return;
+    float v = 0.0f;
+    auto bfword = [&](int layer, int rel, int nblk) -> float {
+        // rel: offset inside this layer's bf16 fragments; nblk: n-tiles per k-block
+        const int f = rel / P::FB, w = rel % P::FB, half = w / 256, lw = w % 256, l = lw / 4, pr = lw % 4;
+        const int kb = f / nblk, nt = f % nblk;
+        uint32_t bits = 0;
+        for (int e = 0; e < 2; ++e) {
+            const float x = bf16_weight<D>(W, layer, kb, nt, l, 2 * pr + e);
+            const float hi = (float)(__bf16)x;
+            bits |= (half ? bf16_bits(x - hi) : bf16_bits(x)) << (16 * e);
+        }
+        return __uint_as_float(bits);
+    };
+    if (k < P::O_L1F) {
+        v = bfword(1, k - P::O_L1B, 8);
+    } else if (k < P::O_L2P) {
+        const int r = k - P::O_L1F, f = r / 64, l = r % 64, ks = f / 8, nt = f % 8;
+        v = w_l1<D>(W, 16 * nt + (l & 15), P::K1R + 4 * ks + (l >> 4));
+    } else if (k < P::O_L2V) {
+        const int r = k - P::O_L2P;
+        if (P::BF) {
+            v = bfword(2, r, 4);
+        } else {
+            const int f = r / 64, l = r % 64, ks = f / 4, nt = f % 4;
+            v = w_l2p<D>(W, 16 * nt + (l & 15), 16 * kstep_t(50, ks) + 4 * (l >> 4) + kstep_i(50, ks));
+        }
+    } else if (k < P::O_L3) {
+        const int r = k - P::O_L2V;
+        if (P::BF) {
+            v = bfword(3, r, 4);
+        } else {
+            const int f = r / 64, l = r % 64, ks = f / 4, nt = f % 4;
+            v = w_l2v<D>(W, 16 * nt + (l & 15), 16 * kstep_t(64, ks) + 4 * (l >> 4) + kstep_i(64, ks));
+        }
+    } else if (k < P::O_BIAS) {
+        const int r = k - P::O_L3;
+        if (P::BF) {
+            v = bfword(4, r, 1);
+        } else {
+            const int ks = r / 64, l = r % 64, n = l & 15, g = l >> 4;
+            v = ks < P::KSP ? w_l3<D>(W, n, 16 * kstep_t(50, ks) + 4 * g + kstep_i(50, ks))
+                            : w_l3<D>(W, n, 64 + 16 * kstep_t(64, ks - P::KSP) + 4 * g + kstep_i(64, ks - P::KSP));
+        }
+    } else if (k < P::O_LOGSTD) {
+        v = bias_value<D>(W, k - P::O_BIAS);
+    } else if (k < P::O_MEAN) {
+        v = W[PolicyLayout<D>::P_LOGSTD + (k - P::O_LOGSTD)];
+    } else if (k < P::O_SCALE) {
+        v = W[PolicyLayout<D>::O_MEAN + (k - P::O_MEAN)];
+    } else if (k < P::O_SCALE + D) {
+        v = W[PolicyLayout<D>::O_SCALE + (k - P::O_SCALE)];
+    }
+    out[k] = v;
+}
+
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// split-bf16 product of one 32-k block: small terms first, then hi*hi
+__device__ __forceinline__ f4v mfma3(const bf8v& ah, const bf8v& al, const bf8v& bh, const bf8v& bl, f4v c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+// x -> (hi, lo) bf16 operands
+__device__ __forceinline__ void split8(const float (&x)[8], bf8v& hi, bf8v& lo) {
 #pragma unroll
-    for (int j = 0; j < OUT / 2; ++j) acc[j] = f2{b[2 * j], b[2 * j + 1]};
-    W16 ring[PF];
-#pragma unroll
-    for (int k = 0; k < PF; ++k)
-        if (k < NC) ring[k] = load16(W + 16 * k, TOT - 16 * k < 16 ? TOT - 16 * k : 16);
-    Chunks<0, NC, IN, OUT>::run(W, x, acc, ring);
-#pragma unroll
-    for (int j = 0; j < OUT / 2; ++j) { y[2 * j] = acc[j].x; y[2 * j + 1] = acc[j].y; }
+    for (int j = 0; j < 8; ++j) {
+        hi[j] = (__bf16)x[j];
+        lo[j] = (__bf16)(x[j] - (float)hi[j]);
+    }
+}
+// B operand of k-block (t0, t0 + 1) from two C-layout tiles
+__device__ __forceinline__ void split_tiles(const f4v& a, const f4v& b, bf8v& hi, bf8v& lo) {
+    const float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    split8(x, hi, lo);
+}
+__device__ __forceinline__ void ld_frag(const float* sw, int off, int l, bf8v& hi, bf8v& lo) {
+    const float4 h = *reinterpret_cast<const float4*>(sw + off + 4 * l);
+    const float4 o = *reinterpret_cast<const float4*>(sw + off + 256 + 4 * l);
+    hi = __builtin_bit_cast(bf8v, h);
+    lo = __builtin_bit_cast(bf8v, o);
 }
 
 // tanh(x) = sign(x) (1 - 2 / (exp(2|x|) + 1)) on v_exp_f32 / v_rcp_f32 (abs error < 2e-7)
@@ -103,89 +242,289 @@ __device__ __forceinline__ float tanh_fast(float x) {
     return __builtin_copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
 }
 
-template <int D>
-__device__ __forceinline__ float value_net(cptr W, const float* x) {
-    using L = PolicyLayout<D>;
-    float h1[64], h2[64];
-    dense<D, 64>(W + L::V_W1, W + L::V_B1, x, h1);
+enum : uint32_t { TAG_POLICY = 3 };
+#ifndef CF2_POLICY_RT
+#define CF2_POLICY_RT 2          // row tiles (16 rows each) per wave chunk: each fragment read feeds RT MFMAs
+#endif
+#ifndef CF2_POLICY_BLOCK
+#define CF2_POLICY_BLOCK 256     // threads per block (one staged copy of the fragments per block)
+#endif
+#ifndef CF2_POLICY_WAVES
+#define CF2_POLICY_WAVES 2       // waves per SIMD the register budget is sized for
+#endif
+constexpr int RT = CF2_POLICY_RT;
+constexpr int CHUNK = 16 * RT;
+constexpr int PB = CF2_POLICY_BLOCK, PW = PB / 64;
+
+// The observations of one chunk, raw fp32: per row tile the bf16 k-blocks' 8 consecutive inputs
+// of this lane's group (x8) and the fp32 k-steps' single inputs (x1).  Loads are unconditional
+// (indices clamped into the buffer): a row past n is never written out and an input index past
+// D meets a zero weight; branch-free loads keep the waitcnt counting exact, so the prefetch of
+// the next chunk stays in flight under this chunk's MFMAs.
+template <int D, int PREC>
+struct ObsRegs {
+    using P = Packed<D, PREC>;
+    float x8[RT][P::KB1 > 0 ? P::KB1 : 1][8];
+    float x1[RT][P::KS1];
+};
+template <int D, int PREC>
+__device__ __forceinline__ void load_obs(const float* __restrict__ obs, uint32_t n, uint32_t r0, int l,
+                                         ObsRegs<D, PREC>& X) {
+    using P = Packed<D, PREC>;
 #pragma unroll
-    for (int j = 0; j < 64; ++j) h1[j] = tanh_fast(h1[j]);
-    dense<64, 64>(W + L::V_W2, W + L::V_B2, h1, h2);
-    float v = W[L::V_B3];
+    for (int rt = 0; rt < RT; ++rt) {
+        const uint32_t row = __builtin_elementwise_min(r0 + 16 * rt + (uint32_t)(l & 15), n - 1u);
+        const float* src = obs + (size_t)row * D;
 #pragma unroll
-    for (int j = 0; j < 64; ++j) v = __builtin_fmaf(W[L::V_W3 + j], tanh_fast(h2[j]), v);
-    return v;
+        for (int kb = 0; kb < P::KB1; ++kb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {     // rows are 8-B aligned (D even): 4 x float2
+                const float2 v = *reinterpret_cast<const float2*>(src + 32 * kb + 8 * (l >> 4) + 2 * q);
+                X.x8[rt][kb][2 * q] = v.x;
+                X.x8[rt][kb][2 * q + 1] = v.y;
+            }
+#pragma unroll
+        for (int ks = 0; ks < P::KS1; ++ks)
+            X.x1[rt][ks] = src[__builtin_elementwise_min(P::K1R + 4 * ks + (l >> 4), D - 1)];
+    }
 }
 
-enum : uint32_t { TAG_POLICY = 3 };
-
 // mode: 0 = policy (mu, sample, logp) + value of every row; 1 = value only, rows with mask[r] != 0
-template <int D, int MODE>
-__global__ void __launch_bounds__(256) policy_kernel(const float* __restrict__ Wg, uint32_t n,
-                                                     const float* __restrict__ obs, uint32_t key0, uint32_t key1,
-                                                     uint32_t counter, uint32_t row_offset, int sample,
-                                                     float* __restrict__ act, float* __restrict__ val,
-                                                     float* __restrict__ logp, const uint8_t* __restrict__ mask) {
-    using L = PolicyLayout<D>;
-    constexpr uint32_t B = 256;
-    const cptr W = (cptr)Wg;
-    __shared__ __align__(16) float s_x[B * D];
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, r = base + tid;
-    const uint32_t nvalid = n - base < B ? n - base : B;
+template <int D, int PREC, int MODE>
+__global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const float* __restrict__ Wp, uint32_t n,
+                                                                      const float* __restrict__ obs, uint32_t key0,
+                                                                      uint32_t key1, uint32_t counter,
+                                                                      uint32_t row_offset, int sample,
+                                                                      float* __restrict__ act, float* __restrict__ val,
+                                                                      float* __restrict__ logp,
+                                                                      const uint8_t* __restrict__ mask) {
+    using P = Packed<D, PREC>;
+    constexpr bool PI = MODE == 0, BF = P::BF;
+    __shared__ __align__(16) float s_w[P::TOTAL];
+    const uint32_t nchunks = (n + CHUNK - 1) / CHUNK;
+    const uint32_t wave = blockIdx.x * PW + (threadIdx.x >> 6), nwaves = gridDim.x * PW;
     if (MODE == 1) {
-        // value-only pass (time-out bootstraps): nothing to do for a block without marked rows
-        const int m = r < n ? (int)mask[r] : 0;
-        if (!__syncthreads_or(m)) return;
-    }
-    {   // stage the block's rows (contiguous, 16-B aligned: B * D * 4 is a multiple of 16)
-        const float* src = obs + (size_t)base * D;
-        if (nvalid == B && (B * D) % 4 == 0) {
-            const float4* s4 = reinterpret_cast<const float4*>(src);
-            float4* d4 = reinterpret_cast<float4*>(s_x);
-            for (uint32_t k = tid; k < B * D / 4; k += B) d4[k] = s4[k];
-        } else {
-            for (uint32_t k = tid; k < nvalid * D; k += B) s_x[k] = src[k];
+        // value-only pass (time-out bootstraps, usually no row marked): a block none of whose
+        // chunks has a marked row exits before staging the weights
+        int any = 0;
+        for (uint32_t c = wave; c < nchunks; c += nwaves) {
+            const uint32_t rr = c * CHUNK + (uint32_t)(threadIdx.x & 63);
+            any |= ((threadIdx.x & 63) < CHUNK && rr < n && mask[rr] != 0) ? 1 : 0;
         }
+        if (!__syncthreads_or(any)) return;
+    }
+    {
+        const float4* src = reinterpret_cast<const float4*>(Wp);
+        float4* dst = reinterpret_cast<float4*>(s_w);
+        for (int k = threadIdx.x; k < P::TOTAL / 4; k += PB) dst[k] = src[k];
     }
     __syncthreads();
-    if (r >= n) return;
-    if (MODE == 1 && !mask[r]) return;
-    // the obs row is read from LDS once per network, so it is not live across the value net
-    float x[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = s_x[tid * D + k];
-    const float v = value_net<D>(W, x);
-    val[r] = v;
-    if (MODE == 1) return;
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = s_x[tid * D + k];
-    float h1[50], h2[50], mu[4];
-    dense<D, 50>(W + L::P_W1, W + L::P_B1, x, h1);
-#pragma unroll
-    for (int j = 0; j < 50; ++j) h1[j] = fmaxf(h1[j], 0.0f);
-    dense<50, 50>(W + L::P_W2, W + L::P_B2, h1, h2);
-#pragma unroll
-    for (int j = 0; j < 50; ++j) h2[j] = fmaxf(h2[j], 0.0f);
-    dense<50, 4>(W + L::P_W3, W + L::P_B3, h2, mu);
-    float eps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (sample) {
-        const Keys K = make_keys(key0, key1);
-        const U4 u = philox(K, 0u, counter, row_offset + r, TAG_POLICY);
-        box_muller(u.x, u.y, eps[0], eps[1]);
-        box_muller(u.z, u.w, eps[2], eps[3]);
-    }
-    float lp = 0.0f;
-    float4 a;
-    float* ap = &a.x;
+    const int l = threadIdx.x & 63, r16 = l & 15, g = l >> 4;
+    float ls[4], sd[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float ls = W[L::P_LOGSTD + k];
-        ap[k] = mu[k] + __builtin_amdgcn_exp2f(1.4426950408889634f * ls) * eps[k];
-        lp += -0.5f * eps[k] * eps[k] - ls - 0.91893853320467274f;    // 0.5 log(2 pi)
+        ls[k] = s_w[P::O_LOGSTD + k];
+        sd[k] = __builtin_amdgcn_exp2f(1.4426950408889634f * ls[k]);
     }
-    reinterpret_cast<float4*>(act)[r] = a;
-    if (logp) logp[r] = sample ? lp : 1.0f;
+    // this lane's standardisation constants (its input indices do not change between chunks)
+    float mean8[P::KB1 > 0 ? P::KB1 : 1][8], scale8[P::KB1 > 0 ? P::KB1 : 1][8], mean1[P::KS1], scale1[P::KS1];
+#pragma unroll
+    for (int kb = 0; kb < P::KB1; ++kb)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            mean8[kb][j] = s_w[P::O_MEAN + 32 * kb + 8 * g + j];
+            scale8[kb][j] = s_w[P::O_SCALE + 32 * kb + 8 * g + j];
+        }
+#pragma unroll
+    for (int ks = 0; ks < P::KS1; ++ks) {
+        const int k = __builtin_elementwise_min(P::K1R + 4 * ks + g, D - 1);
+        mean1[ks] = s_w[P::O_MEAN + k];
+        scale1[ks] = s_w[P::O_SCALE + k];
+    }
+    ObsRegs<D, PREC> X;
+    if (wave < nchunks) load_obs<D, PREC>(obs, n, wave * CHUNK, l, X);
+    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+        const uint32_t r0 = c * CHUNK;
+        // the fragments are loop-invariant: without an opaque base the compiler hoists all LDS
+        // reads out of the chunk loop and spills them (an integer offset, not a laundered pointer:
+        // the reads must stay LDS reads)
+        int off = 0;
+        asm volatile("" : "+v"(off));
+        const float* sw = s_w + off;
+        ObsRegs<D, PREC> Xc = X;
+        // observation standardisation (obs - mean) * scale, per input index of this lane
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+            for (int kb = 0; kb < P::KB1; ++kb)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) Xc.x8[rt][kb][j] = (Xc.x8[rt][kb][j] - mean8[kb][j]) * scale8[kb][j];
+#pragma unroll
+            for (int ks = 0; ks < P::KS1; ++ks) Xc.x1[rt][ks] = (Xc.x1[rt][ks] - mean1[ks]) * scale1[ks];
+        }
+        // prefetch the next chunk's observations while this one runs on the matrix cores
+        if (c + nwaves < nchunks) load_obs<D, PREC>(obs, n, (c + nwaves) * CHUNK, l, X);
+        if (MODE == 1) {
+            const uint32_t rr = r0 + (uint32_t)l;
+            if (!__builtin_amdgcn_ballot_w64(l < CHUNK && rr < n && mask[rr] != 0)) continue;
+        }
+        // ---- layer 1: [pi | v] 128 neurons (8 n-tiles); MODE 1 runs only the v half
+        constexpr int NT0 = PI ? 0 : 4;
+        f4v h1[8][RT];
+#pragma unroll
+        for (int nt = NT0; nt < 8; ++nt) {
+            const f4v b = *reinterpret_cast<const f4v*>(&sw[P::O_BIAS + P::B_L1 + 16 * nt + 4 * g]);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = b;
+        }
+#pragma unroll
+        for (int kb = 0; kb < P::KB1; ++kb) {
+            bf8v bh[RT], bl[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) split8(Xc.x8[rt][kb], bh[rt], bl[rt]);
+#pragma unroll
+            for (int nt = NT0; nt < 8; ++nt) {
+                bf8v ah, al;
+                ld_frag(sw, P::O_L1B + (kb * 8 + nt) * P::FB, l, ah, al);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = mfma3(ah, al, bh[rt], bl[rt], h1[nt][rt]);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < P::KS1; ++ks)
+#pragma unroll
+            for (int nt = NT0; nt < 8; ++nt) {
+                const float a = sw[P::O_L1F + (ks * 8 + nt) * P::FF + l];
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = mfma4(a, Xc.x1[rt][ks], h1[nt][rt]);
+            }
+#pragma unroll
+        for (int nt = NT0; nt < 8; ++nt)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h1[nt][rt][i] = nt < 4 ? fmaxf(h1[nt][rt][i], 0.0f) : tanh_fast(h1[nt][rt][i]);
+        // ---- layer 2: pi 50 -> 50 (ReLU), v 64 -> 64 (tanh); inputs straight from the layer-1 accumulators
+        f4v h2p[4][RT], h2v[4][RT];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const f4v bp = *reinterpret_cast<const f4v*>(&sw[P::O_BIAS + P::B_L2P + 16 * nt + 4 * g]);
+            const f4v bv = *reinterpret_cast<const f4v*>(&sw[P::O_BIAS + P::B_L2V + 16 * nt + 4 * g]);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) { h2p[nt][rt] = bp; h2v[nt][rt] = bv; }
+        }
+#pragma unroll
+        for (int half = PI ? 0 : 1; half < 2; ++half) {      // 0: pi, 1: v
+            f4v(&acc)[4][RT] = half ? h2v : h2p;
+            const int O = half ? P::O_L2V : P::O_L2P, T0 = half ? 4 : 0;
+            if constexpr (BF) {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) {
+                    bf8v bh[RT], bl[RT];
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt)
+                        split_tiles(h1[T0 + 2 * kb][rt], h1[T0 + 2 * kb + 1][rt], bh[rt], bl[rt]);
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) {
+                        bf8v ah, al;
+                        ld_frag(sw, O + (kb * 4 + nt) * P::FB, l, ah, al);
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) acc[nt][rt] = mfma3(ah, al, bh[rt], bl[rt], acc[nt][rt]);
+                    }
+                }
+            } else {
+                constexpr int V0 = 50, V1 = 64;
+#pragma unroll
+                for (int ks = 0; ks < (half ? P::KSV : P::KSP); ++ks) {
+                    const int t = half ? kstep_t(V1, ks) : kstep_t(V0, ks), i = half ? kstep_i(V1, ks) : kstep_i(V0, ks);
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) {
+                        const float a = sw[O + (ks * 4 + nt) * P::FF + l];
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) acc[nt][rt] = mfma4(a, h1[T0 + t][rt][i], acc[nt][rt]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (PI) h2p[nt][rt][i] = fmaxf(h2p[nt][rt][i], 0.0f);
+                    h2v[nt][rt][i] = tanh_fast(h2v[nt][rt][i]);
+                }
+        // ---- layer 3: one n-tile, rows 0..3 = mu, row 4 = v
+        f4v o[RT];
+        {
+            const f4v b = *reinterpret_cast<const f4v*>(&sw[P::O_BIAS + P::B_L3 + 4 * g]);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) o[rt] = b;
+        }
+#pragma unroll
+        for (int half = PI ? 0 : 1; half < 2; ++half) {
+            f4v(&h)[4][RT] = half ? h2v : h2p;
+            if constexpr (BF) {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) {
+                    bf8v ah, al;
+                    ld_frag(sw, P::O_L3 + (2 * half + kb) * P::FB, l, ah, al);
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) {
+                        bf8v bh, bl;
+                        split_tiles(h[2 * kb][rt], h[2 * kb + 1][rt], bh, bl);
+                        o[rt] = mfma3(ah, al, bh, bl, o[rt]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < (half ? P::KSV : P::KSP); ++ks) {
+                    const int t = half ? kstep_t(64, ks) : kstep_t(50, ks), i = half ? kstep_i(64, ks) : kstep_i(50, ks);
+                    const float a = sw[P::O_L3 + ((half ? P::KSP : 0) + ks) * P::FF + l];
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) o[rt] = mfma4(a, h[t][rt][i], o[rt]);
+                }
+            }
+        }
+        // lanes 0..15 hold mu[0..3] of row 16 rt + l, lanes 16..31 hold v in register 0
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const uint32_t row = r0 + 16 * rt + r16;
+            if (row >= n) continue;
+            if (g == 1 && (MODE == 0 || mask[row])) val[row] = o[rt][0];
+            if (PI && g == 0) {
+                float eps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (sample) {
+                    const Keys K = make_keys(key0, key1);
+                    const U4 u = philox(K, 0u, counter, row_offset + row, TAG_POLICY);
+                    box_muller(u.x, u.y, eps[0], eps[1]);
+                    box_muller(u.z, u.w, eps[2], eps[3]);
+                }
+                float lp = 0.0f;
+                float4 a;
+                float* ap = &a.x;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    ap[k] = o[rt][k] + sd[k] * eps[k];
+                    lp += -0.5f * eps[k] * eps[k] - ls[k] - 0.91893853320467274f;    // 0.5 log(2 pi)
+                }
+                reinterpret_cast<float4*>(act)[row] = a;
+                if (logp) logp[row] = sample ? lp : 1.0f;
+            }
+        }
+    }
+}
+
+static int policy_grid(uint32_t n) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t want = (n + PW * CHUNK - 1) / (PW * CHUNK);
+    // resident blocks per CU: LDS (~58-62 KB of fragments per block) and the wave budget
+    const uint32_t by_waves = (uint32_t)(4 * CF2_POLICY_WAVES / PW);
+    const uint32_t per_cu = by_waves < 2u ? (by_waves ? by_waves : 1u) : 2u;
+    const uint32_t cap = per_cu * (uint32_t)cus;
+    return (int)(want < cap ? want : cap);
 }
 
 // Batched GAE (algs/core.py:459-535 finish_path per episode slice, with per-env boundaries):
@@ -238,44 +577,88 @@ extern "C" int cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float
     return e == hipSuccess ? CF2_OK : CF2_ERR_HIP;
 }
 
+template <int D, int PREC>
+static int policy_launch(const float* packed_dev, uint32_t n, const float* obs_dev, uint32_t k0, uint32_t k1,
+                         uint32_t counter, uint32_t row_offset, int sample, float* act_dev, float* val_dev,
+                         float* logp_dev, const uint8_t* mask_dev, hipStream_t s) {
+    const dim3 grid(policy_grid(n)), block(PB);
+    if (mask_dev)
+        hipLaunchKernelGGL((policy_kernel<D, PREC, 1>), grid, block, 0, s, packed_dev, n, obs_dev, 0u, 0u, 0u, 0u, 0,
+                           nullptr, val_dev, nullptr, mask_dev);
+    else
+        hipLaunchKernelGGL((policy_kernel<D, PREC, 0>), grid, block, 0, s, packed_dev, n, obs_dev, k0, k1, counter,
+                           row_offset, sample, act_dev, val_dev, logp_dev, nullptr);
+    return hipGetLastError() == hipSuccess ? CF2_OK : CF2_ERR_HIP;
+}
+
+static int policy_dispatch(const float* packed_dev, uint32_t n, uint32_t obs_dim, int precision, const float* obs_dev,
+                           uint32_t k0, uint32_t k1, uint32_t counter, uint32_t row_offset, int sample, float* act_dev,
+                           float* val_dev, float* logp_dev, const uint8_t* mask_dev, hipStream_t s) {
+#define CF2_POLICY_CASE(D_, P_)                                                                                \
+    if (obs_dim == D_ && precision == P_)                                                                      \
+        return policy_launch<D_, P_>(packed_dev, n, obs_dev, k0, k1, counter, row_offset, sample, act_dev,      \
+                                     val_dev, logp_dev, mask_dev, s);
+    CF2_POLICY_CASE(34, CF2_POLICY_F32)
+    CF2_POLICY_CASE(34, CF2_POLICY_BF16X3)
+    CF2_POLICY_CASE(42, CF2_POLICY_F32)
+    CF2_POLICY_CASE(42, CF2_POLICY_BF16X3)
+#undef CF2_POLICY_CASE
+    return CF2_ERR_UNSUPPORTED;
+}
+
+static bool policy_shape_ok(uint32_t obs_dim, int precision) {
+    return (obs_dim == 34 || obs_dim == 42) && (precision == CF2_POLICY_F32 || precision == CF2_POLICY_BF16X3);
+}
+
 extern "C" size_t cf2_policy_weights_count(uint32_t obs_dim) {
     if (obs_dim == 34) return PolicyLayout<34>::TOTAL;
     if (obs_dim == 42) return PolicyLayout<42>::TOTAL;
     return 0;
 }
 
-extern "C" int cf2_policy_forward(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
-                                  uint64_t seed, uint32_t counter, uint32_t row_offset, int sample, float* act_dev,
-                                  float* val_dev, float* logp_dev, void* stream) {
-    if (!weights_dev || !obs_dev || !act_dev || !val_dev) return CF2_ERR_INVALID_ARG;
-    if (obs_dim != 34 && obs_dim != 42) return CF2_ERR_UNSUPPORTED;
-    if (((uintptr_t)obs_dev & 15u) || ((uintptr_t)act_dev & 15u)) return CF2_ERR_INVALID_ARG;
-    if (n == 0) return CF2_OK;
-    const dim3 grid((n + 255) / 256), block(256);
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    if (obs_dim == 34)
-        hipLaunchKernelGGL((policy_kernel<34, 0>), grid, block, 0, (hipStream_t)stream, weights_dev, n, obs_dev, k0, k1,
-                           counter, row_offset, sample, act_dev, val_dev, logp_dev, nullptr);
-    else
-        hipLaunchKernelGGL((policy_kernel<42, 0>), grid, block, 0, (hipStream_t)stream, weights_dev, n, obs_dev, k0, k1,
-                           counter, row_offset, sample, act_dev, val_dev, logp_dev, nullptr);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? CF2_OK : CF2_ERR_HIP;
+extern "C" size_t cf2_policy_packed_count(uint32_t obs_dim, int precision) {
+    if (!policy_shape_ok(obs_dim, precision)) return 0;
+    if (obs_dim == 34) return precision == CF2_POLICY_F32 ? Packed<34, CF2_POLICY_F32>::TOTAL : Packed<34, CF2_POLICY_BF16X3>::TOTAL;
+    return precision == CF2_POLICY_F32 ? Packed<42, CF2_POLICY_F32>::TOTAL : Packed<42, CF2_POLICY_BF16X3>::TOTAL;
 }
 
-extern "C" int cf2_value_forward_masked(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
-                                        const uint8_t* mask_dev, float* val_dev, void* stream) {
-    if (!weights_dev || !obs_dev || !mask_dev || !val_dev) return CF2_ERR_INVALID_ARG;
-    if (obs_dim != 34 && obs_dim != 42) return CF2_ERR_UNSUPPORTED;
-    if ((uintptr_t)obs_dev & 15u) return CF2_ERR_INVALID_ARG;
-    if (n == 0) return CF2_OK;
-    const dim3 grid((n + 255) / 256), block(256);
-    if (obs_dim == 34)
-        hipLaunchKernelGGL((policy_kernel<34, 1>), grid, block, 0, (hipStream_t)stream, weights_dev, n, obs_dev, 0u, 0u, 0u,
-                           0u, 0, nullptr, val_dev, nullptr, mask_dev);
+extern "C" int cf2_policy_pack(const float* weights_dev, uint32_t obs_dim, int precision, float* packed_dev,
+                               void* stream) {
+    if (!weights_dev || !packed_dev) return CF2_ERR_INVALID_ARG;
+    if (!policy_shape_ok(obs_dim, precision)) return CF2_ERR_UNSUPPORTED;
+    if ((uintptr_t)packed_dev & 15u) return CF2_ERR_INVALID_ARG;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint32_t total = (uint32_t)cf2_policy_packed_count(obs_dim, precision);
+    const dim3 grid((total + 255) / 256), block(256);
+    if (obs_dim == 34 && precision == CF2_POLICY_F32)
+        hipLaunchKernelGGL((pack_kernel<34, CF2_POLICY_F32>), grid, block, 0, s, weights_dev, packed_dev);
+    else if (obs_dim == 34)
+        hipLaunchKernelGGL((pack_kernel<34, CF2_POLICY_BF16X3>), grid, block, 0, s, weights_dev, packed_dev);
+    else if (precision == CF2_POLICY_F32)
+        hipLaunchKernelGGL((pack_kernel<42, CF2_POLICY_F32>), grid, block, 0, s, weights_dev, packed_dev);
     else
-        hipLaunchKernelGGL((policy_kernel<42, 1>), grid, block, 0, (hipStream_t)stream, weights_dev, n, obs_dev, 0u, 0u, 0u,
-                           0u, 0, nullptr, val_dev, nullptr, mask_dev);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? CF2_OK : CF2_ERR_HIP;
+        hipLaunchKernelGGL((pack_kernel<42, CF2_POLICY_BF16X3>), grid, block, 0, s, weights_dev, packed_dev);
+    return hipGetLastError() == hipSuccess ? CF2_OK : CF2_ERR_HIP;
+}
+
+extern "C" int cf2_policy_forward(const float* packed_dev, uint32_t n, uint32_t obs_dim, int precision,
+                                  const float* obs_dev, uint64_t seed, uint32_t counter, uint32_t row_offset,
+                                  int sample, float* act_dev, float* val_dev, float* logp_dev, void* stream) {
+    if (!packed_dev || !obs_dev || !act_dev || !val_dev) return CF2_ERR_INVALID_ARG;
+    if (!policy_shape_ok(obs_dim, precision)) return CF2_ERR_UNSUPPORTED;
+    if (((uintptr_t)obs_dev & 7u) || ((uintptr_t)act_dev & 15u) || ((uintptr_t)packed_dev & 15u))
+        return CF2_ERR_INVALID_ARG;
+    if (n == 0) return CF2_OK;
+    return policy_dispatch(packed_dev, n, obs_dim, precision, obs_dev, (uint32_t)seed, (uint32_t)(seed >> 32), counter,
+                           row_offset, sample, act_dev, val_dev, logp_dev, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int cf2_value_forward_masked(const float* packed_dev, uint32_t n, uint32_t obs_dim, int precision,
+                                        const float* obs_dev, const uint8_t* mask_dev, float* val_dev, void* stream) {
+    if (!packed_dev || !obs_dev || !mask_dev || !val_dev) return CF2_ERR_INVALID_ARG;
+    if (!policy_shape_ok(obs_dim, precision)) return CF2_ERR_UNSUPPORTED;
+    if (((uintptr_t)obs_dev & 7u) || ((uintptr_t)packed_dev & 15u)) return CF2_ERR_INVALID_ARG;
+    if (n == 0) return CF2_OK;
+    return policy_dispatch(packed_dev, n, obs_dim, precision, obs_dev, 0u, 0u, 0u, 0u, 0, nullptr, val_dev, nullptr,
+                           mask_dev, (hipStream_t)stream);
 }

@@ -241,21 +241,32 @@ int  cf2_hj_disturbance(const cf2_config* cfg, const float* V_dev, const float* 
 
 /* ---- batched rollout caller ----
  * Gaussian MLP actor-critic forward of the reference's PPO networks for a batch of observations,
- * one fused launch: ActorCritic.step (algs/core.py:371-395), MLPGaussianActor (core.py:228-291)
- * pi D->50->50->4 ReLU, MLPCritic D->64->64->1 tanh (algs/ppo/defaults.py:8-13).  fp32.
- * weights_dev: cf2_policy_weights_count(D) floats (layout in csrc/cf2sim_policy.hip: input-major
- * matrices, pi then v, log_std after the pi head); obs_dev [n, D] (D = 34 or 42, 16-B aligned);
- * sample != 0: act = mu + exp(log_std) * eps, eps ~ N(0,1) from Philox keyed (seed,
- * counter, row + row_offset); else act = mu.  Outputs act_dev [n,4] (16-B aligned), val_dev [n],
- * logp_dev [n] (sum of Normal log-densities; may be NULL). */
+ * one fused launch on the matrix cores: ActorCritic.step (algs/core.py:371-395), MLPGaussianActor
+ * (core.py:228-291) pi D->50->50->4 ReLU, MLPCritic D->64->64->1 tanh (algs/ppo/defaults.py:8-13).
+ * fp32 activations and accumulation; products in one of two precisions:
+ *   CF2_POLICY_F32     exact fp32 (v_mfma_f32_16x16x4_f32, the result of an fmaf chain over k);
+ *   CF2_POLICY_BF16X3  split-bf16 operands (x = hi + lo, three bf16 MFMAs per product block):
+ *                      <= ~1.1e-5 relative error per product, ~5x the fp32 rate.
+ * Weights: the flat block (cf2_policy_weights_count(D) floats; layout in csrc/cf2sim_policy.hip:
+ * input-major matrices, pi then v, log_std after the pi head) is converted once per weight update
+ * by cf2_policy_pack into the packed block (cf2_policy_packed_count(D, precision) floats, 16-B
+ * aligned: MFMA operand fragments in the kernel's order) that the forward calls take with the
+ * same precision.
+ * obs_dev [n, D] (D = 34 or 42, 8-B aligned); sample != 0: act = mu + exp(log_std) * eps,
+ * eps ~ N(0,1) from Philox keyed (seed, counter, row + row_offset); else act = mu.  Outputs
+ * act_dev [n,4] (16-B aligned), val_dev [n], logp_dev [n] (sum of Normal log-densities; may be
+ * NULL). */
+enum cf2_policy_precision { CF2_POLICY_F32 = 0, CF2_POLICY_BF16X3 = 1 };
 size_t cf2_policy_weights_count(uint32_t obs_dim);
-int  cf2_policy_forward(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
+size_t cf2_policy_packed_count(uint32_t obs_dim, int precision);
+int  cf2_policy_pack(const float* weights_dev, uint32_t obs_dim, int precision, float* packed_dev, void* stream);
+int  cf2_policy_forward(const float* packed_dev, uint32_t n, uint32_t obs_dim, int precision, const float* obs_dev,
                         uint64_t seed, uint32_t counter, uint32_t row_offset, int sample,
                         float* act_dev, float* val_dev, float* logp_dev, void* stream);
 /* Value of the rows with mask_dev[r] != 0 only (time-out bootstraps V(final obs)); other rows of
  * val_dev are left untouched. */
-int  cf2_value_forward_masked(const float* weights_dev, uint32_t n, uint32_t obs_dim, const float* obs_dev,
-                              const uint8_t* mask_dev, float* val_dev, void* stream);
+int  cf2_value_forward_masked(const float* packed_dev, uint32_t n, uint32_t obs_dim, int precision,
+                              const float* obs_dev, const uint8_t* mask_dev, float* val_dev, void* stream);
 
 /* Batched GAE over [T, n] rollout buffers (algs/core.py:459-535 finish_path on every env's
  * episode slices): done/trunc uint8 (terminal -> bootstrap 0, time-out -> trunc_val), the end of

@@ -18,13 +18,14 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--env-id", default="DroneHoverBulletFreeEnvWithGust-v0")
     ap.add_argument("--torch-policy", action="store_true", help="torch layers instead of the fused HIP policy")
+    ap.add_argument("--precision", default="fp32", help="fused policy products: fp32 | bf16x3")
     args = ap.parse_args()
     from cf2sim.rollout import FusedActorCritic, MLPActorCritic, collect
     from cf2sim.vec_env import BatchedCrazyflieEnv
     envs = BatchedCrazyflieEnv(args.env_id, args.envs, seed=0, want_final_obs=True)
     ac = MLPActorCritic().cuda()
     if not args.torch_policy:
-        ac = FusedActorCritic(ac, seed=0)
+        ac = FusedActorCritic(ac, seed=0, precision=args.precision)
     g = torch.Generator(device="cuda").manual_seed(0)
     obs = envs.reset()
     collect(envs, ac, 4, obs=obs, generator=g)          # warm-up (kernels, GEMM heuristics)
@@ -52,7 +53,7 @@ def main():
     print(json.dumps({"rollout_env_steps_per_s": args.envs * args.steps / dt, "ms_per_step": dt / args.steps * 1e3,
                       "policy_ms_per_step": pol_ms, "env_ms_per_step": env_ms, "envs": args.envs,
                       "steps": args.steps, "env_id": args.env_id,
-                      "policy": "torch" if args.torch_policy else "fused HIP"}))
+                      "policy": "torch" if args.torch_policy else f"fused HIP ({args.precision})"}))
     envs.close()
 
 
