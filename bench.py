@@ -116,20 +116,23 @@ def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
                       f"(2048 envs x 600 env-steps, {dt1:.1f} s)"}
 
 
+def step_kernel_key() -> str:
+    """Content key of the step kernel's build (kernel source, headers, flags: cf2sim.build), so a
+    traffic measurement stays valid across rebuilds that do not touch the step kernel."""
+    from cf2sim.build import _obj_key
+    return _obj_key("cf2sim_kernels.hip")
+
+
 def load_traffic(workload_key: str):
     """Per-launch HBM bytes of the step kernel from rocprofv3 PMC passes (tools/pmc_traffic.sh),
-    used only if they were measured on this workload with this very library build (content stamp
-    of libcf2sim.so); otherwise None."""
+    used only if they were measured on this workload with this very kernel build; otherwise None."""
     p = os.path.join(ROOT, "profiles", "step_kernel_traffic.json")
-    stamp = os.path.join(ROOT, "disturbance-crazyfile-simulation_amd", "cf2sim", "libcf2sim.so.stamp")
     try:
         with open(p) as f:
             d = json.load(f)
-        with open(stamp) as f:
-            cur = f.read().strip()
-        if d.get("workload") == workload_key and d.get("library_stamp") == cur:
+        if d.get("workload") == workload_key and d.get("kernel_key") == step_kernel_key():
             return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+    except (OSError, ValueError, ImportError):
         pass
     return None
 

@@ -21,6 +21,12 @@ def mean_counter(d, name, kern):
     return sum(v) / len(v)
 
 
+def kernel_key():
+    sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+    from cf2sim.build import _obj_key
+    return _obj_key("cf2sim_kernels.hip")
+
+
 N = 262144
 calib_rd = N * 4 * 84
 calib_wr = N * 4 * (72 + 34)
@@ -38,7 +44,7 @@ res = {
     "calibration": {"kernel": "tools/membench.hip SoA R84 W72 +obs34 (4 B/lane)", "known_read_bytes": calib_rd,
                     "known_write_bytes": calib_wr, "FETCH_SIZE_bytes": c_f, "WRITE_SIZE_bytes": c_w,
                     "read_factor": kr, "write_factor": kw},
-    "library_stamp": open(os.path.join(ROOT, "disturbance-crazyfile-simulation_amd", "cf2sim", "libcf2sim.so.stamp")).read().strip(),
+    "kernel_key": kernel_key(),
     "note": "FETCH_SIZE/WRITE_SIZE count L2 memory-side requests; Infinity-Cache hits are counted "
             "(MI355X_MICROARCH.md HBM section), so this is L2->fabric traffic.",
 }
