@@ -125,6 +125,19 @@ __device__ __forceinline__ void normals_range(const G& g, uint32_t b0, float* z)
     }
 }
 
+// (the reset table already holds the Box-Muller outputs of its normal slots)
+template <int LO, int HI>
+__device__ __forceinline__ void normals_range(const TableRng& g, uint32_t b0, float* z) {
+#pragma unroll
+    for (int blk = LO / 4; blk < (HI + 3) / 4; ++blk) {
+        const U4 u = g.block(b0 + blk);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (4 * blk + k >= LO && 4 * blk + k < HI) z[4 * blk + k] = __uint_as_float(w[k]);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // rotation helpers (PyBullet C-API semantics)
 // ------------------------------------------------------------------------------------
@@ -899,12 +912,18 @@ __device__ __forceinline__ float downwash(const KParams& P, const float p[3], ui
 // ------------------------------------------------------------------------------------
 // reset (base.py:420-464 + task_specific_reset + apply_domain_randomization)
 // ------------------------------------------------------------------------------------
-template <bool NOISE, bool DR, int PHYS, class G>
-__device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, uint32_t gid, float* out) {
+// The reset in three pieces (reset_env runs them in order; the step kernel's auto-reset runs them
+// on different waves, see block_epilogue):
+//   reset_kinematics  initial pose / velocities (task_specific_reset hover_free.py:237-289), motor
+//                     state and latency ring, last action, readback -- what the observation needs;
+//   reset_params      domain randomisation (base.py:241-298), const-wind draw, Boltzmann level;
+//   reset_observe     the two reset sensor calls (base.py:444-456 incl. the stale-rpy_dot LPF
+//                     seed) and the history / observation row.
+template <int PHYS, class G>
+__device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const G& g, uint32_t gid) {
     const U4 b0 = g.block(0), b1 = g.block(1), b2 = g.block(2), b3 = g.block(3);
     const uint32_t u[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
                             b2.x, b2.y, b2.z, b2.w, b3.x, b3.y, b3.z, b3.w};
-    const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
     E.ep_step = 0;
     E.props_on = 0;
 #pragma unroll
@@ -957,7 +976,21 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
     const M3 R0 = rotmat(quat);
     float ww[3];
     mtv(R0, rate, ww);
-    // domain randomization
+    if (PHYS == PHYS_BULLET_T) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.w[k] = ww[k];
+        euler_from_quat(E.q, E.rpy);
+        mtv(R0, E.w, E.wb);      // R(q) of the reset quaternion
+    } else {
+        euler_from_quat(E.q, E.rpy);
+        mtv(R0, ww, E.wb);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) E.w[k] = E.wb[k];
+    }
+}
+
+template <bool DR, class G>
+__device__ __forceinline__ void reset_params(const KParams& P, Env& E, const G& g) {
     E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
     E.k0 = P.ft0; E.k1 = P.ft1;
 #pragma unroll
@@ -994,24 +1027,25 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
         }
         E.gust_left = 0;
     }
+    if (P.level_mode == LEVEL_BOLTZMANN_T) {          // the new episode's level (after the const-wind draw)
+        E.level_idx = boltzmann_index(P, u01(g.block(3).y));
+        E.level = P.tab->level_values[E.level_idx];
+    }
+}
+
+// stale: the finished episode's body rates (the gyro LPF seed); E.bias is the never-reset gyro bias.
+// half: 0 = both calls and the whole observation row; 1 = the first call only, out[0 .. OL+4)
+// (o_0 and A_0); 2 = the second call and out[OL+4 .. OD) (o_1, A_1), the first call's gyro walk
+// only (its held measurement is not needed there).
+template <bool NOISE, int HALF, class G>
+__device__ __forceinline__ void reset_observe(const KParams& P, Env& E, const G& g, const float stale[3], float* out) {
+    constexpr int OL = NOISE ? 13 : 17;
     if (NOISE) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) E.lpf[k] = stale[k];
     }
-    if (PHYS == PHYS_BULLET_T) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.w[k] = ww[k];
-        euler_from_quat(E.q, E.rpy);
-        mtv(R0, E.w, E.wb);      // R(q) of the reset quaternion
-    } else {
-        euler_from_quat(E.q, E.rpy);
-        mtv(R0, ww, E.wb);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.w[k] = E.wb[k];
-    }
     float o0[17], o1[17];
-    compute_observation<NOISE>(P, E, g, 32, 0, o0);
-    constexpr int OL = NOISE ? 13 : 17;
+    compute_observation<NOISE>(P, E, g, 32, 0, o0, HALF != 2);
 #pragma unroll
     for (int k = 0; k < OL; ++k) E.obs_prev[k] = o0[k];
     E.halias0 = E.halias1 = 1;
@@ -1019,12 +1053,40 @@ __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, 
     for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int k = 0; k < 4; ++k) E.hact[s][k] = E.la[k];
-    compute_observation<NOISE>(P, E, g, 40, 0, o1);
-    compute_history<NOISE>(P, E, o1, out);
-    if (P.level_mode == LEVEL_BOLTZMANN_T) {
-        E.level_idx = boltzmann_index(P, u01(u[13]));
-        E.level = P.tab->level_values[E.level_idx];
+    if (HALF == 1) {
+#pragma unroll
+        for (int k = 0; k < OL; ++k) out[k] = o0[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[OL + k] = E.la[k];      // halias0: the action buffer's last entry
+        return;
     }
+    compute_observation<NOISE>(P, E, g, 40, 0, o1);
+    if (HALF == 2) {
+#pragma unroll
+        for (int k = 0; k < OL; ++k) { out[OL + 4 + k] = o1[k]; E.obs_prev[k] = o1[k]; }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[2 * OL + 4 + k] = E.la[k];
+        E.halias0 = E.halias1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.hact[0][k] = E.hact[1][k];
+        E.halias1 = E.la_view;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E.hact[1][k] = E.la[k];
+        return;
+    }
+    compute_history<NOISE>(P, E, o1, out);
+}
+
+template <bool NOISE, bool DR, int PHYS, class G>
+__device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, uint32_t gid, float* out) {
+    const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
+    reset_kinematics<PHYS>(P, E, g, gid);
+    const int level_idx0 = E.level_idx;
+    const float level0 = E.level;
+    reset_params<DR>(P, E, g);
+    // reset_observe does not read the level; keep the redrawn one
+    (void)level_idx0; (void)level0;
+    reset_observe<NOISE, 0>(P, E, g, stale, out);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1199,6 +1261,10 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         // of the env-step is not a full one (aggregate_phy_steps % obs_rate != 0)
         compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy, P.held_persistent != 0);
     }
+    // the history (o_{k-1}, last actions) is only read by compute_history: the one-step kernel
+    // loads it after the physics, so its 21 registers are not live across the sub-steps (the final
+    // sensor call hides the load latency; -0.6 us at 262144 envs)
+    if (STORE) load_hist<NOISE>(Tile(io.sf, P.N, i), E);
     float onx[17];
     TREADY("v"(E.q[3]), "v"(E.lpf[2]));
     TSTAMP(2);   // physics sub-steps done
@@ -1252,9 +1318,10 @@ template <bool NOISE, bool DR, int PHYS>
 __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
                                          ResetSeed& rs, const double* hj_grid) {
     Env E;
-    // every state load is issued up front: on gfx9 vmcnt also counts stores, so a load issued
-    // after the state stores would wait for the whole store burst to drain
-    load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/true);
+    // every state load is issued before the first state store: on gfx9 vmcnt also counts stores,
+    // so a load issued after the state stores would wait for the whole store burst to drain (the
+    // history is loaded after the physics sub-steps, still ahead of store_core, in step_env_body)
+    load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
     return step_env_body<NOISE, DR, PHYS, true>(P, io, i, E, obs_row, rs, hj_grid);
 }
 
@@ -1316,6 +1383,87 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
     for (int k = 0; k < OD; k += 2) *reinterpret_cast<float2*>(obs_row + k) = make_float2(o[k], o[k + 1]);
     store_env<NOISE, DR, PHYS>(P, sf, i, E, true);
     TSTAMP(8);   // reset stores issued
+}
+
+// One quarter of an auto-reset (block_epilogue runs the four roles on four waves at once; the
+// union of their stores is store_env(params_dirty) and of their row writes the reset
+// observation, as reset_env + store_env produce them):
+//   0: kinematics, motor state, ring           -> groups 0-6(+ring), 12 (Simple), 28
+//   1: kinematics + the first sensor call      -> obs row o_0 | A_0
+//   2: kinematics + the second sensor call     -> obs row o_1 | A_1; groups 10, 11, 14-19, 21-23
+//   3: domain randomisation, disturbance, level -> groups 13, 24-27, 29
+// Roles 1 and 2 recompute the reset pose from the same table entries, so the critical path is one
+// pose + one sensor call instead of the whole reset.
+template <bool NOISE, bool DR, int PHYS>
+__device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__ sf, uint32_t i, const ResetSeed& rs,
+                                           const TableRng& g, float* __restrict__ obs_row, uint32_t role) {
+    constexpr int OL = NOISE ? 13 : 17;
+    const Tile T(sf, P.N, i);
+    const uint32_t gid = P.gid_off + i;
+    Env E;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { E.wb[k] = rs.wb[k]; E.bias[k] = rs.bias[k]; }
+    const float stale[3] = {rs.wb[0], rs.wb[1], rs.wb[2]};
+    if (role == 3) {
+        E.level = rs.level;
+        E.level_idx = rs.level_idx;
+        reset_params<DR>(P, E, g);
+        if (dstb_stored(P)) T.st(G_DSTB, f4(E.dstb[0], E.dstb[1], E.dstb[2], 0.0f));
+        if (DR) {
+            T.st(G_PARAM, f4(E.dt, E.m, E.J[0], E.J[1]));
+            T.st(G_PARAM + 1, f4(E.J[2], E.k0, E.k1, E.B[0]));
+            T.st(G_PARAM + 2, f4(E.B[1], E.B[2], E.B[3], E.K[0]));
+        }
+        T.st(G_LEVEL, f4(E.K[1], E.K[2], E.K[3], E.level));
+        T.st(G_LEVEL_IDX, f4(ib(E.level_idx), 0.0f, 0.0f, 0.0f));
+        return;
+    }
+    reset_kinematics<PHYS>(P, E, g, gid);
+    if (role == 0) {
+        T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
+        T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
+        T.st(2, f4(E.v[1], E.v[2], E.w[0], E.w[1]));
+        const int fl = (E.aidx & 15) | (1 << 4) | (1 << 5) | (E.la_view << 6) | (E.props_on << 7);   // halias0/1 = 1
+        T.st(G_CORE3, f4(E.w[2], ib(0), ib((int)(rs.ctr + 1u)), ib(fl)));
+        T.st(G_MOTOR, f4(E.x[0], E.x[1], E.x[2], E.x[3]));
+        if (P.use_motor_dyn) T.st(G_MOTOR_LO, f4(0.0f, 0.0f, 0.0f, 0.0f));
+        T.st(G_OU, f4(rs.ou[0], rs.ou[1], rs.ou[2], rs.ou[3]));
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (r < P.buf_size) T.st(G_ABUF + r, f4(E.abuf[r][0], E.abuf[r][1], E.abuf[r][2], E.abuf[r][3]));
+        if (PHYS == PHYS_SIMPLE_T) T.st(G_RPY, f4(E.rpy[0], E.rpy[1], E.rpy[2], 0.0f));
+        return;
+    }
+    if (role == 1) {
+        float o[OL + 4];
+        reset_observe<NOISE, 1>(P, E, g, stale, o);
+#pragma unroll
+        for (int k = 0; k < OL + 4; ++k) obs_row[k] = o[k];
+        return;
+    }
+    float o[2 * (OL + 4)];
+    reset_observe<NOISE, 2>(P, E, g, stale, o);
+#pragma unroll
+    for (int k = OL + 4; k < 2 * (OL + 4); ++k) obs_row[k] = o[k];
+    if (NOISE || gust_mode(P))
+        T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(0)));
+    if (NOISE) {
+        T.st(G_LPF, f4(E.lpf[0], E.lpf[1], E.lpf[2], 0.0f));
+        if (P.held_persistent) {
+            T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
+            T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
+            T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
+        }
+    }
+    T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
+    T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
+#pragma unroll
+    for (int g4 = 0; g4 < (OL + 3) / 4; ++g4) {
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = 4 * g4 + k < OL ? E.obs_prev[4 * g4 + k] : 0.0f;
+        T.st(G_OBSP + g4, f4(v[0], v[1], v[2], v[3]));
+    }
 }
 
 // End of a block's env-step: list the finished envs (wave ballot + one LDS atomic per wave), reset
@@ -1384,14 +1532,38 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
                 }
             }
             __syncthreads();
+#ifndef CF2_RESET_ONE_WAVE
+            if (B == 256u) {
+                // four waves split each reset by role (reset_role); the role of a wave rotates with
+                // the block index so the co-resident blocks' roles spread over the SIMDs
+                const uint32_t rl = tid & 63u, role = ((tid >> 6) + blockIdx.x) & 3u;
+                const bool act = rl < nc;
+                ResetSeed q;
+                uint32_t t = 0;
+                if (act) {
+                    t = s_list[c0 + rl];
+                    const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(row[c]); q.bias[c] = __uint_as_float(row[3 + c]); }
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(row[6 + c]);
+                    q.level = __uint_as_float(row[10]);
+                    q.level_idx = (int)row[11];
+                    q.ctr = row[12];
+                }
+                __syncthreads();     // every role has its seed before roles 1 and 2 overwrite the rows
+                if (act) {
+                    const TableRng tg{s_rand + rl, C};
+                    reset_role<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD, role);
+                }
+                __syncthreads();     // the next chunk reuses s_rand
+                continue;
+            }
+#endif
             // the resetting wave rotates with the block index, so that the resets of the blocks
             // sharing a CU do not all queue on one SIMD
             const uint32_t rl = tid - 64u * (blockIdx.x % (B / 64u));
-#ifdef CF2_AB_NO_RESET_MATH
-            if (rl < nc && P.N == 0u) {   // A/B only: draws kept, reset math skipped
-#else
             if (rl < nc) {
-#endif
                 const uint32_t pos = c0 + rl, t = s_list[pos];
                 const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
                 ResetSeed q;
@@ -1403,7 +1575,19 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
                 q.level_idx = (int)row[11];
                 q.ctr = row[12];
                 const TableRng tg{s_rand + rl, C};
+#ifdef CF2_AB_CHEAP_RESET
+                // A/B only: a minimal reset (hover pose, zeroed obs row) in place of the reset math
+                {
+                    const Tile T(io.sf, P.N, base + t);
+                    T.st(0, f4(P.init_xyz[0], P.init_xyz[1], P.init_xyz[2], 0.0f));
+                    T.st(1, f4(0.0f, 0.0f, 1.0f, 0.0f));
+                    T.st(2, f4(0.0f, 0.0f, 0.0f, 0.0f));
+                    T.st(G_CORE3, f4(0.0f, ib(0), ib((int)(q.ctr + 1u)), ib(0)));
+                    for (int k = 0; k < OD; ++k) s_obs[t * OD + k] = __uint_as_float(tg.t[k * C]);
+                }
+#else
                 reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD);
+#endif
             }
             __syncthreads();     // the next chunk reuses s_rand
         }
