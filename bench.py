@@ -151,6 +151,8 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=16384)
     ap.add_argument("--cpu-steps", type=int, default=1000)
     ap.add_argument("--env-kw", default="{}", help="JSON env kwargs (ablations), e.g. '{\"observation_noise\": 0}'")
+    ap.add_argument("--rollout-k", type=int, default=32,
+                    help="also time the fused K-step rollout (cf2_rollout, random actions) on 1 GPU; 0 = skip")
     args = ap.parse_args()
     env_kw = json.loads(args.env_kw)
 
@@ -251,6 +253,26 @@ def main():
         torch.cuda.synchronize()
         kern_ms = sum(a.elapsed_time(b) for a, b in ev) / 20
 
+    fused = None
+    if world == 1 and args.rollout_k > 0:
+        # the north star's "synthetic random-action rollouts" with the actions known in advance:
+        # K env-steps per launch, the state in registers; every step's outputs written to its slab
+        K = args.rollout_k
+        racts = torch.rand(K, n, 4, device=dev, generator=g) * 2 - 1
+        env.rollout(racts)                                   # warm-up (allocates the output slabs)
+        torch.cuda.synchronize()
+        reps = 3
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
+        for _ in range(reps):
+            env.rollout(racts)
+        f1.record(stream)
+        torch.cuda.synchronize()
+        us = f0.elapsed_time(f1) * 1e3 / (reps * K)
+        fused = {"value": n / (us * 1e-6), "unit": "env-steps/s", "us_per_env_step": us, "k": K,
+                 "outputs": "obs, rew, done, trunc, cost, level per step (K slabs)"}
+        del racts
+
     total_env_steps = n * args.steps * world
     value = total_env_steps / elapsed
     bytes_per = algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
@@ -286,6 +308,7 @@ def main():
                          "algorithmic_bytes_per_env_step": bytes_per,
                          "kernel_ms_per_launch": kern_ms},
             "cpu_baseline": cpu,
+            "fused_rollout": fused,
         }
         print(json.dumps(line), flush=True)
     env.close()

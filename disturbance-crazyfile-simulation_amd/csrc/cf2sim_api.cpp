@@ -19,6 +19,8 @@ struct cf2_ctx {
     KTables T;
     KTables* tab_dev = nullptr;
     float* sf = nullptr;           // internal AoSoA state, state_bytes(N)
+    uint8_t* hj_bits = nullptr;    // per-node HJ sign bits of the bound tables
+    size_t hj_bits_bytes = 0;
     int device = 0;
 };
 
@@ -152,6 +154,7 @@ static void fill_params(const cf2_config* c, KParams& P) {
     P.gust_max = (float)c->gust_max_level;
     P.tab = nullptr;
     P.V = nullptr;
+    P.hj_bits = nullptr;
 }
 
 extern "C" {
@@ -205,6 +208,7 @@ int cf2_destroy(cf2_ctx* ctx) {
     if (!ctx) return CF2_ERR_INVALID_ARG;
     hipError_t e1 = hipFree(ctx->sf);
     (void)hipFree(ctx->tab_dev);
+    if (ctx->hj_bits) (void)hipFree(ctx->hj_bits);
     delete ctx;
     if (e1 != hipSuccess) return hip_fail(e1);
     return CF2_OK;
@@ -233,9 +237,25 @@ int cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables, const i
     for (int l = 0; l < ctx->cfg.num_levels; ++l)
         if (table_of_level[l] >= num_tables) return CF2_ERR_INVALID_ARG;
     for (int l = 0; l < ctx->cfg.num_levels; ++l) ctx->T.table_of_level[l] = table_of_level[l];
-    const hipError_t e = hipMemcpy(ctx->tab_dev, &ctx->T, sizeof(KTables), hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpy(ctx->tab_dev, &ctx->T, sizeof(KTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e);
+    // Derived per-node sign bits (distur_gener's rule over the 7 taps around each node): the
+    // env-step gathers one byte per env instead of 7 floats.  Derived once per binding: rebind
+    // after changing the table contents.
+    const size_t need = (size_t)num_tables * (size_t)HJ_TABLE;
+    if (need > ctx->hj_bits_bytes) {
+        if (ctx->hj_bits) (void)hipFree(ctx->hj_bits);
+        ctx->hj_bits = nullptr;
+        ctx->hj_bits_bytes = 0;
+        e = hipMalloc(&ctx->hj_bits, need);
+        if (e != hipSuccess) return hip_fail(e);
+        ctx->hj_bits_bytes = need;
+    }
+    e = launch_hj_sign_table(V_dev, (uint32_t)num_tables, ctx->hj_bits, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess) return hip_fail(e);
     ctx->P.V = V_dev;
+    ctx->P.hj_bits = ctx->hj_bits;
     return CF2_OK;
 }
 

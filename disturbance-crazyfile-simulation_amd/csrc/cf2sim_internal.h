@@ -96,6 +96,7 @@ struct KParams {
     float dw_coeff[3], prop_radius, formation_dx, formation_dz;
     const struct KTables* tab;   // device-resident lookup tables (dynamically indexed)
     const float* V;              // HJ value tables [num_tables][15^6]
+    const uint8_t* hj_bits;      // per-node disturbance sign bits of V [num_tables][15^6] (cf2_bind_hj_tables)
 };
 
 // Lookup tables indexed with per-env (divergent) indices: kept in device memory, not in the
@@ -134,5 +135,7 @@ hipError_t launch_state_convert(const KParams& P, float* sf, float* state_f, int
 struct HjGrid { double p[6][HJ_PTS]; };   // grid nodes by value (hj_kernel kernarg)
 hipError_t launch_hj(const HjGrid& G, const double umax[3], const float* V, const float* states, uint32_t n,
                      float level, float* dstb, float* uopt, hipStream_t s);
+// the sign bits hj_signs derives from the 7 taps around each grid node, for every node of every table
+hipError_t launch_hj_sign_table(const float* V, uint32_t num_tables, uint8_t* bits, hipStream_t s);
 
 }  // namespace cf2

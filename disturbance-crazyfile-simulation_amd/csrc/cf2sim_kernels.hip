@@ -274,14 +274,11 @@ __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f
 // returns bit i set <=> dV/dx_{3+i} > 0 (opt disturbance = -dmax_i).  grid: the 6 x 15 grid
 // points (KTables::hj_grid) staged in LDS by the calling kernel: the nearest-node searches then
 // cost LDS round trips instead of serialised global loads.
-__device__ __forceinline__ unsigned hj_signs(const float* __restrict__ V, const double st[6], const double* grid) {
-    int idx[6];
-#pragma unroll
-    for (int d = 0; d < 6; ++d) idx[d] = grid_nearest(grid + d * HJ_PTS, st[d]);
+// distur_gener's sign rule at grid node c (flat index) with per-dim indices idx: for each rate
+// dimension d = 3..5 the one-sided differences L, R of V around the node (GridProcessing.py
+// spatial derivative with the boundary extrapolation of distur_gener.py:160-183), bit d-3 = L > -R
+__device__ __forceinline__ unsigned hj_node_bits(const float* __restrict__ V, int c, const int idx[6]) {
     const int stride[6] = {759375, 50625, 3375, 225, 15, 1};
-    int c = 0;
-#pragma unroll
-    for (int d = 0; d < 6; ++d) c += idx[d] * stride[d];
     const float Vc = V[c];
     unsigned bits = 0;
 #pragma unroll
@@ -304,6 +301,22 @@ __device__ __forceinline__ unsigned hj_signs(const float* __restrict__ V, const 
         bits |= (L > -Rr ? 1u : 0u) << i;
     }
     return bits;
+}
+// nearest grid node of a state (Grid.get_index, GridProcessing.py:52-71): flat index and per-dim indices
+__device__ __forceinline__ int hj_node(const double st[6], const double* grid, int idx[6]) {
+    const int stride[6] = {759375, 50625, 3375, 225, 15, 1};
+    int c = 0;
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+        idx[d] = grid_nearest(grid + d * HJ_PTS, st[d]);
+        c += idx[d] * stride[d];
+    }
+    return c;
+}
+__device__ __forceinline__ unsigned hj_signs(const float* __restrict__ V, const double st[6], const double* grid) {
+    int idx[6];
+    const int c = hj_node(st, grid, idx);
+    return hj_node_bits(V, c, idx);
 }
 
 // every thread of the block takes part (contains a block barrier)
@@ -1236,7 +1249,11 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
             float e[3];
             quat2euler(E.q, e);
             const double st[6] = {(double)e[0], (double)e[1], (double)e[2], (double)E.wb[0], (double)E.wb[1], (double)E.wb[2]};
-            const unsigned bits = hj_signs(P.V + (size_t)t * HJ_TABLE, st, hj_grid);
+            // the node's sign bits were derived from its 7 taps once per table (cf2_bind_hj_tables):
+            // one byte gathered per env-step instead of 7 scattered floats of the 45.6 MB table
+            int idx[6];
+            const int c = hj_node(st, hj_grid, idx);
+            const unsigned bits = P.hj_bits[(size_t)t * HJ_TABLE + (size_t)c];
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const float dm = (float)((double)E.level * (double)P.umax_d[k]);
@@ -1575,19 +1592,7 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
                 q.level_idx = (int)row[11];
                 q.ctr = row[12];
                 const TableRng tg{s_rand + rl, C};
-#ifdef CF2_AB_CHEAP_RESET
-                // A/B only: a minimal reset (hover pose, zeroed obs row) in place of the reset math
-                {
-                    const Tile T(io.sf, P.N, base + t);
-                    T.st(0, f4(P.init_xyz[0], P.init_xyz[1], P.init_xyz[2], 0.0f));
-                    T.st(1, f4(0.0f, 0.0f, 1.0f, 0.0f));
-                    T.st(2, f4(0.0f, 0.0f, 0.0f, 0.0f));
-                    T.st(G_CORE3, f4(0.0f, ib(0), ib((int)(q.ctr + 1u)), ib(0)));
-                    for (int k = 0; k < OD; ++k) s_obs[t * OD + k] = __uint_as_float(tg.t[k * C]);
-                }
-#else
                 reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD);
-#endif
             }
             __syncthreads();     // the next chunk reuses s_rand
         }
@@ -1909,6 +1914,19 @@ __global__ void state_convert_kernel(uint32_t N, float* __restrict__ sf, float* 
 
 // the grid nodes arrive by value in the kernarg segment (720 B): the stand-alone call needs no
 // device table, allocation or host synchronisation
+// one thread per grid node: the sign bits hj_signs would compute for any state nearest to it
+__global__ void __launch_bounds__(256) hj_sign_table_kernel(const float* __restrict__ V, uint32_t total,
+                                                            uint8_t* __restrict__ bits) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= total) return;
+    const uint32_t t = k / (uint32_t)HJ_TABLE, c = k - t * (uint32_t)HJ_TABLE;
+    int idx[6];
+    uint32_t r = c;
+#pragma unroll
+    for (int d = 5; d >= 0; --d) { idx[d] = (int)(r % HJ_PTS); r /= HJ_PTS; }
+    bits[k] = (uint8_t)hj_node_bits(V + (size_t)t * HJ_TABLE, (int)c, idx);
+}
+
 __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, const float* __restrict__ states,
                           uint32_t n, float level, float* __restrict__ dstb, float* __restrict__ uopt) {
     __shared__ double s_grid[6 * HJ_PTS];
@@ -2091,6 +2109,12 @@ hipError_t launch_init(const KParams& P, float* sf, hipStream_t s) {
     hipLaunchKernelGGL(init_kernel, grid, block, 0, s, P, sf);
     return hipGetLastError();
 }
+hipError_t launch_hj_sign_table(const float* V, uint32_t num_tables, uint8_t* bits, hipStream_t s) {
+    const uint32_t total = num_tables * (uint32_t)HJ_TABLE;
+    hipLaunchKernelGGL(hj_sign_table_kernel, dim3((total + 255) / 256), dim3(256), 0, s, V, total, bits);
+    return hipGetLastError();
+}
+
 hipError_t launch_hj(const HjGrid& G, const double umax[3], const float* V, const float* states, uint32_t n,
                      float level, float* dstb, float* uopt, hipStream_t s) {
     if (n == 0) return hipSuccess;

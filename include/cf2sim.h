@@ -192,7 +192,11 @@ int  cf2_layout_get(const cf2_ctx* ctx, cf2_layout* out);
 
 /* Bind HJ value tables: V_dev = [num_tables][15^6] float32 C-order [roll,pitch,yaw,p,q,r]
  * (the on-disk fastrack_{level}_15x15.npy format).  table_level_index maps Boltzmann level
- * index -> table row (or -1 = no table, dstb 0).  Caller owns V_dev for the ctx lifetime. */
+ * index -> table row (or -1 = no table, dstb 0).  Caller owns V_dev for the ctx lifetime.
+ * Binding derives, once, the disturbance sign bits of every grid node (the distur_gener rule over
+ * the node's 7 value taps, distur_gener.py:155-183; 1 byte per node, 11.4 MB per table, owned by
+ * the ctx): the env-step gathers one byte per env.  Rebind after changing the table contents.
+ * Synchronous. */
 int  cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables,
                         const int32_t* table_of_level /* host, num_levels entries */);
 
