@@ -16,8 +16,11 @@ HEADERS = ["cf2sim_internal.h", "cf2sim_rng.h"]
 # ~1 ulp) and the hardware sin/cos/log are allowed: the kernel is compared against the fp32 and
 # fp64 CPU restatements with stated tolerances (tests/test_gpu_parity.py), not bitwise.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=fast",
-         "-fgpu-approx-transcendentals", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-pass-failed",
-         "-fno-slp-vectorize"]   # SLP-packed v_pk_* f32 ops need register-pair shuffles that cost more than they save
+         "-fgpu-approx-transcendentals", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-pass-failed"]
+# per-source extras: the env-step kernels without SLP vectorisation (packed v_pk_* f32 ops need
+# register-pair shuffles that cost more than they save there: +3 us); the policy kernel with it
+# (its activation splits / tanh / ReLU pack pairwise: -2 us of 41.6 at 262144 rows)
+SOURCE_FLAGS = {"cf2sim_kernels.hip": ["-fno-slp-vectorize"], "cf2sim_api.cpp": ["-fno-slp-vectorize"]}
 
 
 def _hipcc() -> str:
@@ -47,12 +50,12 @@ def _headers_blob() -> bytes:
     return b"".join(_read(os.path.join(SRC_DIR, h)) for h in HEADERS) + _read(os.path.join(INC_DIR, "cf2sim.h"))
 
 
-def _compile_flags():
-    return [f for f in FLAGS if f != "-shared"] + ["-c"]
+def _compile_flags(src: str | None = None):
+    return [f for f in FLAGS if f != "-shared"] + SOURCE_FLAGS.get(src, []) + ["-c"]
 
 
 def _obj_key(src: str) -> str:
-    return _digest(" ".join(_compile_flags()).encode(), _read(os.path.join(SRC_DIR, src)), _headers_blob())
+    return _digest(" ".join(_compile_flags(src)).encode(), _read(os.path.join(SRC_DIR, src)), _headers_blob())
 
 
 def _lib_key() -> str:
@@ -85,7 +88,7 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         key = _obj_key(src)
         if not force and os.path.exists(obj) and _stamp(obj) == key:
             continue
-        cmd = [_hipcc(), *_compile_flags(), "-I", INC_DIR, "-o", obj + ".tmp", os.path.join(SRC_DIR, src)]
+        cmd = [_hipcc(), *_compile_flags(src), "-I", INC_DIR, "-o", obj + ".tmp", os.path.join(SRC_DIR, src)]
         if verbose:
             print(" ".join(cmd))
         procs.append((subprocess.Popen(cmd), obj, key))

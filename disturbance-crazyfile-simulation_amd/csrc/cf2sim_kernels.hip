@@ -263,9 +263,15 @@ __device__ __forceinline__ void quat2euler(const float q[4], float e[3]) {
 // HJ value-table gather (7 taps: centre and +-1 along the three rate dims)
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int grid_nearest(const double* pts, double s) {
+    // searchsorted(side='left') on the sorted nodes = the number of nodes below s: a branch-free
+    // binary search over 16 slots (slot 15 is +inf), 4 compares instead of 15
+    static_assert(HJ_PTS == 15, "16-slot search");
     int idx = 0;
 #pragma unroll
-    for (int k = 0; k < HJ_PTS; ++k) idx += pts[k] < s ? 1 : 0;   // searchsorted(side='left') on sorted pts
+    for (int step = 8; step >= 1; step >>= 1) {
+        const int k = idx + step - 1;
+        idx += (k < HJ_PTS && pts[k < HJ_PTS ? k : HJ_PTS - 1] < s) ? step : 0;
+    }
     if (idx > 0 && (idx == HJ_PTS || fabs(s - pts[idx - 1]) < fabs(s - pts[idx]))) return idx - 1;
     return idx;
 }
