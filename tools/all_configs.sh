@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 : > "$OUT"
 run() {   # label, bench args...
   local label=$1; shift
-  timeout -k 10 180 python bench.py --steps 200 --warmup 50 --no-cpu-baseline "$@" 2>/dev/null |
+  timeout -k 10 180 python bench.py --steps 200 --warmup 50 --no-cpu-baseline --rollout-k 32 "$@" 2>/dev/null |
     python -c "import json,sys; d=json.loads(sys.stdin.read()); d['label']='$label'; print(json.dumps(d))" >> "$OUT" || exit 1
 }
 run C2 --env-id DroneHoverBulletFreeEnvWithConstWind-v0 --envs-per-gpu 4096
@@ -22,5 +22,5 @@ for l in open(sys.argv[1]):
     d = json.loads(l)
     r = d["roofline"]
     print(f"{d['label']:13s} {d['config']['envs_per_gpu']:7d} envs  {d['value']:.3e} env-steps/s  "
-          f"kernel {r['kernel_ms_per_launch'] * 1e3:6.1f} us  {r['achieved']:6.0f} GB/s")
+          f"kernel {r['kernel_ms_per_launch'] * 1e3:6.1f} us  {r['achieved']:6.0f} GB/s  fused {d['fused_rollout']['us_per_env_step']:6.1f} us/env-step")
 PY
