@@ -1489,28 +1489,25 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
     }
 }
 
-// End of a block's env-step: list the finished envs (wave ballot + one LDS atomic per wave), reset
+// End of a block's env-step: list the finished envs (wave ballots into per-wave lists), reset
 // them block-cooperatively (see step_kernel) and write the block's obs rows out coalesced.  Every
-// thread of the block calls it; s_cnt must be 0 on entry (set before a barrier the caller passed).
+// thread of the block calls it.
 template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C>
 __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& io, uint32_t base, uint32_t tid,
                                                bool do_reset, const ResetSeed& rs, float* s_obs, uint32_t* s_list,
-                                               uint32_t* s_rand, uint32_t* s_cnt) {
+                                               uint32_t* s_rand, uint32_t* s_wcnt) {
     constexpr int OD = NOISE ? 34 : 42;
+    constexpr uint32_t W = B / 64u;
     if (P.auto_reset) {
-        __syncthreads();     // s_cnt initialised
+        // finished envs listed per wave (ballot; no atomics, no counter to initialise): wave w's
+        // resets at s_list[64 w ..], its count in s_wcnt[w]; global reset order is wave-major
         const uint64_t m = __ballot(do_reset);
-        if (m) {
-            const int lane = (int)(threadIdx.x & 63);
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t pos = 0;
-            if (lane == leader) pos = atomicAdd(s_cnt, (uint32_t)__popcll(m));
-            pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (do_reset) s_list[pos] = tid;
-        }
-        // a resetting env's seed is parked in its own LDS obs row (its final obs is already in
-        // final_obs; the row is overwritten by the reset observation after the seed is read)
+        const uint32_t wv = tid >> 6, lane = tid & 63u;
+        if (lane == 0) s_wcnt[wv] = (uint32_t)__popcll(m);
         if (do_reset) {
+            s_list[64u * wv + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = tid;
+            // the seed is parked in the env's own LDS obs row (its final obs is already in
+            // final_obs; the row is overwritten by the reset observation after the seed is read)
             uint32_t* row = reinterpret_cast<uint32_t*>(s_obs + tid * OD);
 #pragma unroll
             for (int k = 0; k < 3; ++k) { row[k] = __float_as_uint(rs.wb[k]); row[3 + k] = __float_as_uint(rs.bias[k]); }
@@ -1522,24 +1519,55 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
         }
         __syncthreads();
         TSTAMP(4);   // block barrier passed
+        uint32_t wc[W], cnt = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < W; ++w) { wc[w] = s_wcnt[w]; cnt += wc[w]; }
 #ifdef CF2_AB_NO_RESET
-        const uint32_t cnt = 0;      // A/B only: measures the auto-reset tail's share
-#else
-        const uint32_t cnt = *s_cnt;
+        cnt = 0;     // A/B only: measures the auto-reset tail's share
 #endif
+        // global reset position -> block-local env index
+        auto env_at = [&](uint32_t p) -> uint32_t {
+            uint32_t w = 0;
+#pragma unroll
+            for (uint32_t k = 0; k + 1 < W; ++k)
+                if (w == k && p >= wc[k]) { p -= wc[k]; w = k + 1; }
+            return s_list[64u * w + p];
+        };
         // Resets run in chunks of C envs.  Their ~26 Philox blocks per env are drawn by every
-        // thread of the block in parallel into LDS; then one lane per env runs the reset math
-        // on the table.  (On one lane each, the draws made the reset tail, which every wave of
-        // the block waits for, about as long as the env-step itself.)
+        // thread of the block in parallel into LDS; then the reset math runs on the table, split
+        // by role over the four waves.  (On one lane each, the draws made the reset tail, which
+        // every wave of the block waits for, about as long as the env-step itself.)
         for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
             const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
+#ifndef CF2_RESET_ONE_WAVE
+            const bool roles = B == 256u;
+#else
+            const bool roles = false;
+#endif
+            // role lanes take their seed now: this chunk's rows are only overwritten after the
+            // barrier below (and other chunks' roles never touch them), so no extra barrier
+            const uint32_t rl = tid & 63u, role = ((tid >> 6) + blockIdx.x) & 3u;
+            const bool act = roles && rl < nc;
+            ResetSeed q;
+            uint32_t t = 0;
+            if (act) {
+                t = env_at(c0 + rl);
+                const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(row[c]); q.bias[c] = __uint_as_float(row[3 + c]); }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(row[6 + c]);
+                q.level = __uint_as_float(row[10]);
+                q.level_idx = (int)row[11];
+                q.ctr = row[12];
+            }
             {
                 const Keys K = make_keys(P.key0, P.key1);
                 for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
-                    const uint32_t sl = w / nc, e = w - sl * nc, pos = c0 + e;
-                    const uint32_t t = s_list[pos];
-                    const uint32_t ctr = reinterpret_cast<const uint32_t*>(s_obs + t * OD)[12];
-                    U4 u = philox(K, reset_block_of_slot((int)sl), ctr, P.gid_off + base + t, TAG_RESET);
+                    const uint32_t sl = w / nc, e = w - sl * nc;
+                    const uint32_t te = env_at(c0 + e);
+                    const uint32_t ctr = reinterpret_cast<const uint32_t*>(s_obs + te * OD)[12];
+                    U4 u = philox(K, reset_block_of_slot((int)sl), ctr, P.gid_off + base + te, TAG_RESET);
                     if (reset_slot_normal_xy((int)sl)) {
                         float z0, z1;
                         box_muller(u.x, u.y, z0, z1);
@@ -1550,55 +1578,36 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
                         box_muller(u.z, u.w, z2, z3);
                         u.z = __float_as_uint(z2); u.w = __float_as_uint(z3);
                     }
-                    uint32_t* q = s_rand + sl * 4 * C + e;
-                    q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
+                    uint32_t* qq = s_rand + sl * 4 * C + e;
+                    qq[0] = u.x; qq[C] = u.y; qq[2 * C] = u.z; qq[3 * C] = u.w;
                 }
             }
             __syncthreads();
-#ifndef CF2_RESET_ONE_WAVE
-            if (B == 256u) {
-                // four waves split each reset by role (reset_role); the role of a wave rotates with
-                // the block index so the co-resident blocks' roles spread over the SIMDs
-                const uint32_t rl = tid & 63u, role = ((tid >> 6) + blockIdx.x) & 3u;
-                const bool act = rl < nc;
-                ResetSeed q;
-                uint32_t t = 0;
-                if (act) {
-                    t = s_list[c0 + rl];
-                    const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(row[c]); q.bias[c] = __uint_as_float(row[3 + c]); }
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(row[6 + c]);
-                    q.level = __uint_as_float(row[10]);
-                    q.level_idx = (int)row[11];
-                    q.ctr = row[12];
-                }
-                __syncthreads();     // every role has its seed before roles 1 and 2 overwrite the rows
+            if (roles) {
+                // the four waves split each reset by role (reset_role); the role of a wave rotates
+                // with the block index so the co-resident blocks' roles spread over the SIMDs
                 if (act) {
                     const TableRng tg{s_rand + rl, C};
                     reset_role<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD, role);
                 }
-                __syncthreads();     // the next chunk reuses s_rand
-                continue;
-            }
-#endif
-            // the resetting wave rotates with the block index, so that the resets of the blocks
-            // sharing a CU do not all queue on one SIMD
-            const uint32_t rl = tid - 64u * (blockIdx.x % (B / 64u));
-            if (rl < nc) {
-                const uint32_t pos = c0 + rl, t = s_list[pos];
-                const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t * OD);
-                ResetSeed q;
+            } else {
+                // one wave runs whole resets; it rotates with the block index, so the resets of
+                // the blocks sharing a CU do not all queue on one SIMD
+                const uint32_t r1 = tid - 64u * (blockIdx.x % W);
+                if (r1 < nc) {
+                    const uint32_t t1 = env_at(c0 + r1);
+                    const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t1 * OD);
+                    ResetSeed q1;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) { q.wb[c] = __uint_as_float(row[c]); q.bias[c] = __uint_as_float(row[3 + c]); }
+                    for (int c = 0; c < 3; ++c) { q1.wb[c] = __uint_as_float(row[c]); q1.bias[c] = __uint_as_float(row[3 + c]); }
 #pragma unroll
-                for (int c = 0; c < 4; ++c) q.ou[c] = __uint_as_float(row[6 + c]);
-                q.level = __uint_as_float(row[10]);
-                q.level_idx = (int)row[11];
-                q.ctr = row[12];
-                const TableRng tg{s_rand + rl, C};
-                reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD);
+                    for (int c = 0; c < 4; ++c) q1.ou[c] = __uint_as_float(row[6 + c]);
+                    q1.level = __uint_as_float(row[10]);
+                    q1.level_idx = (int)row[11];
+                    q1.ctr = row[12];
+                    const TableRng tg{s_rand + r1, C};
+                    reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t1, q1, tg, s_obs + t1 * OD);
+                }
             }
             __syncthreads();     // the next chunk reuses s_rand
         }
@@ -1668,15 +1677,14 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 #endif
     constexpr uint32_t C = CF2_RESET_CHUNK;                // auto-resets per chunk
     __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
-    __shared__ uint32_t s_cnt;
-    if (threadIdx.x == 0) s_cnt = 0;
+    __shared__ uint32_t s_wcnt[B / 64];                    // finished envs per wave
     const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
     bool do_reset = false;
     ResetSeed rs;
     __shared__ double s_hjgrid[6 * HJ_PTS];
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
-    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, &s_cnt);
+    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
     if (uint64_t* r = timing_row())
