@@ -72,6 +72,7 @@ class CF2Config(ctypes.Structure):
         ("hj_grid_min", _d * 6), ("hj_grid_dx", _d * 6), ("hj_grid_points", (_d * HJ_PTS) * 6),
         ("num_drones", _i), ("downwash_on", _i), ("dw_coeff", _d * 3), ("prop_radius", _d),
         ("formation_dx", _d), ("formation_dz", _d),
+        ("use_ground_effect", _i), ("gnd_eff_coeff", _d), ("gnd_eff_h_clip", _d),
     ]
 
     def to_dict(self) -> dict:
@@ -406,6 +407,13 @@ def build_config(env_id_or_spec, num_envs: int, seed: int = 0, env_id_offset: in
     c.prop_radius = robot.PROP_RADIUS
     c.formation_dx = float(kw.pop("formation_dx", 0.5))
     c.formation_dz = float(kw.pop("formation_dz", 1.0))
+    # ground effect (BasePhysics.calculate_ground_effect physics.py:27-58; off in every reference env)
+    c.use_ground_effect = int(bool(kw.pop("use_ground_effect", False)))
+    c.gnd_eff_coeff = robot.GND_EFF_COEFF
+    max_thrust = robot.M * 9.81 * robot.THRUST2WEIGHT_RATIO / 4.0                 # agents.py:151
+    max_rpm = math.sqrt((robot.THRUST2WEIGHT_RATIO * robot.M * 9.81) / (4.0 * max_thrust))   # agents.py:155
+    c.gnd_eff_h_clip = 0.25 * robot.PROP_RADIUS * math.sqrt(
+        (15.0 * max_rpm ** 2 * robot.KF * robot.GND_EFF_COEFF) / max_thrust)     # agents.py:156
     if c.num_drones not in (1, 2, 4, 8):
         raise ValueError("num_drones must be 1, 2, 4 or 8")
     if c.num_envs % c.num_drones or c.env_id_offset % c.num_drones:

@@ -156,9 +156,8 @@ class BasePhysics:
         if self.PHYSICS is not None and drone.physics_type != self.PHYSICS:
             raise ValueError(f"{type(self).__name__} needs a {'cf21x_bullet' if self.PHYSICS == PHYS_BULLET else 'cf21x_sys_eq'}"
                              f" drone, got {drone.drone_model} (the kernel keeps their states in different forms)")
-        if use_ground_effect:
-            # computed but never enabled by the reference (physics.py:27-58, use_ground_effect=False)
-            raise NotImplementedError("ground effect is outside the accelerated path (DESIGN.md section 7)")
+        if use_ground_effect and drone.physics_type != PHYS_BULLET:
+            raise ValueError("ground effect needs Bullet physics (SimplePhysics has none, physics.py:130-200)")
         if abs(float(gravity) - float(drone.env.cfg.gravity_world)) > 1e-12:
             raise NotImplementedError("gravity is fixed by the drone's configuration (9.81)")
         self.drone = drone
@@ -168,6 +167,10 @@ class BasePhysics:
         self.time_step = time_step
         self.number_solver_iterations = number_solver_iterations
         self._lib = _native.load()
+        if drone.physics_type == PHYS_BULLET:
+            # calculate_ground_effect (physics.py:27-58) in the kernel's sub-step when enabled
+            _native.check(self._lib.cf2_set_ground_effect(drone.env._ctx, int(bool(use_ground_effect))),
+                          "cf2_set_ground_effect")
 
     def set_parameters(self, time_step: float | None, number_solver_iterations: int):
         """physics.py:60-68.  ``time_step=None``: every drone integrates with its own per-episode

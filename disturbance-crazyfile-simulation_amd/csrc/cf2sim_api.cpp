@@ -41,6 +41,7 @@ static int validate(const cf2_config* c) {
     if (c->aggregate_phy_steps < 1 || c->aggregate_phy_steps > 4) return CF2_ERR_UNSUPPORTED;
     if (c->obs_rate < 1) return CF2_ERR_INVALID_ARG;
     if (c->buf_size < 1 || c->buf_size > 4) return CF2_ERR_UNSUPPORTED;
+    if (c->use_ground_effect && c->physics != CF2_PHYS_BULLET) return CF2_ERR_UNSUPPORTED;
     if (c->num_levels < 1 || c->num_levels > CF2_NUM_LEVELS_MAX) return CF2_ERR_INVALID_ARG;
     if (c->time_step <= 0.0 || c->mass <= 0.0) return CF2_ERR_INVALID_ARG;
     const int M = c->num_drones > 0 ? c->num_drones : 1;
@@ -150,6 +151,9 @@ static void fill_params(const cf2_config* c, KParams& P) {
     P.prop_radius = (float)c->prop_radius;
     P.formation_dx = (float)c->formation_dx;
     P.formation_dz = (float)c->formation_dz;
+    P.ground_effect = c->use_ground_effect ? 1 : 0;
+    P.gnd_eff_coeff = (float)c->gnd_eff_coeff;
+    P.gnd_eff_h_clip = (float)c->gnd_eff_h_clip;
     P.gust_p = (float)c->gust_onset_prob;
     P.gust_max = (float)c->gust_max_level;
     P.tab = nullptr;
@@ -271,6 +275,7 @@ int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* o
     if (!ctx || !act_dev || !obs_dev || !rew_dev || !done_dev) return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL && !dstb_dev) return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
+    if (ctx->P.ground_effect) return CF2_ERR_UNSUPPORTED;       // physics plug-in only (cf2sim.h)
     if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
     if (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
     StepIO io{ctx->sf, act_dev, dstb_dev, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev,
@@ -286,6 +291,14 @@ int cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, 
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
+int cf2_set_ground_effect(cf2_ctx* ctx, int on) {
+    if (!ctx) return CF2_ERR_INVALID_ARG;
+    if (on && ctx->cfg.physics != CF2_PHYS_BULLET) return CF2_ERR_UNSUPPORTED;   // SimplePhysics has none
+    ctx->P.ground_effect = on ? 1 : 0;
+    ctx->cfg.use_ground_effect = on ? 1 : 0;
+    return CF2_OK;
+}
+
 int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_elems, float* obs_dev, float* rew_dev,
                 uint8_t* done_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, float* final_obs_dev,
                 void* stream) {
@@ -296,6 +309,7 @@ int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_ele
     if (((uintptr_t)obs_dev & 7u) != 0 || (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0))
         return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL) return CF2_ERR_UNSUPPORTED;   // one dstb tensor per step
+    if (ctx->P.ground_effect) return CF2_ERR_UNSUPPORTED;       // physics plug-in only (cf2sim.h)
     if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
     StepIO io{ctx->sf, act_dev, nullptr, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev, final_obs_dev};
     const hipError_t e = launch_rollout(ctx->P, io, (uint32_t)K, (uint32_t)act_stride_elems, (hipStream_t)stream);

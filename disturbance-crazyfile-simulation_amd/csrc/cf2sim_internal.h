@@ -94,6 +94,8 @@ struct KParams {
     double umax_d[3], uni_hi[3];
     int32_t num_drones, downwash_on;                  // multi-drone formations (f4)
     float dw_coeff[3], prop_radius, formation_dx, formation_dz;
+    int32_t ground_effect;                            // BasePhysics.use_ground_effect (physics.py:18-25)
+    float gnd_eff_coeff, gnd_eff_h_clip;
     const struct KTables* tab;   // device-resident lookup tables (dynamically indexed)
     const float* V;              // HJ value tables [num_tables][15^6]
     const uint8_t* hj_bits;      // per-node disturbance sign bits of V [num_tables][15^6] (cf2_bind_hj_tables)

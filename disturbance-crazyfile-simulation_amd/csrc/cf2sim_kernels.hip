@@ -606,6 +606,9 @@ __device__ __forceinline__ void apply_action(const KParams& P, Env& E, const flo
     tz = (-t[0] + t[1] - t[2] + t[3]);
 }
 
+// GE: calculate_ground_effect on (physics_kernel only: the reference's envs never enable it, and the
+// env-step kernels keep their code free of the branch)
+template <bool GE = false>
 __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const float a[4], const float d[3],
                                                const float on[4], bool first_after_reset, float dw = 0.0f) {
     float xprev[4];
@@ -625,12 +628,24 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
     mv(R, dl, drag1);
     mv(R, drag1, dragw);
     const float L = P.prop_xy;
+    const float mp = P.prop_mass, Ip = P.prop_inertia, Lz = P.prop_z;
+    if (GE && fabsf(E.rpy[0]) < 1.5707963267948966f && fabsf(E.rpy[1]) < 1.5707963267948966f) {
+        // BasePhysics.calculate_ground_effect (physics.py:27-58): extra thrust at each prop from its
+        // height z_i = (p + R o_i)_z (getLinkStates), clipped at GND_EFF_H_CLIP; added to the prop
+        // forces (apply_motor_forces, physics.py:243-246), not to the yaw torque.  rpy: the last readback.
+        const float ox[4] = {L, -L, -L, L}, oy[4] = {-L, -L, L, L};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float z = fmaxf(E.p[2] + (R.m[6] * ox[j] + R.m[7] * oy[j] + R.m[8] * Lz), P.gnd_eff_h_clip);
+            const float rr = P.prop_radius * rcp(4.0f * z);
+            f[j] = opaque(f[j] + f[j] * P.gnd_eff_coeff * (rr * rr));
+        }
+    }
     float tb[3];
     tb[0] = L * (-f[0] - f[1] + f[2] + f[3]) + d[0];
     tb[1] = L * (-f[0] + f[1] + f[2] - f[3]) + d[1];
     tb[2] = tz;
     const float fsum = f[0] + f[1] + f[2] + f[3];
-    const float mp = P.prop_mass, Ip = P.prop_inertia, Lz = P.prop_z;
     const float mtot = E.m + 4.0f * mp;
     float Fw[3];
     const float fz = fsum - dw;      // downwash of formation mates: -z of the body, at the COM
@@ -1716,7 +1731,12 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
     float on[4];
     normals<4>(g, 0, on);
     if (PHYS == PHYS_BULLET_T) {
-        bullet_substep(P, E, a, d, on, E.ep_step == 0 && !E.props_on);
+        if (P.ground_effect) {
+            euler_from_quat(E.q, E.rpy);     // drone.rpy of the last readback
+            bullet_substep<true>(P, E, a, d, on, E.ep_step == 0 && !E.props_on);
+        } else {
+            bullet_substep<false>(P, E, a, d, on, E.ep_step == 0 && !E.props_on);
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) E.wb[k] = E.w[k];

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 3
+#define CF2SIM_ABI_VERSION 4
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -162,6 +162,15 @@ typedef struct cf2_config {
     double dw_coeff[3];            /* 2267.18, 0.16, -0.11 */
     double prop_radius;            /* 2.31348e-2 m */
     double formation_dx, formation_dz;   /* 0.5 m, 1.0 m */
+
+    /* ---- ground effect (BasePhysics.calculate_ground_effect envs/physics.py:27-58, applied in
+     * step_forward physics.py:116-120 / 243-246; the reference's envs never enable it;
+     * cf2_physics_step only, see cf2_set_ground_effect): while
+     * |roll|, |pitch| < pi/2 each prop gets the extra thrust f_i * gnd_eff_coeff *
+     * (prop_radius / (4 max(z_i, gnd_eff_h_clip)))^2, z_i = world height of prop i.  Bullet only. */
+    int32_t use_ground_effect;
+    double gnd_eff_coeff;          /* URDF gnd_eff_coeff 11.36859 */
+    double gnd_eff_h_clip;         /* GND_EFF_H_CLIP agents.py:156 */
 } cf2_config;
 
 /* SoA layout descriptor returned by cf2_layout(): state_f[field*num_envs + env],
@@ -221,6 +230,13 @@ int  cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev,
  * overrides every env's dt for this call (BasePhysics.set_parameters physics.py:60-68); <= 0
  * uses the per-env dt (domain randomisation).  act_dev [N,4] 16-B aligned. */
 int  cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float time_step, void* stream);
+/* Ground effect on / off for this context's Bullet physics (the physics object's
+ * use_ground_effect, envs/physics.py:18-25); the initial value is cfg.use_ground_effect.
+ * It applies to cf2_physics_step only: the reference's envs build their physics with the default
+ * use_ground_effect=False (envs/base.py:223-232), so the env-step kernels carry no ground-effect
+ * code and cf2_step / cf2_rollout return CF2_ERR_UNSUPPORTED while it is on.
+ * Returns CF2_ERR_UNSUPPORTED for SimplePhysics contexts. */
+int  cf2_set_ground_effect(cf2_ctx* ctx, int on);
 
 /* K consecutive env-steps fused in one launch (rollout mode; SURVEY section 7 "fused K-step"):
  * the env state stays in registers across the K steps.  Step k reads actions act_dev + k *

@@ -371,6 +371,18 @@ static void bullet_substep(const orc_ctx* X, orc_env* E, const REAL a[4], const 
      * cf21x_bullet.urdf prop1..4_joint), yaw torque and adversary torques on link 4 in its frame
      * (agents.py:330-337, 517-533).  Only dstb[0], dstb[1] are applied (physics.py:228-229). */
     REAL L = R(c->prop_xy);
+    /* ground effect (BasePhysics.calculate_ground_effect physics.py:27-58, applied with the prop
+     * forces physics.py:243-246 while |roll|, |pitch| < pi/2 of the last readback): prop heights
+     * z_i = (p + R o_i)_z (getLinkStates), clipped at GND_EFF_H_CLIP (agents.py:156) */
+    if (c->use_ground_effect && fabs((double)E->rpy[0]) < 1.5707963267948966 && fabs((double)E->rpy[1]) < 1.5707963267948966) {
+        const REAL ox[4] = {L, -L, -L, L}, oy[4] = {-L, -L, L, L}, oz = R(c->prop_z);
+        for (int j = 0; j < 4; ++j) {
+            REAL z = E->p[2] + (Rm[6] * ox[j] + Rm[7] * oy[j] + Rm[8] * oz);
+            if (z < R(c->gnd_eff_h_clip)) z = R(c->gnd_eff_h_clip);
+            const REAL rr = R(c->prop_radius) / (R(4.0) * z);
+            f[j] = f[j] + f[j] * R(c->gnd_eff_coeff) * (rr * rr);
+        }
+    }
     REAL tb[3];
     tb[0] = L * (-f[0] - f[1] + f[2] + f[3]) + dstb[0];
     tb[1] = L * (-f[0] + f[1] + f[2] - f[3]) + dstb[1];
@@ -817,6 +829,7 @@ void* orc_create(const cf2_config* cfg) {
 }
 /* OpenMP threads used by orc_step (default 1; the bench's all-core CPU baseline raises it). */
 void orc_set_threads(void* h, int threads) { ((orc_ctx*)h)->threads = threads; }
+void orc_set_ground_effect(void* h, int on) { ((orc_ctx*)h)->cfg.use_ground_effect = on ? 1 : 0; }
 
 void orc_destroy(void* h) {
     orc_ctx* X = (orc_ctx*)h;
@@ -979,8 +992,12 @@ void orc_physics_step(void* h, const float* act, const double* dstb, double dt_o
         const REAL dt_saved = E->dt;
         if (dt_override > 0.0) E->dt = R(dt_override);
         rng_normals(&g, 0, 4, ou_n);
-        if (c->physics == CF2_PHYS_BULLET) bullet_substep(X, E, a, d, ou_n, E->ep_step == 0 && !E->props_on, R(0.0));
-        else simple_substep(X, E, a, ou_n);
+        if (c->physics == CF2_PHYS_BULLET) {
+            if (c->use_ground_effect) orc_euler_from_quat(E->q, E->rpy);     /* drone.rpy of the last readback */
+            bullet_substep(X, E, a, d, ou_n, E->ep_step == 0 && !E->props_on, R(0.0));
+        } else {
+            simple_substep(X, E, a, ou_n);
+        }
         E->dt = dt_saved;
         E->props_on = 1;
         E->rng_ctr += 1;

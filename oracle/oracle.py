@@ -44,6 +44,7 @@ class _Lib:
             lib.orc_create.argtypes = [_P]
             lib.orc_destroy.argtypes = [_P]
             lib.orc_set_threads.argtypes = [_P, ctypes.c_int]
+            lib.orc_set_ground_effect.argtypes = [_P, ctypes.c_int]
             lib.orc_reset.argtypes = [_P, _u8p, _dp]
             lib.orc_step.argtypes = [_P, _fp, _dp, _dp, _dp, _u8p, _u8p, _dp, _dp, _dp]
             lib.orc_physics_step.argtypes = [_P, _fp, _dp, ctypes.c_double]
@@ -142,6 +143,10 @@ class OracleEnv:
         if want_final:
             info["final_obs"] = fin
         return obs, rew, done.astype(bool), info
+
+    def set_ground_effect(self, on: bool):
+        """BasePhysics.use_ground_effect of this context (orc_set_ground_effect)."""
+        self.lib.orc_set_ground_effect(self.h, int(bool(on)))
 
     def physics_step(self, act, dstb=None, time_step=0.0):
         """One physics sub-step of every env (orc_physics_step; the plugin's step_forward)."""

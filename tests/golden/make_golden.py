@@ -22,6 +22,8 @@ Fixtures written:
   golden_components.npz        apply_action (OU draws recorded), SensorNoise.add_noise (draws
                                recorded), quaternion conversions, Boltzmann probabilities
   golden_hj.npz                distur_gener() on a synthetic (exactly reproducible) value table
+  golden_ground_effect.npz     PyBulletPhysics(use_ground_effect=True).step_forward sub-steps of the
+                               reference's drone placed near the ground (one case tilted past pi/2)
 """
 from __future__ import annotations
 
@@ -404,6 +406,41 @@ def components():
     return rec
 
 
+def ground_effect_trajectories():
+    """PyBulletPhysics(use_ground_effect=True).step_forward (physics.py:27-58, 91-124) driven on the
+    reference's own drone near the ground: the env is built and reset as usual, then the base is
+    placed low (tilted, moving) and the reference's physics object, constructed with ground
+    effect on, is stepped directly; the state is recorded after every sub-step."""
+    from phoenix_drone_simulation.envs import hover_free, physics
+    rec = {}
+    for k in range(4):
+        np.random.seed(2000 + k)
+        env = hover_free.DroneHoverBulletFreeEnvWithoutAdversary(observation_noise=0, domain_randomization=-1,
+                                                                motor_thrust_noise=0)
+        env.reset()
+        bc, dr = env.bc, env.drone
+        rng = np.random.default_rng(50 + k)
+        p = np.array([rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5), [0.005, 0.03, 0.08, 0.2][k]])
+        rpy = rng.uniform(-0.3, 0.3, 3) if k < 3 else np.array([0.2, 2.0, 0.1])   # k=3: |pitch| > pi/2
+        bc.resetBasePositionAndOrientation(dr.body_unique_id, p, quat_from_euler(rpy))
+        bc.resetBaseVelocity(dr.body_unique_id, rng.normal(0, 0.2, 3), rng.normal(0, 1.0, 3))
+        dr.update_information()
+        phys = physics.PyBulletPhysics(dr, bc, time_step=env.time_step, use_ground_effect=True)
+        key = f"ge__{k}"
+        rec[key + "__init_p"] = bc.p.copy(); rec[key + "__init_q"] = bc.q.copy()
+        rec[key + "__init_v"] = bc.v.copy(); rec[key + "__init_w"] = bc.w.copy()
+        rec[key + "__init_x"] = np.array(dr.x, float); rec[key + "__init_abuf"] = np.array(dr.action_buffer, float)
+        acts = (rng.uniform(-1, 1, (120, 4)) * 0.15 + dr.HOVER_ACTION).astype(np.float32)
+        S = []
+        for a in acts:
+            phys.step_forward(np.array(a, np.float64))
+            S.append(np.concatenate([bc.p, bc.q, bc.v, bc.w, np.array(dr.x, float)]))
+        rec[key + "__actions"] = acts
+        rec[key + "__states"] = np.array(S)
+        rec[key + "__time_step"] = np.array(env.time_step)
+    return rec
+
+
 def synthetic_value_table():
     """Exactly reproducible fp32 15^6 table: integer bowl + dyadic hash noise (ties included)."""
     i = np.indices((15,) * 6, dtype=np.int64)
@@ -445,14 +482,19 @@ def hj_vectors():
     return rec
 
 
-def main():
+FIXTURES = {"golden_components.npz": lambda: components(),
+            "golden_hj.npz": lambda: hj_vectors(),
+            "golden_env_trajectories.npz": lambda: env_trajectories(),
+            "golden_ground_effect.npz": lambda: ground_effect_trajectories()}
+
+
+def main(names=None):
+    """Write every fixture, or only the ones named on the command line."""
     install_stubs()
-    np.savez_compressed(os.path.join(HERE, "golden_components.npz"), **components())
-    np.savez_compressed(os.path.join(HERE, "golden_hj.npz"), **hj_vectors())
-    np.savez_compressed(os.path.join(HERE, "golden_env_trajectories.npz"), **env_trajectories())
-    for f in ("golden_components.npz", "golden_hj.npz", "golden_env_trajectories.npz"):
+    for f in names or FIXTURES:
+        np.savez_compressed(os.path.join(HERE, f), **FIXTURES[f]())
         print(f, os.path.getsize(os.path.join(HERE, f)))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -16,6 +16,8 @@ What each fixture pins (reference file:line):
          reward/done/info are the reference's code; SimplePhysics is the reference's code; the
          Bullet integrator inside the fake physics server is a numpy restatement (PyBullet is
          not installable here: parity of that one piece vs PyBullet is unpinned).
+* ge     PyBulletPhysics(use_ground_effect=True).step_forward near the ground: calculate_ground_effect
+         (physics.py:27-58) with the prop heights from getLinkStates, every sub-step recorded
 """
 import os
 
@@ -145,3 +147,54 @@ def test_env_steps_match_reference(key):
         assert bool(d[0]) == bool(done[t]), t
         assert info["cost"][0] == cost[t], t
     env.close()
+
+
+def ge_keys():
+    g = load("golden_ground_effect.npz")
+    return sorted({k.split("__")[0] + "__" + k.split("__")[1] for k in g.files})
+
+
+def oracle_ge_from_golden(g, key, precision="f64", ground_effect=True):
+    """Oracle env holding the reference drone's low-altitude start state, ground effect on."""
+    c = build_config("DroneHoverBulletFreeEnvWithoutAdversary-v0", 1, observation_noise=0, domain_randomization=-1,
+                     motor_thrust_noise=0, max_episode_steps=0, auto_reset=False)
+    env = O.OracleEnv(c, precision)
+    sf, si = env.get_state()
+    sf[:] = 0
+    sf[0:3, 0] = g[key + "__init_p"]; sf[3:7, 0] = g[key + "__init_q"]; sf[7:10, 0] = g[key + "__init_v"]
+    sf[10:13, 0] = g[key + "__init_w"]; sf[16:20, 0] = g[key + "__init_x"]
+    abuf = g[key + "__init_abuf"]
+    for r in range(abuf.shape[0]):
+        sf[24 + 4 * r:28 + 4 * r, 0] = abuf[r]
+    sf[81, 0] = c.time_step; sf[82, 0] = c.mass; sf[83:86, 0] = (c.ixx, c.iyy, c.izz)
+    sf[86, 0] = c.ft0; sf[87, 0] = c.ft1
+    sf[88:92, 0] = c.A; sf[92:96, 0] = c.B; sf[96:100, 0] = c.K
+    si[:] = 0
+    env.set_state(sf, si)
+    env.set_ground_effect(ground_effect)
+    assert float(g[key + "__time_step"]) == c.time_step
+    return env
+
+
+@pytest.mark.parametrize("key", ge_keys())
+def test_ground_effect_substeps_match_reference(key):
+    """calculate_ground_effect + PyBulletPhysics.step_forward (physics.py:27-58, 91-124) with
+    use_ground_effect=True, near the ground: every sub-step's p, q, v, w and motor state within
+    1e-9 of the reference; ge__3 is flipped past |roll| = pi/2 (no ground effect, physics.py:55-58)."""
+    g = load("golden_ground_effect.npz")
+    acts, S = g[key + "__actions"], g[key + "__states"]
+    env = oracle_ge_from_golden(g, key)
+    off = oracle_ge_from_golden(g, key, ground_effect=False)
+    for t in range(len(acts)):
+        env.physics_step(acts[t:t + 1])
+        off.physics_step(acts[t:t + 1])
+        sf = env.get_state()[0][:, 0]
+        got = np.concatenate([sf[0:13], sf[16:20] + sf[104:108]])
+        err = np.abs(got - S[t]) / (1 + np.abs(S[t]))
+        assert err.max() < 1e-9, (t, err.max(), np.argmax(err))
+    dz = abs(env.get_state()[0][2, 0] - off.get_state()[0][2, 0])
+    if key.endswith("3"):
+        assert dz == 0.0                                  # flipped past pi/2: no ground effect
+    else:
+        assert dz > 1e-4                                  # the extra thrust near the ground shows
+    env.close(); off.close()

@@ -10,6 +10,8 @@
 2. Known answers of the rigid-body step (hover equilibrium, free fall with Bullet damping,
    torque-free rotation invariants, torque / disturbance signs, drag sign), run on the kernel
    through the physics plug-in (cf2_physics_step) from states set with cf2_set_state.
+3. Ground effect (tests/golden/golden_ground_effect.npz): the reference's PyBulletPhysics with
+   use_ground_effect=True, replayed sub-step by sub-step through the plug-in.
 """
 import numpy as np
 import pytest
@@ -219,3 +221,44 @@ def test_kernel_drag_opposes_velocity(gpu):
         vx.append(float(_state(drone)[7, 0]))
         drone.close()
     assert vx[0] < vx[1]
+
+
+def test_kernel_ground_effect_replays_reference(gpu):
+    """PyBulletPhysics(use_ground_effect=True) on the kernel (cf2_set_ground_effect +
+    cf2_physics_step) replays the reference's ground-effect sub-steps
+    (tests/golden/golden_ground_effect.npz, physics.py:27-58, 91-124): p, q, v, w and the motor
+    state within 2e-5 of the fp64 reference over 120 sub-steps near the ground, one env per case
+    (ge__3 flipped past |roll| = pi/2, where the reference applies none)."""
+    from cf2sim.physics import PyBulletPhysics
+    from test_golden import ge_keys
+    g = load("golden_ground_effect.npz")
+    keys = ge_keys()
+    n = len(keys)
+    c = _cfg(n=n)
+    drone = _drone(c)
+    sf, si = drone.env.get_state()
+    sf, si = sf.cpu().numpy().astype(np.float64), si.cpu().numpy()
+    for j, key in enumerate(keys):
+        sf[:, j] = 0.0
+        sf[0:3, j] = g[key + "__init_p"]; sf[3:7, j] = g[key + "__init_q"]; sf[7:10, j] = g[key + "__init_v"]
+        sf[10:13, j] = g[key + "__init_w"]; sf[16:20, j] = g[key + "__init_x"]
+        abuf = g[key + "__init_abuf"]
+        for r in range(abuf.shape[0]):
+            sf[24 + 4 * r:28 + 4 * r, j] = abuf[r]
+        sf[81, j] = c.time_step; sf[82, j] = c.mass; sf[83:86, j] = (c.ixx, c.iyy, c.izz)
+        sf[86, j] = c.ft0; sf[87, j] = c.ft1
+        sf[88:92, j] = c.A; sf[92:96, j] = c.B; sf[96:100, j] = c.K
+        si[:, j] = 0
+    drone.env.set_state(torch.from_numpy(sf.astype(np.float32)), torch.from_numpy(si))
+    phys = PyBulletPhysics(drone, None, time_step=None, use_ground_effect=True)
+    acts = np.stack([g[k + "__actions"] for k in keys], 1)          # (T, n, 4)
+    worst = 0.0
+    for t in range(acts.shape[0]):
+        phys.step_forward(torch.from_numpy(np.ascontiguousarray(acts[t])).cuda())
+        s = _state(drone)
+        for j, k in enumerate(keys):
+            got = np.concatenate([s[0:13, j], s[16:20, j] + s[104:108, j]])
+            ref = g[k + "__states"][t]
+            worst = max(worst, float((np.abs(got - ref) / (1 + np.abs(ref))).max()))
+    drone.close()
+    assert worst < 2e-5, worst

@@ -49,6 +49,7 @@ def _err(g, r):
     ("PyBulletPhysics", "DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(domain_randomization=-1), 0.005),
     ("SimplePhysics", "DroneHoverSimpleEnv-v0", {}, None),
     ("HipBatchedPhysics", "DroneHoverBulletFreeEnvWithoutAdversary-v0", dict(latency=0.0), 0.004),
+    ("PybulletPhysicsWithAdversary+ground_effect", "DroneHoverBulletFreeEnvWithoutAdversary-v0", {}, None),
 ])
 def test_plugin_step_forward_matches_restatement(gpu, name, env_id, kw, time_step):
     """getattr(cf2sim.physics, name)(drone, bc, time_step=...) stepped 60 sub-steps with random
@@ -58,13 +59,27 @@ def test_plugin_step_forward_matches_restatement(gpu, name, env_id, kw, time_ste
     import torch
     import cf2sim.physics as phoenix_physics
     n, seed = 256, 5
+    name, _, ge = name.partition("+")
     drone, ref = _pair(env_id, n, seed, kw)
-    phys = getattr(phoenix_physics, name)(drone, None, time_step=time_step)
+    phys = getattr(phoenix_physics, name)(drone, None, time_step=time_step, use_ground_effect=bool(ge))
     phys.set_parameters(time_step=time_step, number_solver_iterations=5)
     drone.reset()
     ref.reset()
+    if ge:
+        # the batch starts 3-30 cm above the ground.  Lower is ill-conditioned in any precision:
+        # GND_EFF_H_CLIP is 3.7 um (agents.py:156), so (r/4z)^2 grows without practical bound as a
+        # prop nears z = 0 (x2.8e7 thrust at the clip), where PyBullet's ground plane would be hit
+        ref.set_ground_effect(True)
+        gsf, gsi = drone.env.get_state()
+        z = np.random.default_rng(2).uniform(0.03, 0.3, n)
+        gsf[2] = torch.from_numpy(z.astype(np.float32))
+        drone.env.set_state(gsf, gsi)
+        rsf, rsi = ref.get_state()
+        rsf[2] = z.astype(np.float32)
+        ref.set_state(rsf, rsi)
     rng = np.random.default_rng(1)
     takes_dstb = name in ("PybulletPhysicsWithAdversary", "HipBatchedPhysics")
+    zmin = np.full(n, np.inf)
     for _ in range(60):
         a = (rng.uniform(-1, 1, (n, 4)) * 0.3 + 0.1111).astype(np.float32)
         d = (rng.uniform(-1, 1, (n, 3)) * 2e-4).astype(np.float32) if takes_dstb else None
@@ -74,19 +89,25 @@ def test_plugin_step_forward_matches_restatement(gpu, name, env_id, kw, time_ste
         else:
             phys.step_forward(at)
         ref.physics_step(a, d, time_step or 0.0)
+        if ge:
+            zmin = np.minimum(zmin, ref.get_state()[0][2])
     gsf, gsi = drone.env.get_state()
     rsf, rsi = ref.get_state()
     gsf, gsi = gsf.cpu().numpy(), gsi.cpu().numpy()
     L = drone.env.layout
     fields = list(range(0, 13)) + list(range(L.f_motor, L.f_motor + 8))
-    assert _err(gsf[fields], rsf[fields]) < 2e-5
+    # with ground effect only the drones that stayed >= 5 cm up are compared: below that fp32
+    # and fp64 restatements themselves part by >2e-4 within 60 sub-steps (the 1/z^2 thrust)
+    keep = zmin >= 0.05
+    assert keep.sum() >= n // 3
+    assert _err(gsf[fields][:, keep], rsf[fields][:, keep]) < 2e-5
     np.testing.assert_array_equal(gsi[:3], rsi[:3])        # episode step, RNG counter, flags
     # the agent attributes read back from the snapshot
-    np.testing.assert_allclose(drone.xyz.cpu().numpy(), rsf[0:3].T, rtol=0, atol=2e-5)
-    np.testing.assert_allclose(drone.quaternion.cpu().numpy(), rsf[3:7].T, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(drone.xyz.cpu().numpy()[keep], rsf[0:3].T[keep], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(drone.quaternion.cpu().numpy()[keep], rsf[3:7].T[keep], rtol=0, atol=2e-5)
     if name != "SimplePhysics":
-        rpy = drone.rpy.cpu().numpy()
-        q = rsf[3:7].T
+        rpy = drone.rpy.cpu().numpy()[keep]
+        q = rsf[3:7].T[keep]
         x, y, z, w = q.T
         roll = np.arctan2(2 * (y * z + w * x), w * w - x * x - y * y + z * z)
         np.testing.assert_allclose(rpy[:, 0], roll, atol=1e-4)
@@ -106,6 +127,12 @@ def test_plugin_rejects_mismatched_drone_and_bad_inputs(gpu):
         phys.step_forward(torch.zeros(8, 3, device="cuda"), torch.zeros(8, 3, device="cuda"))
     with pytest.raises(ValueError):
         phys.step_forward(torch.zeros(8, 4, device="cuda"), torch.zeros(8, device="cuda"))
-    with pytest.raises(NotImplementedError):
-        phoenix_physics.PyBulletPhysics(drone, None, time_step=0.005, use_ground_effect=True)
+    simple = phoenix_physics.BatchedDrone("cf21x_sys_eq", num_drones=8)
+    with pytest.raises(ValueError):            # SimplePhysics has no ground effect (physics.py:127-200)
+        phoenix_physics.SimplePhysics(simple, None, time_step=0.005, use_ground_effect=True)
+    phoenix_physics.PyBulletPhysics(drone, None, time_step=0.005, use_ground_effect=True)
+    from cf2sim._native import CF2Error
+    with pytest.raises(CF2Error, match="unsupported|UNSUPPORTED|outside"):   # env-steps carry no ground effect
+        drone.env.step(torch.zeros(8, 4, device="cuda"))
+    simple.close()
     drone.close()
