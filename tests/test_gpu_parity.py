@@ -272,3 +272,43 @@ def test_downwash_formations_match_restatement(gpu, kw):
     assert errs[0] < 2e-5, f"reset observation {errs[0]}"
     assert errs.max() < 5e-4, f"obs max err {errs.max()} {errs}"
     assert dmis == 0
+
+
+@pytest.mark.parametrize("n", [1, 63, 300, 1000])
+def test_ragged_env_counts_match_restatement(gpu, n):
+    """Env counts that fill no whole wave / block (the kernel's tail guards, the per-block reset
+    lists and the coalesced obs copy of a partial block) vs the fp32 restatement: 150 env-steps of
+    the noisy, domain-randomised gust env with wide actions, so auto-resets hit partial blocks."""
+    env_id = "DroneHoverBulletFreeEnvWithGust-v0"
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env = BatchedCrazyflieEnv(env_id, n, seed=21, want_final_obs=True)
+    ref = O.OracleEnv(build_config(env_id, n, seed=21), precision="f32")
+    go, ro = env.reset().cpu().numpy(), ref.reset()
+    assert float((np.abs(go - ro) / (1 + np.abs(ro))).max()) < 2e-5
+    rng = np.random.default_rng(5)
+    resets = 0
+    for t in range(150):
+        a = (rng.uniform(-1, 1, size=(n, 4)) * 0.6 + 0.1111).astype(np.float32)
+        g_o, g_r, g_d, g_i = env.step(torch.from_numpy(a).cuda())
+        r_o, r_r, r_d, r_i = ref.step(a, want_final=True)
+        g_d = g_d.cpu().numpy().astype(bool)
+        np.testing.assert_array_equal(g_d, r_d)
+        resets += int(r_d.sum())
+        err = float((np.abs(g_o.cpu().numpy() - r_o) / (1 + np.abs(r_o))).max())
+        assert err < 5e-4, (t, err)
+        assert float(np.abs(g_r.cpu().numpy() - r_r).max()) < 3e-3
+        if r_d.any():
+            fin = g_i["final_obs"].cpu().numpy()[r_d]
+            assert float((np.abs(fin - r_i["final_obs"][r_d]) / (1 + np.abs(r_i["final_obs"][r_d]))).max()) < 5e-4
+    gsi, rsi = env.get_state()[1].cpu().numpy(), ref.get_state()[1]
+    np.testing.assert_array_equal(gsi[:2], rsi[:2])        # episode steps, RNG counters
+    env.close(); ref.close()
+    assert n < 63 or resets > 0
+
+
+def test_zero_envs_is_rejected(gpu):
+    """An empty batch is an invalid configuration (cf2_create returns CF2_ERR_INVALID_ARG)."""
+    from cf2sim._native import CF2Error
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    with pytest.raises((CF2Error, ValueError)):
+        BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithoutAdversary-v0", 0)
