@@ -53,7 +53,8 @@ enum : int {
     S_OU = 20,                                            // G5
     S_ABUF = 24,                                          // G6-G9, row r in G6+r
     S_BIAS = 40, S_GUST = 43,                             // G10: gyro bias + gust_left (int)
-    S_LPF = 44,                                           // G11
+    S_LPF = 77,                                           // G19.yzw, sensor noise only (G19.x = obs_prev[12]);
+                                                          //   G11 is unused
     S_RPY = 48,                                           // G12 (Simple physics)
     S_DSTB = 52,                                          // G13
     S_HACT = 56,                                          // G14-G15

@@ -376,7 +376,9 @@ struct Tile {
     }
 };
 
-enum : int { G_CORE3 = 3, G_MOTOR = 4, G_OU = 5, G_ABUF = 6, G_BIAS = 10, G_LPF = 11, G_RPY = 12, G_DSTB = 13,
+// G_LPF: with sensor noise the gyro LPF state shares the last o_{k-1} group (13 of its 16 slots
+// are o_{k-1}): that group is read with the state, the other three with the history
+enum : int { G_CORE3 = 3, G_MOTOR = 4, G_OU = 5, G_ABUF = 6, G_BIAS = 10, G_LPF = 19, G_RPY = 12, G_DSTB = 13,
              G_HACT = 14, G_OBSP = 16, G_HELD = 21, G_PARAM = 24, G_LEVEL = 27, G_MOTOR_LO = 28,
              G_LEVEL_IDX = 29 };
 
@@ -392,7 +394,7 @@ __device__ __forceinline__ void load_hist(const Tile& T, Env& E) {
     E.hact[0][0] = h0.x; E.hact[0][1] = h0.y; E.hact[0][2] = h0.z; E.hact[0][3] = h0.w;
     E.hact[1][0] = h1.x; E.hact[1][1] = h1.y; E.hact[1][2] = h1.z; E.hact[1][3] = h1.w;
 #pragma unroll
-    for (int g = 0; g < (OL + 3) / 4; ++g) {
+    for (int g = 0; g < (NOISE ? 3 : (OL + 3) / 4); ++g) {     // noise: o_{k-1}[12] came with the LPF
         const F4 o = T.ld(G_OBSP + g);
         const float v[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -436,7 +438,7 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
     }
     if (NOISE) {
         const F4 l = T.ld(G_LPF);
-        E.lpf[0] = l.x; E.lpf[1] = l.y; E.lpf[2] = l.z;
+        E.obs_prev[12] = l.x; E.lpf[0] = l.y; E.lpf[1] = l.z; E.lpf[2] = l.w;
 #pragma unroll
         for (int k = 0; k < 10; ++k) E.held[k] = 0.0f;
         if (P.held_persistent) {
@@ -473,7 +475,9 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
         if (need_level) lv = T.ld(G_LEVEL);
     }
     E.level = need_level ? lv.w : P.level_fixed;
-    E.level_idx = need_level ? bi(T.ld(G_LEVEL_IDX).x) : 0;
+    // the level index only matters where levels are redrawn (Boltzmann: the HJ table and the
+    // reset keep it); a fixed-level env's index is 0 and its group is not read
+    E.level_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
 }
 
 // state the physics sub-steps update (stored as soon as the last sub-step is done; group 3,
@@ -492,32 +496,36 @@ __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__
         if (r < P.buf_size) T.st(G_ABUF + r, f4(E.abuf[r][0], E.abuf[r][1], E.abuf[r][2], E.abuf[r][3]));
     if (NOISE || gust_mode(P))
         T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(E.gust_left)));
-    if (NOISE) {
-        T.st(G_LPF, f4(E.lpf[0], E.lpf[1], E.lpf[2], 0.0f));
-        if (P.held_persistent) {
-            T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
-            T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
-            T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
-        }
+    if (NOISE && P.held_persistent) {      // (the LPF state is stored with the history, store_tail)
+        T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
+        T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
+        T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
     }
     if (PHYS == PHYS_SIMPLE_T) T.st(G_RPY, f4(E.rpy[0], E.rpy[1], E.rpy[2], 0.0f));
     if (gust_mode(P)) T.st(G_DSTB, f4(E.dstb[0], E.dstb[1], E.dstb[2], 0.0f));
 }
 
-// end of the step: history, counters (group 3 with the last angular-rate component)
+// the o_{k-1} groups; with sensor noise the last one carries the gyro LPF state
 template <bool NOISE>
-__device__ __forceinline__ void store_tail(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
+__device__ __forceinline__ void store_obs_prev(const Tile& T, const Env& E) {
     constexpr int OL = NOISE ? 13 : 17;
-    const Tile T(sf, P.N, i);
-    T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
-    T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
 #pragma unroll
     for (int g = 0; g < (OL + 3) / 4; ++g) {
         float v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = 4 * g + k < OL ? E.obs_prev[4 * g + k] : 0.0f;
+        if (NOISE && G_OBSP + g == G_LPF) { v[1] = E.lpf[0]; v[2] = E.lpf[1]; v[3] = E.lpf[2]; }
         T.st(G_OBSP + g, f4(v[0], v[1], v[2], v[3]));
     }
+}
+
+// end of the step: history, counters (group 3 with the last angular-rate component)
+template <bool NOISE>
+__device__ __forceinline__ void store_tail(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
+    const Tile T(sf, P.N, i);
+    T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
+    T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
+    store_obs_prev<NOISE>(T, E);
     const int fl = (E.aidx & 15) | (E.halias0 << 4) | (E.halias1 << 5) | (E.la_view << 6) | (E.props_on << 7);
     T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
 }
@@ -1428,7 +1436,7 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
 // observation, as reset_env + store_env produce them):
 //   0: kinematics, motor state, ring           -> groups 0-6(+ring), 12 (Simple), 28
 //   1: kinematics + the first sensor call      -> obs row o_0 | A_0
-//   2: kinematics + the second sensor call     -> obs row o_1 | A_1; groups 10, 11, 14-19, 21-23
+//   2: kinematics + the second sensor call     -> obs row o_1 | A_1; groups 10, 14-19 (LPF in 19), 21-23
 //   3: domain randomisation, disturbance, level -> groups 13, 24-27, 29
 // Roles 1 and 2 recompute the reset pose from the same table entries, so the critical path is one
 // pose + one sensor call instead of the whole reset.
@@ -1485,23 +1493,14 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
     for (int k = OL + 4; k < 2 * (OL + 4); ++k) obs_row[k] = o[k];
     if (NOISE || gust_mode(P))
         T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(0)));
-    if (NOISE) {
-        T.st(G_LPF, f4(E.lpf[0], E.lpf[1], E.lpf[2], 0.0f));
-        if (P.held_persistent) {
-            T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
-            T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
-            T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
-        }
+    if (NOISE && P.held_persistent) {
+        T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
+        T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
+        T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
     }
     T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
     T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
-#pragma unroll
-    for (int g4 = 0; g4 < (OL + 3) / 4; ++g4) {
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = 4 * g4 + k < OL ? E.obs_prev[4 * g4 + k] : 0.0f;
-        T.st(G_OBSP + g4, f4(v[0], v[1], v[2], v[3]));
-    }
+    store_obs_prev<NOISE>(T, E);
 }
 
 // End of a block's env-step: list the finished envs (wave ballots into per-wave lists), reset
@@ -1895,11 +1894,12 @@ __global__ void init_kernel(KParams P, float* __restrict__ sf) {
 }
 
 // public snapshot field -> internal slot (cf2sim_internal.h)
-__device__ __forceinline__ int pub_float_slot(int f) {
+// -1: motor A[j] (derived), -2: not stored in this configuration (the gyro LPF without noise)
+__device__ __forceinline__ int pub_float_slot(int f, bool noise) {
     if (f < F_RPY) return f;                              // pos, quat, vel, omega: same slots
     if (f < F_MOTOR) return S_RPY + (f - F_RPY);
     if (f < F_LPF) return f;                              // motor, ou, abuf, bias: same slots
-    if (f < F_HELD) return S_LPF + (f - F_LPF);
+    if (f < F_HELD) return noise ? S_LPF + (f - F_LPF) : -2;
     if (f < F_OBS_PREV) return S_HELD + (f - F_HELD);
     if (f < F_HIST_ACT) return S_OBSP + (f - F_OBS_PREV);
     if (f < F_PARAM) return S_HACT + (f - F_HIST_ACT);
@@ -1926,13 +1926,17 @@ __device__ __forceinline__ size_t slot_index(uint32_t i, int slot) {     // in f
     return (size_t)(i >> 6) * (NG * 256) + (size_t)(slot >> 2) * 256 + (i & 63u) * 4 + (slot & 3);
 }
 __global__ void state_convert_kernel(uint32_t N, float* __restrict__ sf, float* __restrict__ pf,
-                                     int32_t* __restrict__ pi, int to_public) {
+                                     int32_t* __restrict__ pi, int to_public, int noise) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     for (int f = 0; f < NF; ++f) {
-        const int slot = pub_float_slot(f);
+        const int slot = pub_float_slot(f, noise != 0);
+        if (slot == -2) {    // not stored: exported as 0, ignored on import
+            if (to_public) pf[(size_t)f * N + i] = 0.0f;
+            continue;
+        }
         if (slot < 0) {      // motor A[j]: exported as 1 - B[j], ignored on import
-            if (to_public) pf[(size_t)f * N + i] = 1.0f - sf[slot_index(i, pub_float_slot(f + 4))];
+            if (to_public) pf[(size_t)f * N + i] = 1.0f - sf[slot_index(i, pub_float_slot(f + 4, noise != 0))];
             continue;
         }
         float* in = sf + slot_index(i, slot);
@@ -2135,7 +2139,7 @@ hipError_t launch_physics(const KParams& P, float* sf, const float* act, const f
 hipError_t launch_state_convert(const KParams& P, float* sf, float* state_f, int32_t* state_i, int to_public,
                                 hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
-    hipLaunchKernelGGL(state_convert_kernel, grid, block, 0, s, P.N, sf, state_f, state_i, to_public);
+    hipLaunchKernelGGL(state_convert_kernel, grid, block, 0, s, P.N, sf, state_f, state_i, to_public, (int)P.noise);
     return hipGetLastError();
 }
 hipError_t launch_init(const KParams& P, float* sf, hipStream_t s) {
