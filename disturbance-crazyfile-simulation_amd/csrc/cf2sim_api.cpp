@@ -189,6 +189,16 @@ int cf2_create(const cf2_config* cfg, cf2_ctx** out_ctx) {
     ctx->cfg = *cfg;
     fill_params(cfg, ctx->P);
     fill_tables(cfg, ctx->T);
+    {   // the reset-only parameters the kernels read from the device tables
+        KTables& T = ctx->T;
+        const KParams& P = ctx->P;
+        for (int k = 0; k < 3; ++k) T.init_xyz[k] = P.init_xyz[k];
+        T.pos_lim = P.pos_lim; T.angle_lim = P.angle_lim; T.yaw_lim = P.yaw_lim;
+        T.vel_lim = P.vel_lim; T.rate_lim = P.rate_lim; T.yaw_rate_lim = P.yaw_rate_lim;
+        T.action_std = P.action_std; T.motor_std = P.motor_std;
+        T.hover_x = P.hover_x; T.hover_action = P.hover_action;
+        for (int k = 0; k < 9; ++k) { T.dr_lo[k] = P.dr_lo[k]; T.dr_hi[k] = P.dr_hi[k]; }
+    }
     hipError_t e = hipGetDevice(&ctx->device);
     if (e != hipSuccess) { delete ctx; return hip_fail(e); }
     const size_t N = cfg->num_envs;

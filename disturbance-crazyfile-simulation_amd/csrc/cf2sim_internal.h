@@ -109,6 +109,11 @@ struct KTables {
     float level_values[32];
     int32_t table_of_level[32];
     double hj_grid[6][HJ_PTS];
+    // reset-only parameters (copies of the KParams fields of the same names): read by the reset
+    // code from here, so the step's kernarg block loads ~35 fewer scalars at kernel entry
+    float init_xyz[3], pos_lim, angle_lim, yaw_lim, vel_lim, rate_lim, yaw_rate_lim;
+    float action_std, motor_std, hover_x, hover_action;
+    float dr_lo[9], dr_hi[9];
 };
 
 struct StepIO {

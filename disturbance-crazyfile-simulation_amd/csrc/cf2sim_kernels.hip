@@ -961,7 +961,16 @@ __device__ __forceinline__ float downwash(const KParams& P, const float p[3], ui
 //   reset_params      domain randomisation (base.py:241-298), const-wind draw, Boltzmann level;
 //   reset_observe     the two reset sensor calls (base.py:444-456 incl. the stale-rpy_dot LPF
 //                     seed) and the history / observation row.
-template <int PHYS, class G>
+// where the reset-only parameters are read: TAB = the device tables (P.tab; the fused rollout,
+// whose register budget cannot hold them from kernel entry), else the kernarg block (the step
+// kernel: its reset tail would wait on the scalar loads)
+template <bool TAB>
+__device__ __forceinline__ decltype(auto) reset_src(const KParams& P) {
+    if constexpr (TAB) return (*P.tab);
+    else return (P);
+}
+
+template <int PHYS, bool TAB = false, class G>
 __device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const G& g, uint32_t gid) {
     const U4 b0 = g.block(0), b1 = g.block(1), b2 = g.block(2), b3 = g.block(3);
     const uint32_t u[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
@@ -971,11 +980,12 @@ __device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const
 #pragma unroll
     for (int j = 0; j < 4; ++j) E.x[j] = E.xl[j] = 0.0f;
     E.aidx = 0;
+    const auto& Tr = reset_src<TAB>(P);  // reset-only parameters
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int j = 0; j < 4; ++j) E.abuf[r][j] = 0.0f;
-    float pos[3] = {P.init_xyz[0], P.init_xyz[1], P.init_xyz[2]};
+    float pos[3] = {Tr.init_xyz[0], Tr.init_xyz[1], Tr.init_xyz[2]};
     if (P.num_drones > 1) {
         float off[3];
         formation_offset(P, gid % (uint32_t)P.num_drones, off);
@@ -986,28 +996,28 @@ __device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const
     float vel[3] = {0.0f, 0.0f, 0.0f}, rate[3] = {0.0f, 0.0f, 0.0f};
     if (P.reset_dist) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) pos[k] += -P.pos_lim + (P.pos_lim - -P.pos_lim) * u01(u[k]);
+        for (int k = 0; k < 3; ++k) pos[k] += -Tr.pos_lim + (Tr.pos_lim - -Tr.pos_lim) * u01(u[k]);
         float rpy[3];
-        rpy[0] = -P.angle_lim + (P.angle_lim - -P.angle_lim) * u01(u[4]);
-        rpy[1] = -P.angle_lim + (P.angle_lim - -P.angle_lim) * u01(u[5]);
-        rpy[2] = -P.yaw_lim + (P.yaw_lim - -P.yaw_lim) * u01(u[3]);
+        rpy[0] = -Tr.angle_lim + (Tr.angle_lim - -Tr.angle_lim) * u01(u[4]);
+        rpy[1] = -Tr.angle_lim + (Tr.angle_lim - -Tr.angle_lim) * u01(u[5]);
+        rpy[2] = -Tr.yaw_lim + (Tr.yaw_lim - -Tr.yaw_lim) * u01(u[3]);
         quat_from_euler(rpy, quat);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) vel[k] = vel[k] + (-P.vel_lim + (P.vel_lim - -P.vel_lim) * u01(u[8 + k]));
-        rate[0] = rate[0] + (-P.rate_lim + (P.rate_lim - -P.rate_lim) * u01(u[11]));
-        rate[1] = rate[1] + (-P.rate_lim + (P.rate_lim - -P.rate_lim) * u01(u[12]));
-        rate[2] = -P.yaw_rate_lim + (P.yaw_rate_lim - -P.yaw_rate_lim) * u01(u[7]);
+        for (int k = 0; k < 3; ++k) vel[k] = vel[k] + (-Tr.vel_lim + (Tr.vel_lim - -Tr.vel_lim) * u01(u[8 + k]));
+        rate[0] = rate[0] + (-Tr.rate_lim + (Tr.rate_lim - -Tr.rate_lim) * u01(u[11]));
+        rate[1] = rate[1] + (-Tr.rate_lim + (Tr.rate_lim - -Tr.rate_lim) * u01(u[12]));
+        rate[2] = -Tr.yaw_rate_lim + (Tr.yaw_rate_lim - -Tr.yaw_rate_lim) * u01(u[7]);
         float nx[4];
         normals<4>(g, 4, nx);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) E.x[j] = P.hover_x + P.motor_std * nx[j];
+        for (int j = 0; j < 4; ++j) E.x[j] = Tr.hover_x + Tr.motor_std * nx[j];
         float nb[16];
         normals<16>(g, 5, nb);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                E.abuf[r][j] = r < P.buf_size ? clampf(P.hover_action + P.action_std * nb[4 * r + j], -1.0f, 1.0f) : 0.0f;
+                E.abuf[r][j] = r < P.buf_size ? clampf(Tr.hover_action + Tr.action_std * nb[4 * r + j], -1.0f, 1.0f) : 0.0f;
     }
     abuf_last(P, E, E.la);
     E.la_view = 1;
@@ -1031,17 +1041,18 @@ __device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const
     }
 }
 
-template <bool DR, class G>
+template <bool DR, bool TAB = false, class G>
 __device__ __forceinline__ void reset_params(const KParams& P, Env& E, const G& g) {
     E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
     E.k0 = P.ft0; E.k1 = P.ft1;
 #pragma unroll
     for (int j = 0; j < 4; ++j) { E.B[j] = P.B; E.K[j] = P.K; }
     if (DR) {
+        const auto& Tr = reset_src<TAB>(P);   // reset-only parameters
         const U4 d0 = g.block(9), d1 = g.block(10), d2 = g.block(11), d3 = g.block(12);
         const uint32_t d[16] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w,
                                 d2.x, d2.y, d2.z, d2.w, d3.x, d3.y, d3.z, d3.w};
-#define DRAW(b, ui) (P.dr_lo[b] + (P.dr_hi[b] - P.dr_lo[b]) * u01(d[ui]))
+#define DRAW(b, ui) (Tr.dr_lo[b] + (Tr.dr_hi[b] - Tr.dr_lo[b]) * u01(d[ui]))
         E.dt = DRAW(0, 0); E.m = DRAW(1, 1);
         E.J[0] = DRAW(2, 2); E.J[1] = DRAW(3, 3); E.J[2] = DRAW(4, 4);
         E.k0 = DRAW(5, 5); E.k1 = DRAW(6, 6);
@@ -1119,13 +1130,13 @@ __device__ __forceinline__ void reset_observe(const KParams& P, Env& E, const G&
     compute_history<NOISE>(P, E, o1, out);
 }
 
-template <bool NOISE, bool DR, int PHYS, class G>
+template <bool NOISE, bool DR, int PHYS, bool TAB = false, class G>
 __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, uint32_t gid, float* out) {
     const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
-    reset_kinematics<PHYS>(P, E, g, gid);
+    reset_kinematics<PHYS, TAB>(P, E, g, gid);
     const int level_idx0 = E.level_idx;
     const float level0 = E.level;
-    reset_params<DR>(P, E, g);
+    reset_params<DR, TAB>(P, E, g);
     // reset_observe does not read the level; keep the redrawn one
     (void)level_idx0; (void)level0;
     reset_observe<NOISE, 0>(P, E, g, stale, out);
@@ -1832,7 +1843,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
                 // finished episode (stale body rates, gyro bias, OU state, level) from E itself
                 float o[OD];
                 const TableRng tg{s_rand + (pos - c0), C};
-                reset_env<NOISE, DR, PHYS>(P, E, tg, P.gid_off + i, o);
+                reset_env<NOISE, DR, PHYS, /*TAB=*/true>(P, E, tg, P.gid_off + i, o);
 #pragma unroll
                 for (int q = 0; q < OD; q += 2) *reinterpret_cast<float2*>(obs_row + q) = make_float2(o[q], o[q + 1]);
             }
