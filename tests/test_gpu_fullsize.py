@@ -118,3 +118,37 @@ def test_full_size_hj_adversary_slices(gpu):
     assert diverged.sum() <= 2, f"{int(diverged.sum())} envs left the 5e-4 band"
     assert worst < 5e-4
     full.close()
+
+
+def test_maximum_env_count(gpu):
+    """CF2_MAX_ENVS_PER_CTX (2^23 envs, 4 GB of state in one context): the largest grid steps
+    with finite outputs, and its first and last 256 envs equal the fp32 restatement run on those
+    slices alone (the last tile's addressing and the final block of a 32768-block grid); one env
+    more is rejected at creation."""
+    from cf2sim._native import CF2Error
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env_id, n, s = "DroneHoverBulletFreeEnvWithGust-v0", 1 << 23, 256
+    big = BatchedCrazyflieEnv(env_id, n, seed=4)
+    refs = [O.OracleEnv(build_config(env_id, s, seed=4, env_id_offset=k), precision="f32") for k in (0, n - s)]
+    go = big.reset()
+    for k, r in zip((0, n - s), refs):
+        assert _nerr(go[k:k + s].cpu().numpy(), r.reset()) < 2e-5
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(12)
+    worst = 0.0
+    for t in range(6):
+        a = (torch.rand(n, 4, device="cuda", generator=gen) * 2 - 1).contiguous()
+        g_o, g_r, g_d, _ = big.step(a)
+        assert bool(torch.isfinite(g_o).all()) and bool((g_r <= 0).all())
+        for k, r in zip((0, n - s), refs):
+            r_o, r_r, r_d, _ = r.step(a[k:k + s].cpu().numpy())
+            np.testing.assert_array_equal(g_d[k:k + s].cpu().numpy().astype(bool), r_d)
+            worst = max(worst, _nerr(g_o[k:k + s].cpu().numpy(), r_o))
+    assert worst < 5e-4, worst
+    big.close()
+    for r in refs:
+        r.close()
+    del big, go, g_o, g_r, g_d, a
+    torch.cuda.empty_cache()
+    with pytest.raises((CF2Error, ValueError)):
+        BatchedCrazyflieEnv(env_id, n + 1, seed=4)
