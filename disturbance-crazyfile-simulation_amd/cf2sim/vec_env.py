@@ -229,6 +229,50 @@ class BatchedCrazyflieEnv:
             raise ValueError("state tensors do not match cf2_layout")
         _native.check(self.lib.cf2_set_state(self._ctx, sf.data_ptr(), si.data_ptr(), self.stream), "cf2_set_state")
 
+    # ---- checkpoint / resume (the reference never checkpoints env state) ----
+    def save_checkpoint(self, path: str):
+        """Write the whole batch to a safetensors file: the state snapshot, the current
+        observations and the raw cf2_config (seed, offsets and every constant), so that
+        ``from_checkpoint`` resumes bit-identically (every draw is keyed by the seed, the global
+        env id and the per-env counter in the snapshot).  Bound HJ tables are not saved."""
+        from safetensors.torch import save_file
+        sf, si = self.get_state()
+        torch.cuda.synchronize(self.device)
+        cfg = torch.frombuffer(bytearray(bytes(self.cfg)), dtype=torch.uint8)
+        save_file({"state_f": sf.cpu(), "state_i": si.cpu(), "obs": self.obs.cpu(), "config": cfg}, path,
+                  metadata={"env_id": self.env_id, "abi_version": str(self.lib.cf2_abi_version()),
+                            "want_final_obs": str(int(self.want_final_obs))})
+
+    def load_checkpoint(self, path: str):
+        """Restore a batch saved by ``save_checkpoint`` into this env, whose configuration must be
+        the saved one (ValueError otherwise)."""
+        from safetensors import safe_open
+        with safe_open(path, framework="pt") as f:
+            meta = f.metadata() or {}
+            t = {k: f.get_tensor(k) for k in f.keys()}
+        if meta.get("abi_version") != str(self.lib.cf2_abi_version()):
+            raise ValueError(f"checkpoint written by ABI {meta.get('abi_version')}, library is "
+                             f"{self.lib.cf2_abi_version()}")
+        if bytes(t["config"].numpy().tobytes()) != bytes(self.cfg):
+            raise ValueError("checkpoint configuration differs from this env's")
+        self.set_state(t["state_f"], t["state_i"])
+        self.obs.copy_(t["obs"].to(self.device))
+
+    @classmethod
+    def from_checkpoint(cls, path: str, device=None) -> "BatchedCrazyflieEnv":
+        """A new env holding the batch saved by ``save_checkpoint`` (same config, state, obs)."""
+        from safetensors import safe_open
+        with safe_open(path, framework="pt") as f:
+            meta = f.metadata() or {}
+            raw = f.get_tensor("config").numpy().tobytes()
+        if len(raw) != ctypes.sizeof(CF2Config):
+            raise ValueError("checkpoint config size does not match this build's cf2_config")
+        cfg = CF2Config.from_buffer_copy(raw)
+        env = cls(meta.get("env_id", ""), int(cfg.num_envs), device=device, config=cfg,
+                  want_final_obs=meta.get("want_final_obs") == "1")
+        env.load_checkpoint(path)
+        return env
+
     def gather_observations(self, group=None) -> torch.Tensor:
         """RCCL all-gather of every rank's obs slab (optional policy-side exchange; the physics
         itself needs no collective).  Returns [sum of N over ranks, obs_dim] in rank order."""
