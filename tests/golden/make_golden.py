@@ -22,6 +22,8 @@ Fixtures written:
   golden_components.npz        apply_action (OU draws recorded), SensorNoise.add_noise (draws
                                recorded), quaternion conversions, Boltzmann probabilities
   golden_hj.npz                distur_gener() on a synthetic (exactly reproducible) value table
+  golden_env_hj_trajectories.npz  noise-free rollouts of the HJ-adversary envs (fixed level, hover
+                               and hover_free, and the Boltzmann-level env) on the synthetic table
   golden_ground_effect.npz     PyBulletPhysics(use_ground_effect=True).step_forward sub-steps of the
                                reference's drone placed near the ground (one case tilted past pi/2)
 """
@@ -319,6 +321,62 @@ def env_trajectories():
     return rec
 
 
+def env_hj_trajectories():
+    """Noise-free rollouts of the reference's HJ-adversary envs (hover_free.py:391-444, the
+    hover.py twin, and the Boltzmann-level env hover_free.py:608-683): their step() reads the
+    disturbance from distur_gener (distur_gener.py:19-183), here on the synthetic value table of
+    hj_vectors() saved under every level's file name.  The fixed-level envs run at level 0.5 (the
+    default 1.5 flips the drone within a few env-steps); the Boltzmann env keeps its drawn level,
+    which is recorded."""
+    from phoenix_drone_simulation.envs import hover, hover_free
+    V = synthetic_value_table()
+    acts = flight_actions()
+    rec = {}
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as td:
+        d = os.path.join(td, "phoenix_drone_simulation/adversarial_generation/FasTrack_data")
+        os.makedirs(d)
+        for k in range(31):
+            np.save(os.path.join(d, f"fastrack_{round(0.1 * k, 1)}_15x15.npy"), V)
+        os.chdir(td)
+        try:
+            cases = [("DroneHoverBulletFreeEnvWithAdversary", hover_free, 0.5),
+                     ("DroneHoverBulletEnvWithAdversary", hover, 0.5),
+                     ("DroneHoverBulletFreeEnvWithRandomHJAdversary", hover_free, None)]
+            k = 0
+            for name, mod, level in cases:
+                for rep in range(3):
+                    np.random.seed(3000 + k)
+                    env = getattr(mod, name)(observation_noise=0, domain_randomization=-1, motor_thrust_noise=0)
+                    obs0 = env.reset()
+                    if level is not None:
+                        env.disturbance_level = level
+                    bc, dr = env.bc, env.drone
+                    init = dict(p=bc.p.copy(), q=bc.q.copy(), v=bc.v.copy(), w=bc.w.copy(), x=np.array(dr.x, float),
+                                abuf=np.array(dr.action_buffer, float))
+                    a_seq = acts[(k + 5) % len(acts)]
+                    if rep == 2:
+                        a_seq = (np.random.default_rng(k).uniform(-1, 1, (60, 4)) * 0.1 + dr.HOVER_ACTION).astype(np.float32)
+                    O, Rw, D, C = [], [], [], []
+                    for a in a_seq[:120]:
+                        o, r, dn, info = env.step(np.array(a, np.float64))
+                        O.append(np.array(o, float)); Rw.append(float(r)); D.append(bool(dn)); C.append(float(info["cost"]))
+                        if dn:
+                            break
+                    key = f"{name}__{rep}"
+                    rec[key + "__obs0"] = np.array(obs0, float)
+                    for kk, vv in init.items():
+                        rec[key + "__init_" + kk] = vv
+                    rec[key + "__level"] = np.array(float(env.disturbance_level))
+                    rec[key + "__actions"] = np.array(a_seq[:len(O)], np.float32)
+                    rec[key + "__obs"] = np.array(O); rec[key + "__rew"] = np.array(Rw)
+                    rec[key + "__done"] = np.array(D); rec[key + "__cost"] = np.array(C)
+                    k += 1
+        finally:
+            os.chdir(cwd)
+    return rec
+
+
 @contextlib.contextmanager
 def recording_numpy_random(module, log):
     """Replace module.np.random.{normal,uniform,randn} by recorders that draw standard values
@@ -485,7 +543,8 @@ def hj_vectors():
 FIXTURES = {"golden_components.npz": lambda: components(),
             "golden_hj.npz": lambda: hj_vectors(),
             "golden_env_trajectories.npz": lambda: env_trajectories(),
-            "golden_ground_effect.npz": lambda: ground_effect_trajectories()}
+            "golden_ground_effect.npz": lambda: ground_effect_trajectories(),
+            "golden_env_hj_trajectories.npz": lambda: env_hj_trajectories()}
 
 
 def main(names=None):

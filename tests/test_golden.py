@@ -9,6 +9,8 @@ What each fixture pins (reference file:line):
 * boltz  Boltzmann() probabilities (utils.py:27-39)
 * hj     distur_gener() incl. Grid.get_index and the boundary rules (distur_gener.py:19-183,
          GridProcessing.py:52-71) on an exactly reproducible synthetic value table
+* env_hj whole env-steps of the HJ-adversary envs (fixed level: hover_free and hover; Boltzmann
+         level) on the synthetic value table, distur_gener run by the reference's step()
 * env    whole env-steps of DroneHoverBulletFreeEnvWithoutAdversary / DroneHoverBulletEnv /
          DroneHoverBulletEnvWithoutAdversary / DroneHoverSimpleEnv driven by the reference's
          real-flight PWM logs: apply_action, latency ring, drag, force/torque assembly,
@@ -98,11 +100,14 @@ ENV_IDS = {"DroneHoverBulletFreeEnvWithoutAdversary": "DroneHoverBulletFreeEnvWi
            "DroneHoverSimpleEnv": "DroneHoverSimpleEnv-v0"}
 
 
-def oracle_from_golden(g, key, env_id, precision="f64"):
-    """Oracle env whose state is the reference env's state right after its reset()."""
+def oracle_from_golden(g, key, env_id, precision="f64", V=None, **kw):
+    """Oracle env whose state is the reference env's state right after its reset() (HJ envs: the
+    recorded level, every level on the table V)."""
     c = build_config(env_id, 1, observation_noise=0, domain_randomization=-1, motor_thrust_noise=0,
-                     max_episode_steps=0, auto_reset=False)
+                     max_episode_steps=0, auto_reset=False, **kw)
     env = O.OracleEnv(c, precision)
+    if V is not None:
+        env.bind_tables(V, [0] * int(c.num_levels))
     sf, si = env.get_state()
     sf[:] = 0
     simple = "Simple" in key
@@ -122,6 +127,8 @@ def oracle_from_golden(g, key, env_id, precision="f64"):
     sf[81, 0] = c.time_step; sf[82, 0] = c.mass; sf[83:86, 0] = (c.ixx, c.iyy, c.izz)
     sf[86, 0] = c.ft0; sf[87, 0] = c.ft1
     sf[88:92, 0] = c.A; sf[92:96, 0] = c.B; sf[96:100, 0] = c.K
+    if key + "__level" in g.files:
+        sf[103, 0] = g[key + "__level"]
     si[:] = 0
     si[2, 0] = (1 << 4) | (1 << 5) | (1 << 6)      # both history entries alias action_buffer[-1]
     env.set_state(sf, si)
@@ -198,3 +205,38 @@ def test_ground_effect_substeps_match_reference(key):
     else:
         assert dz > 1e-4                                  # the extra thrust near the ground shows
     env.close(); off.close()
+
+
+HJ_ENV_IDS = {"DroneHoverBulletFreeEnvWithAdversary": "DroneHoverBulletFreeEnvWithAdversary-v0",
+              "DroneHoverBulletEnvWithAdversary": "DroneHoverBulletEnvWithAdversary-v0",
+              "DroneHoverBulletFreeEnvWithRandomHJAdversary": "DroneHoverBulletFreeEnvWithRandomHJAdversary-v0"}
+
+
+def hj_golden_keys():
+    g = load("golden_env_hj_trajectories.npz")
+    return sorted({k.split("__")[0] + "__" + k.split("__")[1] for k in g.files})
+
+
+def hj_oracle_from_golden(g, key, V, precision="f64"):
+    name = key.split("__")[0]
+    kw = {} if "Random" in name else dict(disturbance_level=float(g[key + "__level"]))
+    return oracle_from_golden(g, key, HJ_ENV_IDS[name], precision, V=V, **kw)
+
+
+@pytest.mark.parametrize("key", hj_golden_keys())
+def test_hj_env_steps_match_reference(key, V):
+    """The HJ-adversary env-step (hover_free.py:391-444, hover.py:649-702, the Boltzmann-level env
+    hover_free.py:608-683): quat2euler + distur_gener on the state at the start of the step, only
+    d[0], d[1] applied, then the env-step as in test_env_steps_match_reference."""
+    g = load("golden_env_hj_trajectories.npz")
+    env = hj_oracle_from_golden(g, key, V)
+    acts, obs, rew, done, cost = (g[key + s] for s in ("__actions", "__obs", "__rew", "__done", "__cost"))
+    assert len(acts) >= 10
+    for t in range(len(acts)):
+        o, r, d, info = env.step(acts[t:t + 1])
+        err = np.abs(o[0] - obs[t]) / (1 + np.abs(obs[t]))
+        assert err.max() < 1e-9, (t, err.max(), np.argmax(err))
+        assert abs(r[0] - rew[t]) <= 1e-9 * (1 + abs(rew[t])), (t, r[0], rew[t])
+        assert bool(d[0]) == bool(done[t]), t
+        assert info["cost"][0] == cost[t], t
+    env.close()

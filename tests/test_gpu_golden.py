@@ -12,6 +12,8 @@
    through the physics plug-in (cf2_physics_step) from states set with cf2_set_state.
 3. Ground effect (tests/golden/golden_ground_effect.npz): the reference's PyBulletPhysics with
    use_ground_effect=True, replayed sub-step by sub-step through the plug-in.
+4. HJ-adversary env-steps (tests/golden/golden_env_hj_trajectories.npz): the reference's own
+   step() with distur_gener on the synthetic value table, replayed with that table bound.
 """
 import numpy as np
 import pytest
@@ -262,3 +264,48 @@ def test_kernel_ground_effect_replays_reference(gpu):
             worst = max(worst, float((np.abs(got - ref) / (1 + np.abs(ref))).max()))
     drone.close()
     assert worst < 2e-5, worst
+
+
+@pytest.mark.parametrize("family", ["DroneHoverBulletFreeEnvWithAdversary", "DroneHoverBulletEnvWithAdversary",
+                                    "DroneHoverBulletFreeEnvWithRandomHJAdversary"])
+def test_kernel_replays_reference_hj_trajectories(gpu, family):
+    """The HJ-adversary env-steps of the reference (tests/golden/golden_env_hj_trajectories.npz:
+    distur_gener on the synthetic value table inside the reference's own step()) replayed on the
+    kernel with the same table bound: obs and reward within 2e-5 of the fp64 reference, done and
+    cost exact (the nearest-node search and the sign rule are exact; only fp32 rounding of the
+    state differs)."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    from test_golden import HJ_ENV_IDS, hj_golden_keys, synthetic_value_table
+    g = load("golden_env_hj_trajectories.npz")
+    keys = [k for k in hj_golden_keys() if k.split("__")[0] == family]
+    env_id, n = HJ_ENV_IDS[family], len(keys)
+    kw = dict(DET, auto_reset=False)
+    if "Random" not in family:
+        kw["disturbance_level"] = float(g[keys[0] + "__level"])
+    env = BatchedCrazyflieEnv(env_id, n, seed=0, **kw)
+    c = build_config(env_id, n, seed=0, **kw)
+    env.bind_hj_tables(torch.from_numpy(synthetic_value_table()).reshape(1, -1).cuda(), [0] * int(c.num_levels))
+    sf, si = env.get_state()
+    sf, si = sf.cpu().numpy().astype(np.float64), si.cpu().numpy()
+    for j, key in enumerate(keys):
+        _golden_state(sf, si, j, g, key, c)
+        sf[103, j] = g[key + "__level"]
+    env.set_state(torch.from_numpy(sf.astype(np.float32)), torch.from_numpy(si))
+    T = max(len(g[k + "__actions"]) for k in keys)
+    worst_o = worst_r = 0.0
+    for t in range(T):
+        a = np.stack([g[k + "__actions"][min(t, len(g[k + "__actions"]) - 1)] for k in keys]).astype(np.float32)
+        o, r, d, info = env.step(torch.from_numpy(a).cuda())
+        o, r, d, cost = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy(), info["cost"].cpu().numpy()
+        for j, k in enumerate(keys):
+            if t >= len(g[k + "__actions"]):
+                continue
+            ro = g[k + "__obs"][t]
+            worst_o = max(worst_o, float((np.abs(o[j] - ro) / (1 + np.abs(ro))).max()))
+            rr = g[k + "__rew"][t]
+            worst_r = max(worst_r, abs(float(r[j]) - rr) / (1 + abs(rr)))
+            assert bool(d[j]) == bool(g[k + "__done"][t]), (k, t)
+            assert cost[j] == g[k + "__cost"][t], (k, t)
+    env.close()
+    assert worst_o < 2e-5, worst_o
+    assert worst_r < 2e-5, worst_r
