@@ -24,6 +24,8 @@ Fixtures written:
   golden_hj.npz                distur_gener() on a synthetic (exactly reproducible) value table
   golden_env_hj_trajectories.npz  noise-free rollouts of the HJ-adversary envs (fixed level, hover
                                and hover_free, and the Boltzmann-level env) on the synthetic table
+  golden_env_uniform_trajectories.npz  noise-free rollouts of the uniform-random-adversary envs
+                               with every sampled dstb recorded
   golden_ground_effect.npz     PyBulletPhysics(use_ground_effect=True).step_forward sub-steps of the
                                reference's drone placed near the ground (one case tilted past pi/2)
 """
@@ -377,6 +379,46 @@ def env_hj_trajectories():
     return rec
 
 
+def env_uniform_trajectories():
+    """Noise-free rollouts of the reference's uniform-random-adversary envs (hover_free.py:858-1000
+    and the hover.py twin :1116-1260): every env-step's dstb_space.sample() is recorded, so the
+    same torques can be fed to the restatement and the kernel as external disturbances."""
+    from phoenix_drone_simulation.envs import hover, hover_free
+    acts = flight_actions()
+    rec = {}
+    k = 0
+    for name, mod in (("DroneHoverBulletFreeEnvWithRandomAdversary", hover_free),
+                      ("DroneHoverBulletEnvWithRandomAdversary", hover)):
+        for rep in range(2):
+            np.random.seed(4000 + k)
+            env = getattr(mod, name)(observation_noise=0, domain_randomization=-1, motor_thrust_noise=0)
+            obs0 = env.reset()
+            drawn = []
+            gen = env.dstb_gen
+            env.dstb_gen = lambda x, gen=gen, drawn=drawn: drawn.append(np.array(gen(x), float)) or drawn[-1]
+            bc, dr = env.bc, env.drone
+            init = dict(p=bc.p.copy(), q=bc.q.copy(), v=bc.v.copy(), w=bc.w.copy(), x=np.array(dr.x, float),
+                        abuf=np.array(dr.action_buffer, float))
+            a_seq = acts[(k + 9) % len(acts)] if rep == 0 else \
+                (np.random.default_rng(k).uniform(-1, 1, (80, 4)) * 0.1 + dr.HOVER_ACTION).astype(np.float32)
+            O, Rw, D, C = [], [], [], []
+            for a in a_seq[:120]:
+                o, r, dn, info = env.step(np.array(a, np.float64))
+                O.append(np.array(o, float)); Rw.append(float(r)); D.append(bool(dn)); C.append(float(info["cost"]))
+                if dn:
+                    break
+            key = f"{name}__{rep}"
+            rec[key + "__obs0"] = np.array(obs0, float)
+            for kk, vv in init.items():
+                rec[key + "__init_" + kk] = vv
+            rec[key + "__dstb"] = np.array(drawn)
+            rec[key + "__actions"] = np.array(a_seq[:len(O)], np.float32)
+            rec[key + "__obs"] = np.array(O); rec[key + "__rew"] = np.array(Rw)
+            rec[key + "__done"] = np.array(D); rec[key + "__cost"] = np.array(C)
+            k += 1
+    return rec
+
+
 @contextlib.contextmanager
 def recording_numpy_random(module, log):
     """Replace module.np.random.{normal,uniform,randn} by recorders that draw standard values
@@ -544,7 +586,8 @@ FIXTURES = {"golden_components.npz": lambda: components(),
             "golden_hj.npz": lambda: hj_vectors(),
             "golden_env_trajectories.npz": lambda: env_trajectories(),
             "golden_ground_effect.npz": lambda: ground_effect_trajectories(),
-            "golden_env_hj_trajectories.npz": lambda: env_hj_trajectories()}
+            "golden_env_hj_trajectories.npz": lambda: env_hj_trajectories(),
+            "golden_env_uniform_trajectories.npz": lambda: env_uniform_trajectories()}
 
 
 def main(names=None):

@@ -240,3 +240,31 @@ def test_hj_env_steps_match_reference(key, V):
         assert bool(d[0]) == bool(done[t]), t
         assert info["cost"][0] == cost[t], t
     env.close()
+
+
+UNI_ENV_IDS = {"DroneHoverBulletFreeEnvWithRandomAdversary": "DroneHoverBulletFreeEnvWithRandomAdversary-v0",
+               "DroneHoverBulletEnvWithRandomAdversary": "DroneHoverBulletEnvWithRandomAdversary-v0"}
+
+
+def uniform_golden_keys():
+    g = load("golden_env_uniform_trajectories.npz")
+    return sorted({k.split("__")[0] + "__" + k.split("__")[1] for k in g.files})
+
+
+@pytest.mark.parametrize("key", uniform_golden_keys())
+def test_uniform_adversary_env_steps_match_reference(key):
+    """The uniform-random-adversary env-step (hover_free.py:950-1007, hover.py:1208-1265) with
+    each step's recorded dstb_space.sample() fed back as an external disturbance."""
+    from cf2sim.config import DSTB_EXTERNAL
+    g = load("golden_env_uniform_trajectories.npz")
+    env = oracle_from_golden(g, key, UNI_ENV_IDS[key.split("__")[0]], disturbance=DSTB_EXTERNAL)
+    acts, dstb, obs, rew, done, cost = (g[key + s] for s in ("__actions", "__dstb", "__obs", "__rew", "__done", "__cost"))
+    assert len(acts) >= 10 and len(dstb) == len(acts)
+    for t in range(len(acts)):
+        o, r, d, info = env.step(acts[t:t + 1], dstb=dstb[t:t + 1])
+        err = np.abs(o[0] - obs[t]) / (1 + np.abs(obs[t]))
+        assert err.max() < 1e-9, (t, err.max(), np.argmax(err))
+        assert abs(r[0] - rew[t]) <= 1e-9 * (1 + abs(rew[t])), (t, r[0], rew[t])
+        assert bool(d[0]) == bool(done[t]), t
+        assert info["cost"][0] == cost[t], t
+    env.close()

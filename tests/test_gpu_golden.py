@@ -13,7 +13,9 @@
 3. Ground effect (tests/golden/golden_ground_effect.npz): the reference's PyBulletPhysics with
    use_ground_effect=True, replayed sub-step by sub-step through the plug-in.
 4. HJ-adversary env-steps (tests/golden/golden_env_hj_trajectories.npz): the reference's own
-   step() with distur_gener on the synthetic value table, replayed with that table bound.
+   step() with distur_gener on the synthetic value table, replayed with that table bound; the
+   uniform-random-adversary env-steps (golden_env_uniform_trajectories.npz) with the recorded
+   dstb_space.sample() torques passed as external disturbances.
 """
 import numpy as np
 import pytest
@@ -296,6 +298,47 @@ def test_kernel_replays_reference_hj_trajectories(gpu, family):
     for t in range(T):
         a = np.stack([g[k + "__actions"][min(t, len(g[k + "__actions"]) - 1)] for k in keys]).astype(np.float32)
         o, r, d, info = env.step(torch.from_numpy(a).cuda())
+        o, r, d, cost = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy(), info["cost"].cpu().numpy()
+        for j, k in enumerate(keys):
+            if t >= len(g[k + "__actions"]):
+                continue
+            ro = g[k + "__obs"][t]
+            worst_o = max(worst_o, float((np.abs(o[j] - ro) / (1 + np.abs(ro))).max()))
+            rr = g[k + "__rew"][t]
+            worst_r = max(worst_r, abs(float(r[j]) - rr) / (1 + abs(rr)))
+            assert bool(d[j]) == bool(g[k + "__done"][t]), (k, t)
+            assert cost[j] == g[k + "__cost"][t], (k, t)
+    env.close()
+    assert worst_o < 2e-5, worst_o
+    assert worst_r < 2e-5, worst_r
+
+
+@pytest.mark.parametrize("family", ["DroneHoverBulletFreeEnvWithRandomAdversary", "DroneHoverBulletEnvWithRandomAdversary"])
+def test_kernel_replays_reference_uniform_adversary_trajectories(gpu, family):
+    """The uniform-random-adversary env-steps of the reference
+    (tests/golden/golden_env_uniform_trajectories.npz) replayed on the kernel with each step's
+    recorded dstb_space.sample() passed as the external disturbance (cf2_step's dstb_dev): obs and
+    reward within 2e-5 of the fp64 reference, done and cost exact."""
+    from cf2sim.config import DSTB_EXTERNAL
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    from test_golden import UNI_ENV_IDS, uniform_golden_keys
+    g = load("golden_env_uniform_trajectories.npz")
+    keys = [k for k in uniform_golden_keys() if k.split("__")[0] == family]
+    env_id, n = UNI_ENV_IDS[family], len(keys)
+    kw = dict(DET, auto_reset=False, disturbance=DSTB_EXTERNAL)
+    env = BatchedCrazyflieEnv(env_id, n, seed=0, **kw)
+    c = build_config(env_id, n, seed=0, **kw)
+    sf, si = env.get_state()
+    sf, si = sf.cpu().numpy().astype(np.float64), si.cpu().numpy()
+    for j, key in enumerate(keys):
+        _golden_state(sf, si, j, g, key, c)
+    env.set_state(torch.from_numpy(sf.astype(np.float32)), torch.from_numpy(si))
+    T = max(len(g[k + "__actions"]) for k in keys)
+    worst_o = worst_r = 0.0
+    for t in range(T):
+        a = np.stack([g[k + "__actions"][min(t, len(g[k + "__actions"]) - 1)] for k in keys]).astype(np.float32)
+        dv = np.stack([g[k + "__dstb"][min(t, len(g[k + "__dstb"]) - 1)] for k in keys]).astype(np.float32)
+        o, r, d, info = env.step(torch.from_numpy(a).cuda(), torch.from_numpy(dv).cuda())
         o, r, d, cost = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy(), info["cost"].cpu().numpy()
         for j, k in enumerate(keys):
             if t >= len(g[k + "__actions"]):
