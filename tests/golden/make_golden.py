@@ -26,6 +26,8 @@ Fixtures written:
                                and hover_free, and the Boltzmann-level env) on the synthetic table
   golden_env_uniform_trajectories.npz  noise-free rollouts of the uniform-random-adversary envs
                                with every sampled dstb recorded
+  golden_reset_samples.npz     3000 draws of the reference's reset distribution (pose, velocities,
+                               motor state, action ring, domain-randomised parameters)
   golden_ground_effect.npz     PyBulletPhysics(use_ground_effect=True).step_forward sub-steps of the
                                reference's drone placed near the ground (one case tilted past pi/2)
 """
@@ -419,6 +421,29 @@ def env_uniform_trajectories():
     return rec
 
 
+def reset_samples():
+    """Samples of the reference's reset distribution: DroneBaseEnv.reset (base.py:420-464) with
+    task_specific_reset (hover_free.py:237-289) and apply_domain_randomization (base.py:241-298) at
+    the default 10 %, repeated 3000 times; the state and per-episode parameters are recorded after
+    each reset (the same public-snapshot fields the kernel's reset writes)."""
+    from phoenix_drone_simulation.envs import hover_free
+    np.random.seed(5000)
+    env = hover_free.DroneHoverBulletFreeEnvWithoutAdversary()
+    bc, dr = env.bc, env.drone
+    rows = []
+    for _ in range(3000):
+        env.reset()
+        rows.append(np.concatenate([bc.p, bc.q, bc.v, bc.w, np.array(dr.x, float),
+                                    np.array(dr.action_buffer, float).ravel(),
+                                    [env.time_step, bc.m], bc.I,
+                                    [dr.force_torque_factor_0, dr.force_torque_factor_1],
+                                    np.array(dr.B, float), np.array(dr.K, float)]))
+    names = (["p0", "p1", "p2", "q0", "q1", "q2", "q3", "v0", "v1", "v2", "w0", "w1", "w2"]
+             + [f"x{j}" for j in range(4)] + [f"abuf{r}{j}" for r in range(2) for j in range(4)]
+             + ["dt", "m", "Jx", "Jy", "Jz", "k0", "k1"] + [f"B{j}" for j in range(4)] + [f"K{j}" for j in range(4)])
+    return {"samples": np.array(rows), "names": np.array(names)}
+
+
 @contextlib.contextmanager
 def recording_numpy_random(module, log):
     """Replace module.np.random.{normal,uniform,randn} by recorders that draw standard values
@@ -587,7 +612,8 @@ FIXTURES = {"golden_components.npz": lambda: components(),
             "golden_env_trajectories.npz": lambda: env_trajectories(),
             "golden_ground_effect.npz": lambda: ground_effect_trajectories(),
             "golden_env_hj_trajectories.npz": lambda: env_hj_trajectories(),
-            "golden_env_uniform_trajectories.npz": lambda: env_uniform_trajectories()}
+            "golden_env_uniform_trajectories.npz": lambda: env_uniform_trajectories(),
+            "golden_reset_samples.npz": lambda: reset_samples()}
 
 
 def main(names=None):

@@ -268,3 +268,45 @@ def test_uniform_adversary_env_steps_match_reference(key):
         assert bool(d[0]) == bool(done[t]), t
         assert info["cost"][0] == cost[t], t
     env.close()
+
+
+RESET_FIELDS = (list(range(0, 13)) + list(range(16, 20)) + list(range(24, 32)) + [81, 82, 83, 84, 85, 86, 87]
+                + list(range(92, 96)) + list(range(96, 100)))   # public snapshot rows of golden "names"
+
+
+def reset_ks_pvalues(sf):
+    """Two-sample Kolmogorov-Smirnov p-value per reset field: restated resets (sf [NF, N]) vs the
+    reference's own reset() samples (golden_reset_samples.npz)."""
+    from scipy.stats import ks_2samp
+    g = load("golden_reset_samples.npz")
+    ref, names = g["samples"], g["names"]
+    assert ref.shape[1] == len(RESET_FIELDS)
+    p = {str(names[k]): float(ks_2samp(sf[f], ref[:, k]).pvalue) for k, f in enumerate(RESET_FIELDS)}
+
+    def rates(q, w):      # R(q) w: the sampled rpy_dot (hover_free.py:284-289 sets w = R^T rpy_dot)
+        x, y, z, s_ = q
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - s_ * z), 2 * (x * z + s_ * y)],
+                      [2 * (x * y + s_ * z), 1 - 2 * (x * x + z * z), 2 * (y * z - s_ * x)],
+                      [2 * (x * z - s_ * y), 2 * (y * z + s_ * x), 1 - 2 * (x * x + y * y)]])
+        return np.einsum("ijn,jn->in", R, w)
+    mine, theirs = rates(sf[3:7], sf[10:13]), rates(ref[:, 3:7].T, ref[:, 10:13].T)
+    for k in range(3):
+        p[f"rate{k}"] = float(ks_2samp(mine[k], theirs[k]).pvalue)
+    return p
+
+
+def test_reset_distribution_matches_reference_samples():
+    """DroneBaseEnv.reset + task_specific_reset + apply_domain_randomization (base.py:241-298,
+    420-464; hover_free.py:237-289) is random in both implementations (numpy's MT19937 there,
+    Philox here), so the pin is distributional: for each of the 41 pose / velocity / motor /
+    action-ring / DR fields, 4000 restated resets and the reference's 3000 are one distribution
+    by a two-sample KS test (p > 1e-4), and so are the sampled body rates R(q) w (the R^T quirk of
+    hover_free.py:284-289; the 0.028 kg K quirk shows up as p ~ 1e-220 if broken)."""
+    c = build_config("DroneHoverBulletFreeEnvWithoutAdversary-v0", 4000, seed=17)
+    env = O.OracleEnv(c)
+    env.reset()
+    sf, _ = env.get_state()
+    env.close()
+    p = reset_ks_pvalues(sf)
+    bad = {k: v for k, v in p.items() if v < 1e-4}
+    assert not bad, bad

@@ -352,3 +352,39 @@ def test_kernel_replays_reference_uniform_adversary_trajectories(gpu, family):
     env.close()
     assert worst_o < 2e-5, worst_o
     assert worst_r < 2e-5, worst_r
+
+
+def test_kernel_reset_distribution_matches_reference_samples(gpu):
+    """The kernel's reset (cf2_reset at 65 536 envs, and the in-step auto-resets of a second batch
+    after 60 random-action env-steps) vs the reference's own reset() samples
+    (tests/golden/golden_reset_samples.npz): every pose / velocity / motor / action-ring / DR field
+    and the sampled body rates R(q) w are one distribution by a two-sample KS test (p > 1e-4)."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    from test_golden import reset_ks_pvalues
+    env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
+    env = BatchedCrazyflieEnv(env_id, 65536, seed=23)
+    env.reset()
+    sf = env.get_state()[0].cpu().numpy().astype(np.float64)
+    env.close()
+    p = reset_ks_pvalues(sf)
+    bad = {k: v for k, v in p.items() if v < 1e-4}
+    assert not bad, bad
+    # auto-resets inside the step kernel (role-split block epilogue): collect the state of envs
+    # right after their reset (episode step 0 after a done)
+    env = BatchedCrazyflieEnv(env_id, 65536, seed=29)
+    env.reset()
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(4)
+    rows = []
+    for t in range(60):
+        _, _, d, _ = env.step((torch.rand(65536, 4, device="cuda", generator=gen) * 2 - 1).contiguous())
+        if t % 6 == 5:
+            sf, si = env.get_state()
+            fresh = (si[0] == 0).cpu().numpy()
+            rows.append(sf.cpu().numpy().astype(np.float64)[:, fresh])
+    env.close()
+    sf = np.concatenate(rows, 1)
+    assert sf.shape[1] > 3000, sf.shape
+    p = reset_ks_pvalues(sf)
+    bad = {k: v for k, v in p.items() if v < 1e-4}
+    assert not bad, bad
