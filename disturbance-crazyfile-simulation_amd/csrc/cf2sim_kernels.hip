@@ -1458,6 +1458,7 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
     const Tile T(sf, P.N, i);
     const uint32_t gid = P.gid_off + i;
     Env E;
+    TSTAMP(6);   // role start (after the table-draw barrier)
 #pragma unroll
     for (int k = 0; k < 3; ++k) { E.wb[k] = rs.wb[k]; E.bias[k] = rs.bias[k]; }
     const float stale[3] = {rs.wb[0], rs.wb[1], rs.wb[2]};
@@ -1476,6 +1477,8 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
         return;
     }
     reset_kinematics<PHYS>(P, E, g, gid);
+    TREADY("v"(E.q[3]), "v"(E.w[0]));
+    TSTAMP(7);   // reset pose computed
     if (role == 0) {
         T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
         T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
@@ -1502,6 +1505,8 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
     reset_observe<NOISE, 2>(P, E, g, stale, o);
 #pragma unroll
     for (int k = OL + 4; k < 2 * (OL + 4); ++k) obs_row[k] = o[k];
+    TREADY("v"(o[2 * (OL + 4) - 1]));
+    TSTAMP(8);   // role 2: second sensor call + history done
     if (NOISE || gust_mode(P))
         T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(0)));
     if (NOISE && P.held_persistent) {
@@ -1636,6 +1641,7 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
             }
             __syncthreads();     // the next chunk reuses s_rand
         }
+        TSTAMP(12);  // every reset chunk done
     } else {
         __syncthreads();         // every obs row of the block is in LDS
     }

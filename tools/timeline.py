@@ -71,6 +71,12 @@ def main():
         r6, r7, r8 = (t[rw, 9 + k].astype(np.float64) for k in range(3))
         print(f"  reset waves {int(rw.sum())}: reset_env {np.mean(r7 - r6):.0f} cycles, stores {np.mean(r8 - r7):.0f}, "
               f"barrier->reset start {np.mean(r6 - t[rw, 7]):.0f}")
+    r2 = (t[:, 9] != 0) & (t[:, 11] != 0) & (t[:, 15] != 0)     # role-2 waves (stamps 6, 7, 8, 12)
+    if r2.any():
+        a4, r6, r7, r8, e12, e5 = (t[r2, c].astype(np.float64) for c in (7, 9, 10, 11, 15, 8))
+        print(f"  role-2 waves {int(r2.sum())}: draws+barrier {np.mean(r6 - a4):.0f}, pose {np.mean(r7 - r6):.0f}, "
+              f"sensor call+history {np.mean(r8 - r7):.0f}, stores+barrier {np.mean(e12 - r8):.0f}, "
+              f"obs copy {np.mean(e5 - e12):.0f} cycles")
     print(f"waves {n_waves}; span {rend.max():.0f} cycles (realtime x24); per XCD end: " +
           " ".join(f"{x}:{rend[xcc == x].max():.0f}" for x in range(8) if (xcc == x).any()))
     for k, v in dur.items():
