@@ -27,7 +27,8 @@ Fixtures written:
   golden_env_uniform_trajectories.npz  noise-free rollouts of the uniform-random-adversary envs
                                with every sampled dstb recorded
   golden_reset_samples.npz     3000 draws of the reference's reset distribution (pose, velocities,
-                               motor state, action ring, domain-randomised parameters)
+                               motor state, action ring, domain-randomised parameters) for four
+                               env classes, and the Boltzmann env's redrawn levels
   golden_ground_effect.npz     PyBulletPhysics(use_ground_effect=True).step_forward sub-steps of the
                                reference's drone placed near the ground (one case tilted past pi/2)
 """
@@ -426,22 +427,35 @@ def reset_samples():
     task_specific_reset (hover_free.py:237-289) and apply_domain_randomization (base.py:241-298) at
     the default 10 %, repeated 3000 times; the state and per-episode parameters are recorded after
     each reset (the same public-snapshot fields the kernel's reset writes)."""
-    from phoenix_drone_simulation.envs import hover_free
-    np.random.seed(5000)
-    env = hover_free.DroneHoverBulletFreeEnvWithoutAdversary()
-    bc, dr = env.bc, env.drone
-    rows = []
-    for _ in range(3000):
-        env.reset()
-        rows.append(np.concatenate([bc.p, bc.q, bc.v, bc.w, np.array(dr.x, float),
-                                    np.array(dr.action_buffer, float).ravel(),
-                                    [env.time_step, bc.m], bc.I,
-                                    [dr.force_torque_factor_0, dr.force_torque_factor_1],
-                                    np.array(dr.B, float), np.array(dr.K, float)]))
+    from phoenix_drone_simulation.envs import hover, hover_free
     names = (["p0", "p1", "p2", "q0", "q1", "q2", "q3", "v0", "v1", "v2", "w0", "w1", "w2"]
              + [f"x{j}" for j in range(4)] + [f"abuf{r}{j}" for r in range(2) for j in range(4)]
              + ["dt", "m", "Jx", "Jy", "Jz", "k0", "k1"] + [f"B{j}" for j in range(4)] + [f"K{j}" for j in range(4)])
-    return {"samples": np.array(rows), "names": np.array(names)}
+    rec = {"names": np.array(names)}
+    # the default free-hover env; the hover (position-reward) twin (hover.py:204-256); the
+    # AdversaryInitial variant (hover_free.py:1205-1257: pi/4 angles, 300 deg/s rates); the
+    # Boltzmann-level env, whose level is redrawn at every reset (recorded as "level")
+    cases = [("samples", hover_free.DroneHoverBulletFreeEnvWithoutAdversary),
+             ("samples_hover", hover.DroneHoverBulletEnvWithoutAdversary),
+             ("samples_initial", hover_free.DroneHoverBulletFreeEnvWithAdversaryInitial),
+             ("samples_randomhj", hover_free.DroneHoverBulletFreeEnvWithRandomHJAdversary)]
+    for c, (key, cls) in enumerate(cases):
+        np.random.seed(5000 + c)
+        env = cls()
+        bc, dr = env.bc, env.drone
+        rows, levels = [], []
+        for _ in range(3000):
+            env.reset()
+            rows.append(np.concatenate([bc.p, bc.q, bc.v, bc.w, np.array(dr.x, float),
+                                        np.array(dr.action_buffer, float).ravel(),
+                                        [env.time_step, bc.m], bc.I,
+                                        [dr.force_torque_factor_0, dr.force_torque_factor_1],
+                                        np.array(dr.B, float), np.array(dr.K, float)]))
+            levels.append(float(getattr(env, "disturbance_level", 0.0)))
+        rec[key] = np.array(rows, np.float32)
+        if key == "samples_randomhj":
+            rec["levels_randomhj"] = np.array(levels)
+    return rec
 
 
 @contextlib.contextmanager

@@ -274,12 +274,19 @@ RESET_FIELDS = (list(range(0, 13)) + list(range(16, 20)) + list(range(24, 32)) +
                 + list(range(92, 96)) + list(range(96, 100)))   # public snapshot rows of golden "names"
 
 
-def reset_ks_pvalues(sf):
+RESET_CASES = {"samples": "DroneHoverBulletFreeEnvWithoutAdversary-v0",
+               "samples_hover": "DroneHoverBulletEnvWithoutAdversary-v0",
+               "samples_initial": "DroneHoverBulletFreeEnvWithAdversaryInitial-v0",
+               "samples_randomhj": "DroneHoverBulletFreeEnvWithRandomHJAdversary-v0"}
+
+
+def reset_ks_pvalues(sf, key="samples"):
     """Two-sample Kolmogorov-Smirnov p-value per reset field: restated resets (sf [NF, N]) vs the
-    reference's own reset() samples (golden_reset_samples.npz)."""
-    from scipy.stats import ks_2samp
+    reference's own reset() samples of one env class (golden_reset_samples.npz[key]); for the
+    Boltzmann env also a chi-square test of the redrawn level's distribution."""
+    from scipy.stats import chi2_contingency, ks_2samp
     g = load("golden_reset_samples.npz")
-    ref, names = g["samples"], g["names"]
+    ref, names = g[key].astype(np.float64), g["names"]
     assert ref.shape[1] == len(RESET_FIELDS)
     p = {str(names[k]): float(ks_2samp(sf[f], ref[:, k]).pvalue) for k, f in enumerate(RESET_FIELDS)}
 
@@ -292,21 +299,29 @@ def reset_ks_pvalues(sf):
     mine, theirs = rates(sf[3:7], sf[10:13]), rates(ref[:, 3:7].T, ref[:, 10:13].T)
     for k in range(3):
         p[f"rate{k}"] = float(ks_2samp(mine[k], theirs[k]).pvalue)
+    if key == "samples_randomhj":
+        lv = np.round(np.asarray(g["levels_randomhj"]) * 10).astype(int)
+        my = np.round(sf[103] * 10).astype(int)
+        counts = np.stack([np.bincount(my, minlength=21)[:21], np.bincount(lv, minlength=21)[:21]])
+        p["level"] = float(chi2_contingency(counts)[1])
     return p
 
 
-def test_reset_distribution_matches_reference_samples():
+@pytest.mark.parametrize("key", sorted(RESET_CASES))
+def test_reset_distribution_matches_reference_samples(key):
     """DroneBaseEnv.reset + task_specific_reset + apply_domain_randomization (base.py:241-298,
     420-464; hover_free.py:237-289) is random in both implementations (numpy's MT19937 there,
     Philox here), so the pin is distributional: for each of the 41 pose / velocity / motor /
     action-ring / DR fields, 4000 restated resets and the reference's 3000 are one distribution
+    (four env classes: free hover, hover, the pi/4 AdversaryInitial variant, the Boltzmann-level
+    env with its redrawn level by a chi-square test)
     by a two-sample KS test (p > 1e-4), and so are the sampled body rates R(q) w (the R^T quirk of
     hover_free.py:284-289; the 0.028 kg K quirk shows up as p ~ 1e-220 if broken)."""
-    c = build_config("DroneHoverBulletFreeEnvWithoutAdversary-v0", 4000, seed=17)
+    c = build_config(RESET_CASES[key], 4000, seed=17)
     env = O.OracleEnv(c)
     env.reset()
     sf, _ = env.get_state()
     env.close()
-    p = reset_ks_pvalues(sf)
+    p = reset_ks_pvalues(sf, key)
     bad = {k: v for k, v in p.items() if v < 1e-4}
     assert not bad, bad

@@ -354,6 +354,21 @@ def test_kernel_replays_reference_uniform_adversary_trajectories(gpu, family):
     assert worst_r < 2e-5, worst_r
 
 
+@pytest.mark.parametrize("key", ["samples_hover", "samples_initial", "samples_randomhj"])
+def test_kernel_reset_distribution_other_classes(gpu, key):
+    """cf2_reset of the hover, AdversaryInitial and Boltzmann-level env classes at 65 536 envs vs
+    the reference's reset() samples of the same class (KS per field, chi-square on the level)."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    from test_golden import RESET_CASES, reset_ks_pvalues
+    env = BatchedCrazyflieEnv(RESET_CASES[key], 65536, seed=31)
+    env.reset()
+    sf = env.get_state()[0].cpu().numpy().astype(np.float64)
+    env.close()
+    p = reset_ks_pvalues(sf, key)
+    bad = {k: v for k, v in p.items() if v < 1e-4}
+    assert not bad, bad
+
+
 def test_kernel_reset_distribution_matches_reference_samples(gpu):
     """The kernel's reset (cf2_reset at 65 536 envs, and the in-step auto-resets of a second batch
     after 60 random-action env-steps) vs the reference's own reset() samples
