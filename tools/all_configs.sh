@@ -12,6 +12,7 @@ run() {   # label, bench args...
 }
 run C2 --env-id DroneHoverBulletFreeEnvWithConstWind-v0 --envs-per-gpu 4096
 run C3 --env-id DroneHoverBulletFreeEnvWithRandomAdversary-v0 --envs-per-gpu 65536
+run C4-shard --env-id DroneHoverBulletFreeEnvWithGust-v0 --envs-per-gpu 32768
 run C4 --env-id DroneHoverBulletFreeEnvWithGust-v0 --envs-per-gpu 262144
 run C5 --env-id DroneHoverBulletFreeEnvWithDownwash-v0 --envs-per-gpu 262144
 run HJ --env-id DroneHoverBulletFreeEnvWithAdversary-v0 --envs-per-gpu 262144
