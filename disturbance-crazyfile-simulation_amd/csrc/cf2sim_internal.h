@@ -80,6 +80,7 @@ struct KParams {
     uint32_t N, gid_off, key0, key1;
     uint32_t late_block;          // step kernel: first block index past one residency round (set per launch)
     uint32_t out_stride;          // rollout kernel: rows per per-step output slab (set per launch)
+    uint32_t epb;                 // step kernel: envs per block, 64 or CF2_STEP_BLOCK (set per launch)
     int32_t agg, obs_rate, buf_size, use_latency, use_motor_dyn, max_steps, auto_reset, reset_dist;
     int32_t dstb_mode, level_mode, num_levels, gust_dur, noise, dr, phys, held_persistent, need_level;
     float time_step, mass, ixx, iyy, izz, ft0, ft1, K, A, B, hover_x, hover_action, ou_sigma;

@@ -1525,7 +1525,7 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
 template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C>
 __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& io, uint32_t base, uint32_t tid,
                                                bool do_reset, const ResetSeed& rs, float* s_obs, uint32_t* s_list,
-                                               uint32_t* s_rand, uint32_t* s_wcnt) {
+                                               uint32_t* s_rand, uint32_t* s_wcnt, uint32_t EPB = B) {
     constexpr int OD = NOISE ? 34 : 42;
     constexpr uint32_t W = B / 64u;
     if (P.auto_reset) {
@@ -1647,12 +1647,12 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
     }
     // coalesced write of the block's obs rows (contiguous in global memory)
     {
-        const uint32_t nvalid = P.N - base < B ? P.N - base : B;
+        const uint32_t nvalid = P.N - base < EPB ? P.N - base : EPB;
         float* dst = io.obs + (size_t)base * OD;
-        if (nvalid == B && (B * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
+        if (nvalid == EPB && (EPB * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
             const float4* src4 = reinterpret_cast<const float4*>(s_obs);
             float4* dst4 = reinterpret_cast<float4*>(dst);
-            for (uint32_t k = tid; k < B * OD / 4; k += B) dst4[k] = src4[k];
+            for (uint32_t k = tid; k < EPB * OD / 4; k += B) dst4[k] = src4[k];
         } else {
             const float2* src2 = reinterpret_cast<const float2*>(s_obs);
             float2* dst2 = reinterpret_cast<float2*>(dst);
@@ -1709,13 +1709,17 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     constexpr uint32_t C = CF2_RESET_CHUNK;                // auto-resets per chunk
     __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
     __shared__ uint32_t s_wcnt[B / 64];                    // finished envs per wave
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
+    // envs per block: B, or 64 at small N (set per launch): the block's other three waves then
+    // only help with its auto-resets (table draws and reset roles), which at small N are the
+    // launch's critical path, and four times as many CUs take part
+    const uint32_t EPB = P0.epb;
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * EPB, i = base + tid;
     bool do_reset = false;
     ResetSeed rs;
     __shared__ double s_hjgrid[6 * HJ_PTS];
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
-    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
+    if (tid < EPB && i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
+    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, EPB);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
     if (uint64_t* r = timing_row())
@@ -2006,7 +2010,11 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 // ------------------------------------------------------------------------------------
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
-    const dim3 grid((P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK), block(CF2_STEP_BLOCK);
+    // small N (<= 32768 envs: at most one 64-env wave per two SIMDs with the helpers) runs 64 envs
+    // per block (C2 at 4096 envs: 17.7 -> 13.2 us); above that the helper waves would cost
+    // residency (65 536 envs: 15.5 -> 24.7 us)
+    const uint32_t epb = P.N <= 32768u ? 64u : (uint32_t)CF2_STEP_BLOCK;
+    const dim3 grid((P.N + epb - 1) / epb), block(CF2_STEP_BLOCK);
     // blocks resident at once = CUs x blocks per CU at this kernel's VGPR/LDS use (queried once)
     static int round_blocks = -1;
     if (round_blocks < 0) {
@@ -2020,6 +2028,7 @@ static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t 
     }
     KParams Pl = P;
     Pl.late_block = (uint32_t)round_blocks;
+    Pl.epb = epb;
     hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, Pl, io);
     return hipGetLastError();
 }
