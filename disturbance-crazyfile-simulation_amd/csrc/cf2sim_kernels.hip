@@ -1780,7 +1780,7 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
 #ifndef CF2_ROLL_MIN_WAVES
 #define CF2_ROLL_MIN_WAVES 2   // the whole state stays live across the loop (~270 registers at peak)
 #endif
-template <bool NOISE, bool DR, int PHYS, int SPEC>
+template <bool NOISE, bool DR, int PHYS, int SPEC, uint32_t EPB>
 __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_kernel(KParams P0, StepIO io0, uint32_t K,
                                                                                   uint32_t act_stride) {
     const KParams P = shape_view<SPEC>(P0);
@@ -1793,9 +1793,11 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
     __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];
     __shared__ uint32_t s_cnt;
     __shared__ double s_hjgrid[6 * HJ_PTS];
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
+    // EPB: envs per block (64 at small N, as step_kernel; a template parameter here: a runtime
+    // count cost the large-N rollout 2.5 %)
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * EPB, i = base + tid;
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    const bool live = i < P.N;
+    const bool live = tid < EPB && i < P.N;
     const bool need_level = P.need_level || io0.level != nullptr;
     Env E;
     if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, need_level, /*with_hist=*/true);
@@ -1861,12 +1863,12 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
         }
         // coalesced write of the block's obs rows into step k's slab
         {
-            const uint32_t nvalid = P.N - base < B ? P.N - base : B;
+            const uint32_t nvalid = P.N - base < EPB ? P.N - base : EPB;
             float* dst = io0.obs + (size_t)k * n * OD + (size_t)base * OD;
-            if (nvalid == B && (B * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
+            if (nvalid == EPB && (EPB * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
                 const float4* src4 = reinterpret_cast<const float4*>(s_obs);
                 float4* dst4 = reinterpret_cast<float4*>(dst);
-                for (uint32_t q = tid; q < B * OD / 4; q += B) dst4[q] = src4[q];
+                for (uint32_t q = tid; q < EPB * OD / 4; q += B) dst4[q] = src4[q];
             } else {
                 const float2* src2 = reinterpret_cast<const float2*>(s_obs);
                 float2* dst2 = reinterpret_cast<float2*>(dst);
@@ -2043,22 +2045,25 @@ static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t 
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_kernel<NOISE, DR, PHYS, SPEC>, CF2_STEP_BLOCK, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_kernel<NOISE, DR, PHYS, SPEC, CF2_STEP_BLOCK>,
+                                                             CF2_STEP_BLOCK, 0);
         if (e != hipSuccess) return e;
         round_blocks = cus * (per_cu > 0 ? per_cu : 1);
     }
-    const uint32_t blocks = (P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK;
+    // small N: 64 envs per block, the other waves help with the resets (as launch_step_t)
+    const uint32_t epb = P.N <= 32768u ? 64u : (uint32_t)CF2_STEP_BLOCK;
+    const uint32_t blocks = (P.N + epb - 1) / epb;
     const uint32_t nslices = (blocks + (uint32_t)round_blocks - 1) / (uint32_t)round_blocks;
     const uint32_t per = (blocks + nslices - 1) / nslices;           // blocks per slice (balanced)
     constexpr int OD = NOISE ? 34 : 42;
     for (uint32_t b0 = 0; b0 < blocks; b0 += per) {
         const uint32_t nb = blocks - b0 < per ? blocks - b0 : per;
-        const uint32_t e0 = b0 * CF2_STEP_BLOCK;
+        const uint32_t e0 = b0 * epb;
         KParams Ps = P;
-        Ps.N = (P.N - e0 < nb * CF2_STEP_BLOCK) ? P.N - e0 : nb * CF2_STEP_BLOCK;
+        Ps.N = (P.N - e0 < nb * epb) ? P.N - e0 : nb * epb;
         Ps.gid_off = P.gid_off + e0;
         // a slice sees its envs as 0..Ps.N-1: the state view starts at its first tile (e0 is a
-        // multiple of 256, so of 64), each output at its first row; the per-step slab stride
+        // multiple of 64), each output at its first row; the per-step slab stride
         // stays that of the whole population (rollout_kernel strides by its own Ps.N, so the
         // outputs of a sliced launch use an explicit stride below)
         StepIO ios = io;
@@ -2072,8 +2077,12 @@ static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t 
         if (io.level) ios.level = io.level + e0;
         if (io.final_obs) ios.final_obs = io.final_obs + (size_t)e0 * OD;
         Ps.out_stride = P.N;
-        hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s, Ps, ios, K,
-                           act_stride);
+        if (epb == 64u)
+            hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC, 64u>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s, Ps, ios,
+                               K, act_stride);
+        else
+            hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC, CF2_STEP_BLOCK>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s,
+                               Ps, ios, K, act_stride);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
