@@ -17,10 +17,12 @@ HEADERS = ["cf2sim_internal.h", "cf2sim_rng.h"]
 # fp64 CPU restatements with stated tolerances (tests/test_gpu_parity.py), not bitwise.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=fast",
          "-fgpu-approx-transcendentals", "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-pass-failed"]
-# per-source extras: the env-step kernels without SLP vectorisation (packed v_pk_* f32 ops need
-# register-pair shuffles that cost more than they save there: +3 us); the policy kernel with it
-# (its activation splits / tanh / ReLU pack pairwise: -2 us of 41.6 at 262144 rows)
-SOURCE_FLAGS = {"cf2sim_kernels.hip": ["-fno-slp-vectorize"], "cf2sim_api.cpp": ["-fno-slp-vectorize"]}
+# per-source extras: no SLP vectorisation (packed v_pk_* f32 ops need register-pair shuffles
+# that cost more than they save in the env-step kernels: +3 us).  The policy kernel gained 2 us
+# from SLP at 2 waves/SIMD, but at its current 4 waves/SIMD shape SLP makes it spill (56 B/lane,
+# bf16x3 40.0 us vs 38.3 us without)
+SOURCE_FLAGS = {"cf2sim_kernels.hip": ["-fno-slp-vectorize"], "cf2sim_api.cpp": ["-fno-slp-vectorize"],
+                "cf2sim_policy.hip": ["-fno-slp-vectorize"]}
 
 
 def _hipcc() -> str:
