@@ -230,6 +230,21 @@ __device__ __forceinline__ void quat_from_euler(const float e[3], float q[4]) {
     const float il = rsq(x * x + y * y + z * z + w * w);
     q[0] = x * il; q[1] = y * il; q[2] = z * il; q[3] = w * il;
 }
+// the observation's quaternion of the noisy rpy (sensors.py): sin/cos on the transcendental unit
+// (v_sin/v_cos take revolutions), 3 muls + 6 quarter-rate ops instead of ~75 polynomial VALU ops
+__device__ __forceinline__ void quat_from_euler_obs(const float e[3], float q[4]) {
+    constexpr float inv4pi = 0.079577471545947668f;     // half angle in revolutions: e / 2 / (2 pi)
+    const float phi = e[0] * inv4pi, the = e[1] * inv4pi, psi = e[2] * inv4pi;
+    const float sp = __builtin_amdgcn_sinf(phi), cp = __builtin_amdgcn_cosf(phi);
+    const float st = __builtin_amdgcn_sinf(the), ct = __builtin_amdgcn_cosf(the);
+    const float ss = __builtin_amdgcn_sinf(psi), cs = __builtin_amdgcn_cosf(psi);
+    const float x = sp * ct * cs - cp * st * ss;
+    const float y = cp * st * cs + sp * ct * ss;
+    const float z = cp * ct * ss - sp * st * cs;
+    const float w = cp * ct * cs + sp * st * ss;
+    const float il = rsq(x * x + y * y + z * z + w * w);
+    q[0] = x * il; q[1] = y * il; q[2] = z * il; q[3] = w * il;
+}
 __device__ __forceinline__ void euler_from_quat(const float q[4], float e[3]) {
     const float sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
     const float sarg = -2.0f * (q[0] * q[2] - q[3] * q[1]);
@@ -817,7 +832,7 @@ __device__ __forceinline__ void compute_observation(const KParams& P, Env& E, co
             rot[k] = clampf(E.rpy[k] + th, lo[k], -lo[k]);
         }
         float qn[4];
-        quat_from_euler(rot, qn);
+        quat_from_euler_obs(rot, qn);
 #pragma unroll
         for (int k = 0; k < 3; ++k) E.held[k] = pos[k];
 #pragma unroll
