@@ -7,5 +7,6 @@ for p in fp32 bf16x3; do
   cat $OUT/rollout_$p.json
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$p -o r -- python3 tools/rollout_bench.py --precision $p > /dev/null 2> $OUT/prof_$p.err || { tail -5 $OUT/prof_$p.err; exit 1; }
   f=$(find $OUT/prof_$p -name "*kernel_stats.csv" | head -1); cp $f $OUT/kernel_stats_$p.csv
+  f=$(find $OUT/prof_$p -name "*kernel_trace.csv" | head -1); python tools/kernel_gaps.py $f > $OUT/gaps_$p.txt; cat $OUT/gaps_$p.txt
   cut -d, -f1-4 $OUT/kernel_stats_$p.csv | cut -c1-150 | head -12
 done
