@@ -362,15 +362,20 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         obs_buf[0] = o
         d8 = torch.empty(steps, n, dtype=torch.uint8, device=dev)
         tr8 = torch.empty(steps, n, dtype=torch.uint8, device=dev)
-        fin = envs.final_obs
+        # final observations kept per step (rows written only where an episode ended), so that the
+        # time-out values are one masked launch over all T*N rows after the loop
+        fin = torch.empty(steps, n, d, device=dev)
         for t in range(steps):
             ac.step_into(obs_buf[t], buf_a[t], buf_v[t], buf_lp[t])
-            envs.step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], final_obs_out=fin)
-            ac.value_masked(fin, tr8[t], trunc_val[t])              # V(final obs) of the time-outs only
+            envs.step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], final_obs_out=fin[t])
+        per = max(1, (2**31 - 1) // n)                      # row counts of the C ABI are 32-bit
+        for t0 in range(0, steps, per):                      # V(final obs) of the time-outs only
+            t1 = min(steps, t0 + per)
+            ac.value_masked(fin[t0:t1].view(-1, d), tr8[t0:t1].view(-1), trunc_val[t0:t1].view(-1))
         o = obs_buf[steps]
         last_val = ac.value(o)
         adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True)
-        buf_o, buf_d, buf_tr = obs_buf[:steps], d8.bool(), tr8.bool()
+        buf_o, buf_d, buf_tr = obs_buf[:steps], d8.view(torch.bool), tr8.view(torch.bool)   # 0/1 bytes
         return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val, disc)
     for t in range(steps):
         a, v, lp = ac.step(o, generator=generator)

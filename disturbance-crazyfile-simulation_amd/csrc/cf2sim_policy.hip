@@ -310,10 +310,20 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
     if (MODE == 1) {
         // value-only pass (time-out bootstraps, usually no row marked): a block none of whose
         // chunks has a marked row exits before staging the weights
+        // The block's chunks are runs of PW consecutive chunks, one run every nwaves chunks; the
+        // block's m-th chunk is (m / PW) * nwaves + blockIdx.x * PW + m % PW. Each thread checks
+        // whole chunks (CHUNK flag bytes, independent loads), so the scan is a few load latencies
+        // rather than one per chunk of each wave.
         int any = 0;
-        for (uint32_t c = wave; c < nchunks; c += nwaves) {
-            const uint32_t rr = c * CHUNK + (uint32_t)(threadIdx.x & 63);
-            any |= ((threadIdx.x & 63) < CHUNK && rr < n && mask[rr] != 0) ? 1 : 0;
+        const uint32_t per_block = ((nchunks + nwaves - 1) / nwaves) * PW;
+        for (uint32_t m = threadIdx.x; m < per_block; m += PB) {
+            const uint32_t c = (m / PW) * nwaves + blockIdx.x * PW + m % PW;
+            if (c >= nchunks) continue;
+#pragma unroll
+            for (int j = 0; j < CHUNK; ++j) {
+                const uint32_t rr = c * CHUNK + (uint32_t)j;
+                any |= (rr < n && mask[rr] != 0) ? 1 : 0;
+            }
         }
         if (!__syncthreads_or(any)) return;
     }
@@ -346,9 +356,15 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
         scale1[ks] = s_w[P::O_SCALE + k];
     }
     ObsRegs<D, PREC> X;
-    if (wave < nchunks) load_obs<D, PREC>(obs, n, wave * CHUNK, l, X);
+    if (MODE == 0 && wave < nchunks) load_obs<D, PREC>(obs, n, wave * CHUNK, l, X);
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
         const uint32_t r0 = c * CHUNK;
+        if (MODE == 1) {
+            // marked rows are sparse: a chunk without one is skipped before its observations load
+            const uint32_t rr = r0 + (uint32_t)l;
+            if (!__builtin_amdgcn_ballot_w64(l < CHUNK && rr < n && mask[rr] != 0)) continue;
+            load_obs<D, PREC>(obs, n, r0, l, X);
+        }
         // the fragments are loop-invariant: without an opaque base the compiler hoists all LDS
         // reads out of the chunk loop and spills them (an integer offset, not a laundered pointer:
         // the reads must stay LDS reads)
@@ -367,11 +383,7 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
             for (int ks = 0; ks < P::KS1; ++ks) Xc.x1[rt][ks] = (Xc.x1[rt][ks] - mean1[ks]) * scale1[ks];
         }
         // prefetch the next chunk's observations while this one runs on the matrix cores
-        if (c + nwaves < nchunks) load_obs<D, PREC>(obs, n, (c + nwaves) * CHUNK, l, X);
-        if (MODE == 1) {
-            const uint32_t rr = r0 + (uint32_t)l;
-            if (!__builtin_amdgcn_ballot_w64(l < CHUNK && rr < n && mask[rr] != 0)) continue;
-        }
+        if (MODE == 0 && c + nwaves < nchunks) load_obs<D, PREC>(obs, n, (c + nwaves) * CHUNK, l, X);
         // ---- layer 1: [pi | v] 128 neurons (8 n-tiles); MODE 1 runs only the v half
         constexpr int NT0 = PI ? 0 : 4;
         f4v h1[8][RT];
@@ -545,22 +557,41 @@ __global__ void __launch_bounds__(256) gae_kernel(uint32_t T, uint32_t n, const 
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
     float nxt_adv = 0.0f, nxt_val = last_val[e], nxt_ret = last_val[e];
-    for (int t = (int)T - 1; t >= 0; --t) {
-        const size_t k = (size_t)t * n + e;
-        const bool d = done[k] != 0;
-        const float boot = d ? (trunc[k] ? trunc_val[k] : 0.0f) : nxt_val;
-        const float v = val[k];
-        const float r = rew[k];
-        const float rs = rew_den > 0.0f ? fminf(fmaxf(r / rew_den, -10.0f), 10.0f) : r;
-        const float a = (rs + gamma * boot - v) + gamma * lam * (d ? 0.0f : nxt_adv);
-        adv[k] = a;
-        ret[k] = a + v;
-        if (disc) {
-            nxt_ret = r + gamma * (d ? boot : nxt_ret);
-            disc[k] = nxt_ret;
+    // the backward scan is serial in t; the loads of U steps are issued together so the scan
+    // waits for memory once per U steps instead of once per step (the time-out value is read
+    // only where an episode timed out)
+    constexpr int U = 8;
+    for (int t0 = (int)T - 1; t0 >= 0; t0 -= U) {
+        float rr[U], vv[U];
+        uint8_t dd[U], tt[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int t = t0 - j;
+            const size_t k = (size_t)(t < 0 ? 0 : t) * n + e;
+            rr[j] = rew[k];
+            vv[j] = val[k];
+            dd[j] = done[k];
+            tt[j] = trunc[k];
         }
-        nxt_adv = a;
-        nxt_val = v;
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int t = t0 - j;
+            if (t < 0) break;
+            const size_t k = (size_t)t * n + e;
+            const bool d = dd[j] != 0;
+            const float boot = d ? (tt[j] ? trunc_val[k] : 0.0f) : nxt_val;
+            const float v = vv[j], r = rr[j];
+            const float rs = rew_den > 0.0f ? fminf(fmaxf(r / rew_den, -10.0f), 10.0f) : r;
+            const float a = (rs + gamma * boot - v) + gamma * lam * (d ? 0.0f : nxt_adv);
+            adv[k] = a;
+            ret[k] = a + v;
+            if (disc) {
+                nxt_ret = r + gamma * (d ? boot : nxt_ret);
+                disc[k] = nxt_ret;
+            }
+            nxt_adv = a;
+            nxt_val = v;
+        }
     }
 }
 

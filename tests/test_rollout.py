@@ -166,6 +166,20 @@ def test_fused_value_masked_and_collect(gpu):
         v_ref = ac.value(obs)
     assert torch.all(out[~mask] == -7.0)
     assert float(((out[mask] - v_ref[mask]).abs() / (1 + v_ref[mask].abs())).max()) < 2e-5
+    # sparse marks over many chunks (the collect-wide time-out pass), ragged row count, mask and
+    # obs taken at an odd row offset
+    rows = 300_007
+    big = torch.randn(rows + 3, 34, device=gpu)[3:]
+    mflag = torch.zeros(rows + 5, dtype=torch.uint8, device=gpu)[5:]
+    idx = torch.cat([torch.tensor([0, 15, 16, rows - 1], device=gpu), torch.randint(0, rows, (60,), device=gpu)])
+    mflag[idx] = 1
+    out = torch.full((rows,), -7.0, device=gpu)
+    fused.value_masked(big, mflag, out)
+    sel = mflag.bool()
+    with torch.no_grad():
+        v_ref = ac.value(big[sel])
+    assert torch.all(out[~sel] == -7.0)
+    assert float(((out[sel] - v_ref).abs() / (1 + v_ref.abs())).max()) < 2e-5
     n, T = 512, 48
     envs = BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithoutAdversary-v0", n, seed=5, want_final_obs=True,
                                max_episode_steps=20)

@@ -19,10 +19,12 @@ def main():
     ap.add_argument("--env-id", default="DroneHoverBulletFreeEnvWithGust-v0")
     ap.add_argument("--torch-policy", action="store_true", help="torch layers instead of the fused HIP policy")
     ap.add_argument("--precision", default="fp32", help="fused policy products: fp32 | bf16x3")
+    ap.add_argument("--max-episode-steps", type=int, default=500, help="TimeLimit (shorter: more time-outs)")
     args = ap.parse_args()
     from cf2sim.rollout import FusedActorCritic, MLPActorCritic, collect
     from cf2sim.vec_env import BatchedCrazyflieEnv
-    envs = BatchedCrazyflieEnv(args.env_id, args.envs, seed=0, want_final_obs=True)
+    envs = BatchedCrazyflieEnv(args.env_id, args.envs, seed=0, want_final_obs=True,
+                               max_episode_steps=args.max_episode_steps)
     ac = MLPActorCritic().cuda()
     if not args.torch_policy:
         ac = FusedActorCritic(ac, seed=0, precision=args.precision)
@@ -56,7 +58,8 @@ def main():
     env_ms = ev[1].elapsed_time(ev[2]) / args.steps
     print(json.dumps({"rollout_env_steps_per_s": args.envs * args.steps / dt, "ms_per_step": dt / args.steps * 1e3,
                       "policy_ms_per_step": pol_ms, "env_ms_per_step": env_ms, "envs": args.envs,
-                      "steps": args.steps, "env_id": args.env_id,
+                      "steps": args.steps, "env_id": args.env_id, "max_episode_steps": args.max_episode_steps,
+                      "timeouts_per_step": float(ro.trunc.float().mean()) * args.envs,
                       "policy": "torch" if args.torch_policy else f"fused HIP ({args.precision})"}))
     envs.close()
 

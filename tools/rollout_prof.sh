@@ -10,3 +10,6 @@ for p in fp32 bf16x3; do
   f=$(find $OUT/prof_$p -name "*kernel_trace.csv" | head -1); python tools/kernel_gaps.py $f > $OUT/gaps_$p.txt; cat $OUT/gaps_$p.txt
   cut -d, -f1-4 $OUT/kernel_stats_$p.csv | cut -c1-150 | head -12
 done
+# time-out-heavy collect (TimeLimit 40 steps: ~2.5 % of the envs time out per step)
+timeout -k 10 120 python tools/rollout_bench.py --precision bf16x3 --max-episode-steps 40 > $OUT/rollout_bf16x3_tl40.json 2> $OUT/rollout_tl40.err || { tail -5 $OUT/rollout_tl40.err; exit 1; }
+cat $OUT/rollout_bf16x3_tl40.json
