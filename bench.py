@@ -9,7 +9,10 @@ DroneHoverBulletFreeEnvWithGust -- the reference's free-hover task (envs/hover_f
 its default sensor noise, 10 % domain randomisation, motor-thrust noise, 15 ms latency and
 TimeLimit(500) auto-reset, plus Philox-driven torque gusts.  One step = one env-step of every
 env = 2 physics sub-steps at dt = 5 ms.  Actions: uniform(-1, 1) f32 drawn once into a ring of
-device slabs, so every step reads a fresh [N, 4] action tensor from HBM.
+8 device slabs (32 MB at 262 144 envs).  The whole working set (env state ~165 MB, action ring,
+outputs) then stays within the 256 MB Infinity Cache between steps; the line's
+"streaming_actions" object times the same env-step with a 64-slab ring (268 MB), where the state
+streams from HBM every step, as under a training loop's fresh action and rollout buffers.
 
 Multi-GPU: one process per GPU (torchrun); envs are independent, each rank owns
 --envs-per-gpu envs with its own global id range (no collective in the data path; weak
@@ -137,12 +140,24 @@ def load_traffic(workload_key: str):
     return None
 
 
+def bytes_per_env_step(env) -> int:
+    return algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=50)
+    # BASELINE.md's protocol: 1000 warm-up env-steps, then 10 000 timed (~0.4 s of GPU time). All
+    # envs start together, so the first episodes end in one synchronised auto-reset wave (around
+    # env-steps 50-250); after ~1000 env-steps the reset rate is stationary (tools/reset_rate.py)
+    ap.add_argument("--steps", type=int, default=10000)
+    ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--envs-per-gpu", type=int, default=262144)
+    ap.add_argument("--action-ring", type=int, default=8,
+                    help="action slabs cycled through in the timed region (8 x 4 MB at 262 144 envs)")
+    ap.add_argument("--streaming-ring", type=int, default=64,
+                    help="after the timed region, 1000 env-steps with actions cycled through this many "
+                         "slabs (64 x 4 MB: more than the 256 MB Infinity Cache); 0 = skip")
     ap.add_argument("--env-id", default=ENV_ID)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of obs every step")
@@ -189,7 +204,7 @@ def main():
                          + 0.1 * torch.sin(3 * g[3] + 2 * g[4] - g[5] + t) for t in range(hj_tables)])
         env.bind_hj_tables(V.reshape(hj_tables, -1), [lv % hj_tables for lv in range(int(env.cfg.num_levels))])
     env.reset()
-    ring = 8
+    ring = args.action_ring
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     acts = torch.rand(ring, n, 4, device=dev, generator=g) * 2 - 1
@@ -273,9 +288,31 @@ def main():
                  "outputs": "obs, rew, done, trunc, cost, level per step (K slabs)"}
         del racts
 
+    streaming = None
+    if world == 1 and args.streaming_ring > 0:
+        # the same env-step with the actions cycled through a ring larger than the Infinity Cache
+        # (as a training loop's fresh action / rollout buffers do): the env state (~165 MB at 262 144
+        # envs) then no longer stays cache-resident between steps, so this is the HBM-streaming rate
+        sr = args.streaming_ring
+        sacts = torch.rand(sr, n, 4, device=dev, generator=g) * 2 - 1
+        for k in range(2 * sr):
+            env.step_raw(sacts[k % sr].data_ptr())
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s0.record(stream)
+        for k in range(1000):
+            env.step_raw(sacts[k % sr].data_ptr())
+        s1.record(stream)
+        torch.cuda.synchronize()
+        sus = s0.elapsed_time(s1)                            # ms for 1000 launches = us per launch
+        streaming = {"action_ring": sr, "action_bytes": sr * n * 16, "kernel_us_per_launch": sus,
+                     "value": n / (sus * 1e-6), "unit": "env-steps/s",
+                     "hbm_frac": bytes_per_env_step(env) * n / (sus * 1e-6) / 1e9 / HBM_PEAK_GBS}
+        del sacts
+
     total_env_steps = n * args.steps * world
     value = total_env_steps / elapsed
-    bytes_per = algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
+    bytes_per = bytes_per_env_step(env)
     achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
     workload_key = f"{args.env_id}:N={n}"
     traffic = load_traffic(workload_key)
@@ -309,6 +346,7 @@ def main():
                          "kernel_ms_per_launch": kern_ms},
             "cpu_baseline": cpu,
             "fused_rollout": fused,
+            "streaming_actions": streaming,
         }
         print(json.dumps(line), flush=True)
     env.close()

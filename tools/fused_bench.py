@@ -13,6 +13,8 @@ for env_id, n in [("DroneHoverBulletFreeEnvWithConstWind-v0", 4096), ("DroneHove
     env = BatchedCrazyflieEnv(env_id, n, seed=0)
     env.reset()
     a = torch.rand(K, n, 4, device="cuda") * 2 - 1
+    for k in range(1000):                # past the synchronised-start transient
+        env.step_raw(a[k % K].data_ptr())
     obs = torch.empty(K, n, env.obs_dim, device="cuda"); rew = torch.empty(K, n, device="cuda")
     done = torch.empty(K, n, dtype=torch.uint8, device="cuda"); tr = torch.empty_like(done)
     cost = torch.empty(K, n, device="cuda"); lv = torch.empty(K, n, device="cuda")

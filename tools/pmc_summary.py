@@ -7,11 +7,16 @@ import os
 import sys
 from collections import defaultdict
 
-vals = defaultdict(list)
+TAIL = 30   # the timed launches (bench.py --steps 30 after its warm-up): the last 30 dispatches
+
+per = defaultdict(dict)        # counter -> dispatch id -> value (rows of one dispatch summed)
 for f in glob.glob(os.path.join(sys.argv[1], "pmc*", "**", "*counter_collection.csv"), recursive=True):
-    for row in csv.DictReader(open(f)):
+    for i, row in enumerate(csv.DictReader(open(f))):
         if "step_kernel" in row.get("Kernel_Name", ""):
-            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+            d = per[row["Counter_Name"]]
+            key = int(row.get("Dispatch_Id") or i)
+            d[key] = d.get(key, 0.0) + float(row["Counter_Value"])
+vals = {k: [d[i] for i in sorted(d)][-TAIL:] for k, d in per.items()}
 m = {k: sum(v) / len(v) for k, v in vals.items()}
 for k in sorted(m):
     print(f"{k:32s} {m[k]:16.1f}")

@@ -10,14 +10,21 @@ out = sys.argv[1]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def mean_counter(d, name, kern):
-    v = []
+TAIL = 30   # the timed launches: the last 30 dispatches (bench.py --steps 30 after the warm-up)
+
+
+def mean_counter(d, name, kern, tail=TAIL):
+    """Mean per dispatch over the last `tail` dispatches of `kern` (0 = all); a dispatch's counter
+    may come as several rows (per XCD / dimension), which are summed."""
+    per = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for row in csv.DictReader(open(f)):
+        for i, row in enumerate(csv.DictReader(open(f))):
             if kern in row.get("Kernel_Name", "") and row["Counter_Name"] == name:
-                v.append(float(row["Counter_Value"]))
-    if not v:
+                key = int(row.get("Dispatch_Id") or i)
+                per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+    if not per:
         raise SystemExit(f"no {name} samples for {kern} in {d}")
+    v = [per[k] for k in sorted(per)][-tail if tail else 0:]
     return sum(v) / len(v)
 
 
@@ -30,8 +37,8 @@ def kernel_key():
 N = 262144
 calib_rd = N * 4 * 84
 calib_wr = N * 4 * (72 + 34)
-c_f = mean_counter(os.path.join(out, "calib_FETCH_SIZE"), "FETCH_SIZE", "kern") * 1024
-c_w = mean_counter(os.path.join(out, "calib_WRITE_SIZE"), "WRITE_SIZE", "kern") * 1024
+c_f = mean_counter(os.path.join(out, "calib_FETCH_SIZE"), "FETCH_SIZE", "kern", 0) * 1024
+c_w = mean_counter(os.path.join(out, "calib_WRITE_SIZE"), "WRITE_SIZE", "kern", 0) * 1024
 s_f = mean_counter(os.path.join(out, "step_FETCH_SIZE"), "FETCH_SIZE", "step_kernel") * 1024
 s_w = mean_counter(os.path.join(out, "step_WRITE_SIZE"), "WRITE_SIZE", "step_kernel") * 1024
 kr, kw = calib_rd / c_f, calib_wr / c_w
