@@ -4,6 +4,7 @@ this test runs it on the config of every registered hover env and the extension 
 tables, formations, external disturbance, latency / aggregation variants).  Any sanitizer report
 aborts the driver (-fno-sanitize-recover=all)."""
 import ctypes
+import fcntl
 import os
 import subprocess
 
@@ -28,7 +29,11 @@ CASES = [
 
 @pytest.fixture(scope="module")
 def drivers():
-    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], capture_output=True, text=True)
+    # pytest-xdist workers each build the fixture: serialise make so no worker runs a half-linked driver
+    os.makedirs(os.path.join(ROOT, "oracle", "_build"), exist_ok=True)
+    with open(os.path.join(ROOT, "oracle", "_build", ".asan.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail("make asan failed:\n" + r.stderr[-2000:])
     return [os.path.join(ROOT, "oracle", "_build", f"asan_driver_{p}") for p in ("f64", "f32")]
