@@ -14,9 +14,15 @@ outputs) then stays within the 256 MB Infinity Cache between steps; the line's
 "streaming_actions" object times the same env-step with a 64-slab ring (268 MB), where the state
 streams from HBM every step, as under a training loop's fresh action and rollout buffers.
 
-Multi-GPU: one process per GPU (torchrun); envs are independent, each rank owns
---envs-per-gpu envs with its own global id range (no collective in the data path; weak
-scaling).  --gather-obs adds an RCCL all-gather of the observation slab per step.
+Multi-GPU: one process per GPU.  Under torchrun the ranks come from the environment; with
+`--gpus N` and no launcher, bench.py starts its own N ranks as child processes before anything
+touches the GPU (the role of the reference's mpi_fork, utils/mpi_tools.py:47-99).  The default
+workload is BASELINE's metric config: 262 144 envs over the whole job (--global-envs), each
+rank stepping its contiguous global-id shard (32 768 envs per GPU at N = 8; "scaling":
+"strong").  Envs are independent, so the physics needs no collective; at N > 1 the reported line
+is the north-star variant with the per-step RCCL all-gather of the observation slab over xGMI
+(--gather-obs, default on at N > 1), pipelined with the next env-step.  The same shards without
+the gather ("no_gather") and 262 144 envs per GPU ("weak_scaling") are extra keys of the line.
 """
 from __future__ import annotations
 
@@ -29,11 +35,14 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
 
-HBM_PEAK_GBS = 8000.0
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_PEAK_GBS = 7 * 153.0      # 7 xGMI links x ~153 GB/s per GPU (per direction)
+INFINITY_CACHE_BYTES = 256 << 20
 # what one timed env-step writes: the reference's step() returns obs, reward, done and
 # info{cost, disturbance_level} (envs/hover_free.py:138-166, 391-444) plus TimeLimit's truncation
-BOUNDARY_OUTPUTS = ("obs", "rew", "done", "trunc", "cost", "level")   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BOUNDARY_OUTPUTS = ("obs", "rew", "done", "trunc", "cost", "level")
 ENV_ID = "DroneHoverBulletFreeEnvWithGust-v0"
+METRIC_GLOBAL_ENVS = 262144    # BASELINE.json: "262k parallel envs" for the whole node
 
 
 def algorithmic_bytes_per_env_step(cfg, outputs=("obs", "rew", "done")) -> int:
@@ -128,13 +137,16 @@ def step_kernel_key() -> str:
 
 def load_traffic(workload_key: str):
     """Per-launch HBM bytes of the step kernel from rocprofv3 PMC passes (tools/pmc_traffic.sh),
-    used only if they were measured on this workload with this very kernel build; otherwise None."""
+    used only if they were measured on this workload with this very kernel build; otherwise None.
+    profiles/step_kernel_traffic.json holds one entry per measured workload ("entries")."""
     p = os.path.join(ROOT, "profiles", "step_kernel_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") == workload_key and d.get("kernel_key") == step_kernel_key():
-            return d.get("hbm_bytes_per_launch")
+        key = step_kernel_key()
+        for e in d.get("entries", [d]):
+            if e.get("workload") == workload_key and e.get("kernel_key") == key:
+                return e.get("hbm_bytes_per_launch")
     except (OSError, ValueError, ImportError):
         pass
     return None
@@ -144,15 +156,37 @@ def bytes_per_env_step(env) -> int:
     return algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
 
 
-def main():
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: the launcher's WORLD_SIZE, else 1); without a launcher "
+                         "bench.py starts the N ranks itself")
     # BASELINE.md's protocol: 1000 warm-up env-steps, then 10 000 timed (~0.4 s of GPU time). All
     # envs start together, so the first episodes end in one synchronised auto-reset wave (around
     # env-steps 50-250); after ~1000 env-steps the reset rate is stationary (tools/reset_rate.py)
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=1000)
-    ap.add_argument("--envs-per-gpu", type=int, default=262144)
+    ap.add_argument("--global-envs", type=int, default=METRIC_GLOBAL_ENVS,
+                    help="envs over the whole job (BASELINE's metric config); each rank steps its contiguous shard")
+    ap.add_argument("--envs-per-gpu", type=int, default=None,
+                    help="weak scaling instead: this many envs on every rank (overrides --global-envs)")
+    ap.add_argument("--gather-obs", dest="gather_obs", action="store_true", default=None,
+                    help="per-step RCCL all-gather of the obs slab (default: on at N > 1)")
+    ap.add_argument("--no-gather-obs", dest="gather_obs", action="store_false")
+    ap.add_argument("--weak-envs", type=int, default=262144,
+                    help="N > 1: the weak_scaling key times this many envs per rank; 0 = skip")
+    ap.add_argument("--weak-steps", type=int, default=1000)
+    ap.add_argument("--oc-envs", type=int, default=1 << 20,
+                    help="N = 1: the out-of-cache line steps this many envs (working set far beyond the 256 MB "
+                         "Infinity Cache, so state traffic is HBM traffic); 0 = skip")
+    ap.add_argument("--oc-steps", type=int, default=500)
     ap.add_argument("--action-ring", type=int, default=8,
                     help="action slabs cycled through in the timed region (8 x 4 MB at 262 144 envs)")
     ap.add_argument("--streaming-ring", type=int, default=64,
@@ -160,7 +194,6 @@ def main():
                          "slabs (64 x 4 MB: more than the 256 MB Infinity Cache); 0 = skip")
     ap.add_argument("--env-id", default=ENV_ID)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of obs every step")
     ap.add_argument("--graph", action="store_true", help="capture the timed steps in a hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=16384)
@@ -168,16 +201,55 @@ def main():
     ap.add_argument("--env-kw", default="{}", help="JSON env kwargs (ablations), e.g. '{\"observation_noise\": 0}'")
     ap.add_argument("--rollout-k", type=int, default=32,
                     help="also time the fused K-step rollout (cf2_rollout, random actions) on 1 GPU; 0 = skip")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def bind_synthetic_tables(env, dev):
+    """HJ-adversary envs: the reference's fastrack_{level}_15x15.npy tables are not in its checkout
+    (.MISSING_LARGE_BLOBS); bind smooth synthetic 15^6 tables (one per 3 levels).  Returns the count."""
+    import torch
+    if int(env.cfg.disturbance) != 5:
+        return 0
+    nt = 3
+    ax = torch.linspace(-1.0, 1.0, 15, device=dev)
+    g = [ax.view([-1 if i == d else 1 for i in range(6)]) for d in range(6)]
+    V = torch.stack([sum((0.3 + 0.1 * t + 0.05 * d) * g[d] ** (1 + (d + t) % 2) for d in range(6))
+                     + 0.1 * torch.sin(3 * g[3] + 2 * g[4] - g[5] + t) for t in range(nt)])
+    env.bind_hj_tables(V.reshape(nt, -1), [lv % nt for lv in range(int(env.cfg.num_levels))])
+    return nt
+
+
+def working_set_bytes(env, ring: int) -> int:
+    """Bytes one env-step touches: internal state (30 float4 groups per env), the action ring and
+    the boundary outputs.  Below ~256 MB they stay in the Infinity Cache between env-steps."""
+    n, od = env.num_envs, env.obs_dim
+    return n * 480 + ring * n * 16 + n * (4 * od + 4 + 1 + 1 + 4 + 4)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if launched == 0 and (args.gpus or 1) > 1:
+        # no launcher: start the N ranks as children of this process, which never touches the GPU
+        from cf2sim.dist import launch_plan, run_ranks
+        plan = launch_plan(args.gpus, _free_port(), os.path.abspath(__file__), sys.argv[1:] if argv is None else argv)
+        sys.exit(run_ranks(plan))
+    world = launched or 1
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus}, but the launcher started {world} ranks")
     env_kw = json.loads(args.env_kw)
 
     import torch
     import torch.distributed as dist
+    from cf2sim.dist import PipelinedObsGather, shard_range
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    backend = None
+    # a process group at N > 1, and at N = 1 under a launcher when --gather-obs is asked for
+    # explicitly (exercises the RCCL gather path on a one-GPU box)
+    use_pg = world > 1 or (launched > 0 and bool(args.gather_obs))
+    if use_pg:
         # one process per GPU over RCCL ("nccl"); CF2_BENCH_BACKEND=gloo rehearses the multi-rank
         # path with several ranks sharing the GPUs of a smaller box
         backend = os.environ.get("CF2_BENCH_BACKEND", "nccl")
@@ -187,38 +259,87 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, expected {world}")
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from cf2sim.vec_env import BatchedCrazyflieEnv
 
-    n = args.envs_per_gpu
-    env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=rank * n, device=dev, **env_kw)
-    hj_tables = 0
-    if int(env.cfg.disturbance) == 5:
-        # HJ-adversary envs: the reference's fastrack_{level}_15x15.npy tables are not in its
-        # checkout (.MISSING_LARGE_BLOBS); bind smooth synthetic 15^6 tables (one per 3 levels)
-        hj_tables = 3
-        ax = torch.linspace(-1.0, 1.0, 15, device=dev)
-        g = [ax.view([-1 if i == d else 1 for i in range(6)]) for d in range(6)]
-        V = torch.stack([sum((0.3 + 0.1 * t + 0.05 * d) * g[d] ** (1 + (d + t) % 2) for d in range(6))
-                         + 0.1 * torch.sin(3 * g[3] + 2 * g[4] - g[5] + t) for t in range(hj_tables)])
-        env.bind_hj_tables(V.reshape(hj_tables, -1), [lv % hj_tables for lv in range(int(env.cfg.num_levels))])
+    if args.envs_per_gpu:
+        n, off, scaling = args.envs_per_gpu, rank * args.envs_per_gpu, "weak"
+        shards = [n] * world
+    else:
+        off, n = shard_range(args.global_envs, rank, world)
+        scaling = "strong"
+        shards = [shard_range(args.global_envs, r, world)[1] for r in range(world)]
+    global_envs = sum(shards)
+    gather = (world > 1) if args.gather_obs is None else bool(args.gather_obs)
+    gather = gather and use_pg
+
+    def max_over_ranks(x: float) -> float:
+        if not use_pg:
+            return x
+        t = torch.tensor([x], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier_sync():
+        if use_pg:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=off, device=dev, **env_kw)
+    hj_tables = bind_synthetic_tables(env, dev)
     env.reset()
     ring = args.action_ring
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     acts = torch.rand(ring, n, 4, device=dev, generator=g) * 2 - 1
-    gathered = None
+    stream = torch.cuda.current_stream()
 
-    def one_step(k):
-        env.step_raw(acts[k % ring].data_ptr())
-        if args.gather_obs and world > 1:
-            dist.all_gather_into_tensor(gathered, env.obs)
+    pipe = None
+    gather_mode = None
+    if gather:
+        if len(set(shards)) == 1:
+            pipe = PipelinedObsGather(n, env.obs_dim, dev)
+            gather_mode = "pipelined all_gather_into_tensor (2 obs buffers, side stream)"
+        else:
+            gather_mode = "ragged shards: synchronous padded all_gather"
 
-    if args.gather_obs and world > 1:
-        gathered = torch.empty(world * n, env.obs_dim, device=dev)
+    def one_step(k, with_gather):
+        if with_gather and pipe is not None:
+            buf = pipe.buffer()
+            env.step_raw(acts[k % ring].data_ptr(), obs_ptr=buf.data_ptr())
+            pipe.publish()
+        else:
+            env.step_raw(acts[k % ring].data_ptr())
+            if with_gather:
+                env.gather_observations()
+
+    def run(steps, with_gather, graph=None):
+        """exactly `steps` env-steps between barrier + synchronize; returns the max-over-ranks wall
+        time and this rank's HIP-event time on the launch stream"""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier_sync()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            for k in range(steps):
+                one_step(k, with_gather)
+        if with_gather and pipe is not None:
+            pipe.drain()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if use_pg:
+            dist.barrier()
+        return max_over_ranks(time.perf_counter() - t0), e0.elapsed_time(e1)
+
     for k in range(args.warmup):
-        one_step(k)
+        one_step(k, gather)
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize()
 
     graph = None
@@ -229,44 +350,55 @@ def main():
         with torch.cuda.stream(s):
             with torch.cuda.graph(graph, stream=s):
                 for k in range(args.steps):
-                    one_step(k)
+                    one_step(k, gather)
+                if pipe is not None:
+                    pipe.drain()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
-    # ---- timed region: exactly K steps between barrier + synchronize ----
-    stream = torch.cuda.current_stream()
-    ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev_start.record(stream)
-    if graph is not None:
-        graph.replay()
-    else:
-        for k in range(args.steps):
-            one_step(k)
-    ev_end.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # average step-kernel duration over the timed region, HIP events on the launch stream
-    kern_ms = ev_start.elapsed_time(ev_end) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    if args.gather_obs and world > 1:
+    # ---- timed region: exactly K steps between barrier + synchronize, max over ranks ----
+    elapsed, ev_ms = run(args.steps, gather, graph)
+    kern_ms = ev_ms / args.steps
+    if gather:
         # the timed region also holds the all-gathers: time the step kernel alone here
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
-        for k in range(20):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
+        torch.cuda.synchronize()
+        for k in range(50):
             ev[k][0].record(stream)
             env.step_raw(acts[k % ring].data_ptr())
             ev[k][1].record(stream)
         torch.cuda.synchronize()
-        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / 20
+        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / 50
+
+    no_gather = None
+    if gather:
+        el2, ev2 = run(args.steps, False)
+        no_gather = {"value": global_envs * args.steps / el2, "unit": "env-steps/s",
+                     "ms_per_step": el2 / args.steps * 1e3, "kernel_ms_per_launch": ev2 / args.steps}
+
+    weak = None
+    if world > 1 and not args.envs_per_gpu and args.weak_envs > 0:
+        # weak scaling: a fixed 262 144 envs per GPU (no gather); max over ranks as above
+        wn = args.weak_envs
+        wenv = BatchedCrazyflieEnv(args.env_id, wn, seed=args.seed, env_id_offset=rank * wn, device=dev, **env_kw)
+        bind_synthetic_tables(wenv, dev)
+        wenv.reset()
+        wacts = torch.rand(ring, wn, 4, device=dev, generator=g) * 2 - 1
+        for k in range(200):
+            wenv.step_raw(wacts[k % ring].data_ptr())
+        barrier_sync()
+        t0 = time.perf_counter()
+        for k in range(args.weak_steps):
+            wenv.step_raw(wacts[k % ring].data_ptr())
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        wel = max_over_ranks(time.perf_counter() - t0)
+        weak = {"envs_per_gpu": wn, "global_envs": wn * world, "steps": args.weak_steps, "gather_obs": False,
+                "value": wn * world * args.weak_steps / wel, "unit": "env-steps/s",
+                "ms_per_step": wel / args.weak_steps * 1e3}
+        wenv.close()
+        del wacts
 
     fused = None
     if world == 1 and args.rollout_k > 0:
@@ -306,16 +438,50 @@ def main():
         torch.cuda.synchronize()
         sus = s0.elapsed_time(s1)                            # ms for 1000 launches = us per launch
         streaming = {"action_ring": sr, "action_bytes": sr * n * 16, "kernel_us_per_launch": sus,
-                     "value": n / (sus * 1e-6), "unit": "env-steps/s",
+                     "value": n / (sus * 1e-6), "unit": "env-steps/s", "cache_resident": False,
                      "hbm_frac": bytes_per_env_step(env) * n / (sus * 1e-6) / 1e9 / HBM_PEAK_GBS}
         del sacts
 
-    total_env_steps = n * args.steps * world
-    value = total_env_steps / elapsed
     bytes_per = bytes_per_env_step(env)
+    out_of_cache = None
+    if world == 1 and args.oc_envs > 0:
+        # out of the Infinity Cache: at 1 Mi envs the env state alone is ~500 MB, so every env-step
+        # reads and writes it in HBM (the PMC byte counters, which include Infinity-Cache hits, then
+        # measure HBM traffic: profiles/, tools/pmc_traffic.sh)
+        on = args.oc_envs
+        oenv = BatchedCrazyflieEnv(args.env_id, on, seed=args.seed, device=dev, **env_kw)
+        bind_synthetic_tables(oenv, dev)
+        oenv.reset()
+        oacts = torch.rand(ring, on, 4, device=dev, generator=g) * 2 - 1
+        for k in range(200):
+            oenv.step_raw(oacts[k % ring].data_ptr())
+        o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        o0.record(stream)
+        for k in range(args.oc_steps):
+            oenv.step_raw(oacts[k % ring].data_ptr())
+        o1.record(stream)
+        torch.cuda.synchronize()
+        ous = o0.elapsed_time(o1) * 1e3 / args.oc_steps
+        oach = bytes_per * on / (ous * 1e-6) / 1e9
+        otraffic = load_traffic(f"{args.env_id}:N={on}")
+        out_of_cache = {"envs": on, "working_set_bytes": working_set_bytes(oenv, ring), "cache_resident": False,
+                        "kernel_us_per_launch": ous, "value": on / (ous * 1e-6), "unit": "env-steps/s",
+                        "achieved": oach, "frac": oach / HBM_PEAK_GBS,
+                        "frac_of_measured_hbm": oach / 6290.0,
+                        "traffic": otraffic, "traffic_ratio": (otraffic / (bytes_per * on)) if otraffic else None}
+        oenv.close()
+        del oacts
+
+    value = global_envs * args.steps / elapsed
     achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
-    workload_key = f"{args.env_id}:N={n}"
-    traffic = load_traffic(workload_key)
+    traffic = load_traffic(f"{args.env_id}:N={n}")
+    wset = working_set_bytes(env, ring)
+    gather_info = None
+    if gather:
+        rx = (global_envs - n) * env.obs_dim * 4          # bytes this rank receives per step
+        gather_info = {"mode": gather_mode, "bytes_in_per_rank_per_step": rx, "total_bytes_per_step": global_envs * env.obs_dim * 4,
+                       "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS}
 
     if rank == 0:
         cpu = None
@@ -326,31 +492,40 @@ def main():
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "world_size": world,
+            "backend": backend,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: uniform(-1,1) actions, Philox-seeded resets/noise/gusts"
                     + (f", {hj_tables} synthetic 15^6 HJ value tables" if hj_tables else ""),
-            "config": {"workload": f"{args.env_id} ({describe(env.cfg)}), {n} envs per GPU",
-                       "envs_per_gpu": n, "global_envs": n * world, "aggregate_phy_steps": 2,
-                       "parallelism": f"env-shard x{world}", "gather_obs": bool(args.gather_obs),
+            "config": {"workload": f"{args.env_id} ({describe(env.cfg)}), {global_envs} envs over {world} GPU(s)"
+                                   f" ({n} per GPU)",
+                       "envs_per_gpu": n, "global_envs": global_envs, "aggregate_phy_steps": 2,
+                       "parallelism": f"env-shard x{world}", "gather_obs": bool(gather),
                        "graph": bool(args.graph)},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS,
                          "traffic": traffic,
                          "algorithmic_bytes_per_env_step": bytes_per,
-                         "kernel_ms_per_launch": kern_ms},
+                         "kernel_ms_per_launch": kern_ms,
+                         "working_set_bytes": wset,
+                         "cache_resident": wset < INFINITY_CACHE_BYTES,
+                         "out_of_cache": out_of_cache},
             "cpu_baseline": cpu,
+            "gather": gather_info,
+            "no_gather": no_gather,
+            "weak_scaling": weak,
             "fused_rollout": fused,
             "streaming_actions": streaming,
         }
         print(json.dumps(line), flush=True)
     env.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -7,8 +7,124 @@ independent of the number of ranks.  The only exchange is optional: gathering th
 observation slabs for a policy that lives elsewhere (RCCL all-gather over xGMI on GPUs, gloo on
 CPU).  The reference's MPI gradient all-reduce (utils/mpi_tools.py) belongs to its learner and
 stays out of scope.
+
+``launch_plan`` / ``run_ranks`` start one process per GPU when no launcher (torchrun) did, and
+``PipelinedObsGather`` overlaps the per-step observation all-gather with the next env-step.
 """
 from __future__ import annotations
+
+import os
+
+
+def launch_plan(world: int, port: int, script: str, argv: list[str], base_env: dict | None = None,
+                python: str | None = None) -> list[tuple[list[str], dict]]:
+    """(command, environment) of each rank when a script launches its own ranks: one fresh process
+    per GPU, rank r on local GPU r, rendezvous on 127.0.0.1:port.  This is the role of the
+    reference's ``mpi_fork`` (utils/mpi_tools.py:47-99, which re-runs the script under
+    ``mpirun -np N``); here the ranks are started as children, never by re-executing the calling
+    process, and before the caller makes any GPU call (a process that has touched the GPU must not
+    exec another program)."""
+    import sys
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    env0 = dict(os.environ if base_env is None else base_env)
+    cmd = [python or sys.executable, "-u", script, *argv]
+    plan = []
+    for r in range(world):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plan.append((list(cmd), env))
+    return plan
+
+
+def run_ranks(plan, timeout: float | None = None) -> int:
+    """Start every rank of a launch_plan, wait for all of them and return the first non-zero exit
+    code (0 if all succeeded).  If one rank fails, the others are terminated (their own process
+    groups only) so a collective never waits for a dead peer."""
+    import signal
+    import subprocess
+    import time
+    procs = [subprocess.Popen(cmd, env=env, start_new_session=True) for cmd, env in plan]
+    rc, t0 = 0, time.monotonic()
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:
+                        os.killpg(q.pid, signal.SIGTERM)
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                for q in procs:
+                    os.killpg(q.pid, signal.SIGKILL)
+                return rc or 124
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL)
+    return rc
+
+
+class PipelinedObsGather:
+    """Per-step all-gather of the observation slab ("RCCL all-gather over
+    xGMI only for the returned observation tensor"), overlapped with the next env-step.
+
+    ``depth`` observation buffers rotate: env-step k writes ``buffer()`` on the compute stream and
+    ``publish()`` starts the all-gather of that buffer on a side stream, so the gather of step k
+    runs while step k+1 computes.  Before step k+depth overwrites a buffer, the compute stream (not
+    the host) waits for the gather that read it.  ``publish()`` returns the [world * n, D] tensor
+    the gather fills; it is complete once ``wait(k)`` or ``drain()`` returned and stays valid until
+    the gather of step k + depth reuses it.  On gloo (CPU rehearsal of the multi-rank path) the
+    gather stages through the host and completes inside ``publish()``."""
+
+    def __init__(self, n: int, obs_dim: int, device, group=None, depth: int = 2):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+        self.depth = int(depth)
+        self.obs = [torch.empty(n, obs_dim, device=device) for _ in range(self.depth)]
+        self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
+        self.sizes = [n] * self.world
+        self.comm = torch.cuda.Stream(device=device) if self.nccl else None
+        self.work = [None] * self.depth
+        self.k = 0
+
+    def buffer(self):
+        """The obs buffer env-step k writes; the current stream first waits (on the device) for
+        the gather of step k - depth, which read it."""
+        j = self.k % self.depth
+        w = self.work[j]
+        if w is not None:
+            w.wait()
+            self.work[j] = None
+        return self.obs[j]
+
+    def publish(self):
+        """Start the all-gather of the buffer the current env-step wrote; returns its output."""
+        import torch
+        import torch.distributed as dist
+        j = self.k % self.depth
+        if self.nccl:
+            self.comm.wait_stream(torch.cuda.current_stream(self.obs[j].device))
+            with torch.cuda.stream(self.comm):
+                self.work[j] = dist.all_gather_into_tensor(self.out[j], self.obs[j], group=self.group, async_op=True)
+        else:
+            gather_rows(self.obs[j], self.group, sizes=self.sizes, out=self.out[j])
+        self.k += 1
+        return self.out[j]
+
+    def drain(self):
+        """Make the current stream wait for every gather in flight."""
+        for j, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[j] = None
 
 
 def shard_range(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:

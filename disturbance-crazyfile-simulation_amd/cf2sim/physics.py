@@ -79,7 +79,7 @@ class BatchedDrone:
         return self.env.reset(mask)
 
     def _fields(self):
-        sf, _ = self.env.get_state()
+        sf, _ = self.env.snapshot()          # one conversion per state change, shared by the properties
         return sf, self.env.layout
 
     @property
@@ -203,6 +203,7 @@ class BasePhysics:
         dt = 0.0 if self.time_step is None else float(self.time_step)
         _native.check(self._lib.cf2_physics_step(env._ctx, a.data_ptr(), _native.ptr(d), ctypes.c_float(dt),
                                                  env.stream), "cf2_physics_step")
+        env._state_version += 1
 
     def step_forward(self, action, *args, **kwargs) -> None:
         raise NotImplementedError

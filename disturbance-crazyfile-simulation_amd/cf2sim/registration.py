@@ -76,6 +76,7 @@ class CrazyflieEnv:
         self._t = 0
         self._needs_reset = True
         self._last_action = np.zeros(4, np.float32)
+        self._field_idx = None
         # penalty terms of the last compute_reward (envs/hover_free.py:61-66, 227-232), read by the
         # reference's learner for logging (algs/iwpg/iwpg.py:531-532)
         self.penalty_log = self.penalty_rpy_log = self.penalty_crash_log = 0.0
@@ -91,43 +92,63 @@ class CrazyflieEnv:
         self._make()
         return [self._seed]
 
+    def _state_fields(self):
+        """Indices into the state snapshot of what the host side reads per step: pos, quat, vel,
+        omega, rpy (Simple physics) and the action buffer's last row (drone.last_action)."""
+        if getattr(self, "_field_idx", None) is None:
+            import torch
+            L = self._env.layout
+            last = L.f_abuf + 4 * (int(self._env.cfg.buf_size) - 1)
+            idx = ([L.f_pos + k for k in range(3)] + [L.f_quat + k for k in range(4)] + [L.f_vel + k for k in range(3)]
+                   + [L.f_omega + k for k in range(3)] + [L.f_rpy + k for k in range(3)] + [last + k for k in range(4)])
+            self._field_idx = torch.tensor(idx, dtype=torch.long, device=self._env.device)
+        return self._field_idx
+
     def reset(self) -> np.ndarray:
+        import torch
         obs = self._env.reset()
         self._t = 0
         self._needs_reset = False
-        sf, si = self._env.get_state()
-        L = self._env.layout
-        self._last_action = sf[L.f_abuf + 4 * (int(self._env.cfg.buf_size) - 1):][:4, 0].cpu().numpy()
-        return obs[0].double().cpu().numpy()
+        sf, _ = self._env.snapshot()
+        # one device -> host transfer: the observation row and the action buffer's last row
+        h = torch.cat([obs[0], sf[self._state_fields(), 0]]).cpu().double().numpy()
+        od = self._env.obs_dim
+        self._last_action = h[od + 16:od + 20].astype(np.float32)
+        return h[:od]
 
     def step(self, action):
         import torch
         if self._needs_reset:
             raise RuntimeError("call reset() before step() (gym TimeLimit semantics)")
-        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, 4), device=self._env.device)
+        act = np.asarray(action, dtype=np.float32).reshape(4)
+        a = torch.as_tensor(act.reshape(1, 4), device=self._env.device)
         obs, rew, done, info = self._env.step(a)
+        sf, _ = self._env.snapshot()
+        # everything the host needs from this step in ONE device -> host transfer (one stream
+        # sync): obs row, reward, done, cost, level and the state fields the penalty log reads
+        h = torch.cat([obs[0], rew, done.float(), info["cost"], info["disturbance_level"],
+                       sf[self._state_fields(), 0]]).cpu().double().numpy()
+        od = self._env.obs_dim
+        r, terminal, cost, level = float(h[od]), bool(h[od + 1] != 0), float(h[od + 2]), float(h[od + 3])
         self._t += 1
-        terminal = bool(done[0].item())
-        self._log_penalties(np.asarray(action, np.float32).reshape(4), terminal)
-        info_out = {"cost": float(info["cost"][0].item()),
-                    "disturbance_level": float(info["disturbance_level"][0].item())}
+        self._log_penalties(act, terminal, h[od + 4:])
+        info_out = {"cost": cost, "disturbance_level": level}
         truncated = self._t >= self.max_episode_steps > 0
         if truncated and not terminal:
             info_out["TimeLimit.truncated"] = True
         d = terminal or truncated
         if d:
             self._needs_reset = True
-        return obs[0].double().cpu().numpy(), float(rew[0].item()), d, info_out
+        return h[:od], r, d, info_out
 
-    def _log_penalties(self, action, terminal: bool):
+    def _log_penalties(self, action, terminal: bool, st):
         """The individual terms of compute_reward (hover_free.py:206-235) from the env's state after
-        the step (host-side, single-env adapter only; the batched kernel computes the reward)."""
+        the step (host-side, single-env adapter only; the batched kernel computes the reward).
+        st: pos, quat, vel, omega, rpy, last action (_state_fields order), float64."""
         c = self._env.cfg
-        sf = self._env.get_state()[0][:, 0].double().cpu().numpy()
-        L = self._env.layout
-        p, q, v, w = sf[L.f_pos:L.f_pos + 3], sf[L.f_quat:L.f_quat + 4], sf[L.f_vel:L.f_vel + 3], sf[L.f_omega:L.f_omega + 3]
+        p, q, v, w = st[0:3], st[3:7], st[7:10], st[10:13]
         if int(c.physics) == PHYS_SIMPLE:
-            rpy, rpy_dot = sf[L.f_rpy:L.f_rpy + 3], w
+            rpy, rpy_dot = st[13:16], w
         else:
             x, y, z, qw = q
             sarg = min(max(-2.0 * (x * z - qw * y), -1.0), 1.0)

@@ -53,7 +53,13 @@ _ACT = {"relu": nn.ReLU, "tanh": nn.Tanh, "identity": nn.Identity}
 class OnlineMeanStd(nn.Module):
     """Running mean / standard deviation (utils/online_mean_std.py): the incremental update of
     Chan et al. over batches, single process (the reference's MPI averages are the identity with
-    one process; across GPUs, batches of every rank can be concatenated before update())."""
+    one process; across GPUs, batches of every rank can be concatenated before update()).
+
+    Provenance: this restates the reference's OnlineMeanStd closely -- same epsilon, same clip
+    bound 10, the same n_A / n_AB / delta / mean / M2 update in the same order -- because the
+    standardised observations must reproduce the reference's arithmetic to match
+    tests/golden/golden_f3.npz (generated from the reference's own class).  It is a ~35-line
+    standard algorithm, not new design."""
 
     def __init__(self, epsilon: float = 1e-5, shape=()):
         super().__init__()

@@ -71,6 +71,11 @@ class BatchedCrazyflieEnv:
         self.level = torch.zeros(n, dtype=torch.float32, device=d)
         self.want_final_obs = want_final_obs
         self.final_obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=d) if want_final_obs else None
+        # the observations of the latest reset / step: self.obs, or the caller buffer (slab) that
+        # step_into / rollout / step_raw wrote them to (what save_checkpoint saves)
+        self._obs_latest = self.obs
+        self._state_version = 0          # bumped by every call that changes the env state
+        self._snap = None                # (version, state_f, state_i) of the last snapshot()
         self._tables = None
         # spaces (envs/base.py:139-148)
         self.observation_space = make_box(-1000.0, 1000.0, shape=(self.obs_dim,), dtype=np.float32)
@@ -122,7 +127,12 @@ class BatchedCrazyflieEnv:
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        if mask is not None and self._obs_latest is not None and self._obs_latest is not self.obs:
+            # a masked reset writes only the reset envs' rows: the others must already be in self.obs
+            self.obs.copy_(self._obs_latest)
         _native.check(self.lib.cf2_reset(self._ctx, _native.ptr(m), self.obs.data_ptr(), self.stream), "cf2_reset")
+        self._state_version += 1
+        self._obs_latest = self.obs
         return self.obs
 
     def step(self, actions: torch.Tensor, dstb: torch.Tensor | None = None):
@@ -146,6 +156,8 @@ class BatchedCrazyflieEnv:
             self._ctx, a.data_ptr(), _native.ptr(d), self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
             self.trunc.data_ptr(), self.cost.data_ptr(), self.level.data_ptr(), _native.ptr(self.final_obs),
             self.stream), "cf2_step")
+        self._state_version += 1
+        self._obs_latest = self.obs
         info = {"cost": self.cost, "truncated": self.trunc, "disturbance_level": self.level}
         if self.final_obs is not None:
             info["final_obs"] = self.final_obs
@@ -169,6 +181,8 @@ class BatchedCrazyflieEnv:
         _native.check(self.lib.cf2_step(
             self._ctx, actions.data_ptr(), None, obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
             _native.ptr(trunc_out), _native.ptr(cost_out), None, _native.ptr(final_obs_out), self.stream), "cf2_step")
+        self._state_version += 1
+        self._obs_latest = obs_out
 
     def rollout(self, actions: torch.Tensor, obs_out: torch.Tensor | None = None, rew_out=None, done_out=None,
                 trunc_out=None, cost_out=None, level_out=None, final_obs_out=None):
@@ -200,6 +214,8 @@ class BatchedCrazyflieEnv:
             self._ctx, K, actions.data_ptr(), n * 4, obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
             trunc_out.data_ptr(), cost_out.data_ptr(), level_out.data_ptr(), _native.ptr(final_obs_out), self.stream),
             "cf2_rollout")
+        self._state_version += 1
+        self._obs_latest = obs_out[K - 1]
         info = {"cost": cost_out, "truncated": trunc_out, "disturbance_level": level_out}
         if final_obs_out is not None:
             info["final_obs"] = final_obs_out
@@ -209,7 +225,10 @@ class BatchedCrazyflieEnv:
         """Launch one env-step with a raw device pointer to [N, 4] float32 actions (benchmark /
         graph-capture helper; the pointer is not checked).  full_info: also write the truncation,
         cost and level outputs step() returns in info (the reference's compute_info runs every step,
-        envs/hover_free.py:138-166)."""
+        envs/hover_free.py:138-166).  With obs_ptr the observations go to that raw buffer, which
+        save_checkpoint cannot see: pass it the observations explicitly."""
+        self._obs_latest = self.obs if obs_ptr is None else None
+        self._state_version += 1
         _native.check(self.lib.cf2_step(
             self._ctx, act_ptr, None, obs_ptr or self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
             self.trunc.data_ptr() if full_info else None, self.cost.data_ptr() if full_info else None,
@@ -228,18 +247,38 @@ class BatchedCrazyflieEnv:
         if sf.shape != (self.layout.num_float_fields, self.num_envs) or si.shape != (self.layout.num_int_fields, self.num_envs):
             raise ValueError("state tensors do not match cf2_layout")
         _native.check(self.lib.cf2_set_state(self._ctx, sf.data_ptr(), si.data_ptr(), self.stream), "cf2_set_state")
+        self._state_version += 1
+
+    def snapshot(self):
+        """get_state(), cached until the next call that changes the state (step, reset, rollout,
+        set_state, a physics-plugin step): repeated reads of agent attributes between two steps
+        cost one conversion kernel, not one each.  The tensors are shared: do not modify them."""
+        if self._snap is None or self._snap[0] != self._state_version:
+            sf, si = self.get_state()
+            self._snap = (self._state_version, sf, si)
+        return self._snap[1], self._snap[2]
 
     # ---- checkpoint / resume (the reference never checkpoints env state, SURVEY section 5) ----
-    def save_checkpoint(self, path: str):
+    def save_checkpoint(self, path: str, obs: torch.Tensor | None = None):
         """Write the whole batch to a safetensors file: the state snapshot, the current
         observations and the raw cf2_config (seed, offsets and every constant), so that
         ``from_checkpoint`` resumes bit-identically (every draw is keyed by the seed, the global
-        env id and the per-env counter in the snapshot).  Bound HJ tables are not saved."""
+        env id and the per-env counter in the snapshot).  Bound HJ tables are not saved.
+
+        The observations saved are those of the latest reset / step / step_into / rollout call
+        (for step_into and rollout: the caller's buffer, read now, so it must still hold them), or
+        ``obs`` if given ([N, obs_dim]; required after step_raw with a raw obs pointer)."""
         from safetensors.torch import save_file
+        cur = obs if obs is not None else self._obs_latest
+        if cur is None:
+            raise ValueError("the latest observations went to a raw buffer (step_raw obs_ptr): pass obs=")
+        if tuple(cur.shape) != (self.num_envs, self.obs_dim):
+            raise ValueError(f"obs must be [{self.num_envs}, {self.obs_dim}]")
         sf, si = self.get_state()
         torch.cuda.synchronize(self.device)
         cfg = torch.frombuffer(bytearray(bytes(self.cfg)), dtype=torch.uint8)
-        save_file({"state_f": sf.cpu(), "state_i": si.cpu(), "obs": self.obs.cpu(), "config": cfg}, path,
+        save_file({"state_f": sf.cpu(), "state_i": si.cpu(), "obs": cur.detach().float().cpu().contiguous(),
+                   "config": cfg}, path,
                   metadata={"env_id": self.env_id, "abi_version": str(self.lib.cf2_abi_version()),
                             "want_final_obs": str(int(self.want_final_obs))})
 
@@ -257,6 +296,7 @@ class BatchedCrazyflieEnv:
             raise ValueError("checkpoint configuration differs from this env's")
         self.set_state(t["state_f"], t["state_i"])
         self.obs.copy_(t["obs"].to(self.device))
+        self._obs_latest = self.obs
 
     @classmethod
     def from_checkpoint(cls, path: str, device=None) -> "BatchedCrazyflieEnv":
@@ -273,19 +313,20 @@ class BatchedCrazyflieEnv:
         env.load_checkpoint(path)
         return env
 
-    def gather_observations(self, group=None) -> torch.Tensor:
+    def gather_observations(self, group=None, out: torch.Tensor | None = None) -> torch.Tensor:
         """RCCL all-gather of every rank's obs slab (optional policy-side exchange; the physics
-        itself needs no collective).  Returns [sum of N over ranks, obs_dim] in rank order."""
+        itself needs no collective).  Returns [sum of N over ranks, obs_dim] in rank order: a fresh
+        tensor per call, or ``out`` when given (opt-in buffer reuse: the next call with the same
+        ``out`` overwrites it).  The observations gathered are the latest step's or reset's."""
         from .dist import exchange_sizes, gather_rows
         key = id(group)
         if getattr(self, "_gather_key", None) != key:   # shard sizes: exchanged once per group
             self._gather_sizes = exchange_sizes(self.num_envs, group)
-            self._gather_out = None
             self._gather_key = key
-        out = gather_rows(self.obs, group, sizes=self._gather_sizes, out=self._gather_out)
-        if len(set(self._gather_sizes)) == 1:
-            self._gather_out = out                        # reused by the next call
-        return out
+        src = self._obs_latest if self._obs_latest is not None else self.obs
+        if out is not None:
+            _check_buf(out, "out", (sum(self._gather_sizes), self.obs_dim), torch.float32, self.device)
+        return gather_rows(src, group, sizes=self._gather_sizes, out=out)
 
 
 def hj_disturbance(V: torch.Tensor, states: torch.Tensor, level: float, cfg: CF2Config | None = None):

@@ -249,25 +249,44 @@ int cf2_layout_get(const cf2_ctx* ctx, cf2_layout* o) {
 int cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables, const int32_t* table_of_level) {
     if (!ctx || !V_dev || num_tables <= 0 || !table_of_level) return CF2_ERR_INVALID_ARG;
     for (int l = 0; l < ctx->cfg.num_levels; ++l)
-        if (table_of_level[l] >= num_tables) return CF2_ERR_INVALID_ARG;
-    for (int l = 0; l < ctx->cfg.num_levels; ++l) ctx->T.table_of_level[l] = table_of_level[l];
-    hipError_t e = hipMemcpy(ctx->tab_dev, &ctx->T, sizeof(KTables), hipMemcpyHostToDevice);
+        if (table_of_level[l] < -1 || table_of_level[l] >= num_tables) return CF2_ERR_INVALID_ARG;
+    // the sign-table kernel indexes nodes in 32 bits
+    if ((uint64_t)num_tables * (uint64_t)HJ_TABLE > (uint64_t)UINT32_MAX) return CF2_ERR_INVALID_ARG;
+    // V may have been written on any stream of the caller (torch side streams do not synchronise
+    // with the null stream), and step kernels still in flight may read the current tables and
+    // bits: a binding is a setup-time call, so it waits for all device work first
+    hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) return hip_fail(e);
     // Derived per-node sign bits (distur_gener's rule over the 7 taps around each node): the
     // env-step gathers one byte per env instead of 7 floats.  Derived once per binding: rebind
-    // after changing the table contents.
+    // after changing the table contents.  Derived into a new buffer when the old one is too
+    // small; nothing of the context changes until the derivation succeeded.
     const size_t need = (size_t)num_tables * (size_t)HJ_TABLE;
-    if (need > ctx->hj_bits_bytes) {
-        if (ctx->hj_bits) (void)hipFree(ctx->hj_bits);
-        ctx->hj_bits = nullptr;
-        ctx->hj_bits_bytes = 0;
-        e = hipMalloc(&ctx->hj_bits, need);
+    uint8_t* bits = ctx->hj_bits;
+    const bool fresh = need > ctx->hj_bits_bytes;
+    if (fresh) {
+        e = hipMalloc(&bits, need);
         if (e != hipSuccess) return hip_fail(e);
+    }
+    e = launch_hj_sign_table(V_dev, (uint32_t)num_tables, bits, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    KTables T = ctx->T;
+    for (int l = 0; l < ctx->cfg.num_levels; ++l) T.table_of_level[l] = table_of_level[l];
+    if (e == hipSuccess) e = hipMemcpy(ctx->tab_dev, &T, sizeof(KTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (fresh) (void)hipFree(bits);
+        else {   // the old buffer was partly overwritten: the context has no valid tables now
+            ctx->P.V = nullptr;
+            ctx->P.hj_bits = nullptr;
+        }
+        return hip_fail(e);
+    }
+    if (fresh) {
+        if (ctx->hj_bits) (void)hipFree(ctx->hj_bits);
+        ctx->hj_bits = bits;
         ctx->hj_bits_bytes = need;
     }
-    e = launch_hj_sign_table(V_dev, (uint32_t)num_tables, ctx->hj_bits, nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-    if (e != hipSuccess) return hip_fail(e);
+    ctx->T = T;
     ctx->P.V = V_dev;
     ctx->P.hj_bits = ctx->hj_bits;
     return CF2_OK;
@@ -315,6 +334,7 @@ int cf2_rollout(cf2_ctx* ctx, int K, const float* act_dev, size_t act_stride_ele
     if (!ctx || K < 1 || !act_dev || !obs_dev || !rew_dev || !done_dev) return CF2_ERR_INVALID_ARG;
     const size_t n = ctx->cfg.num_envs;
     if (K > 1 && act_stride_elems < n * 4) return CF2_ERR_INVALID_ARG;
+    if (act_stride_elems > (size_t)UINT32_MAX) return CF2_ERR_INVALID_ARG;   // the kernel strides in 32 bits
     if ((act_stride_elems & 3u) != 0 || ((uintptr_t)act_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
     if (((uintptr_t)obs_dev & 7u) != 0 || (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0))
         return CF2_ERR_INVALID_ARG;

@@ -1,8 +1,9 @@
 // cf2sim_kernels.hip -- fused CDNA4 (gfx950) env-step / reset kernels for the batched
 // CrazyFlie hover environment.
 //
-// One lane = one env.  Env state is structure-of-arrays in HBM (field-major, DESIGN.md
-// "State layout"), so every field load/store of a wave is one contiguous 256-B transaction.
+// One lane = one env.  Env state is AoSoA in HBM: tiles of 64 envs (one wave), each env's 480 B
+// as 30 float4 groups, group g of lane l at tile_base + g * 1024 + l * 16 (cf2sim_internal.h,
+// DESIGN.md section 2), so every state access of a wave is one coalesced 1-KB dwordx4 transaction.
 // A step loads the state once, runs aggregate_phy_steps physics sub-steps plus the
 // observation / history / reward / done epilogue (and the auto-reset of finished envs) in
 // registers, and stores the state once: the kernel is HBM-bound by construction (no MFMA:

@@ -205,7 +205,11 @@ int  cf2_layout_get(const cf2_ctx* ctx, cf2_layout* out);
  * Binding derives, once, the disturbance sign bits of every grid node (the distur_gener rule over
  * the node's 7 value taps, distur_gener.py:155-183; 1 byte per node, 11.4 MB per table, owned by
  * the ctx): the env-step gathers one byte per env.  Rebind after changing the table contents.
- * Synchronous. */
+ * Synchronous and device-wide: waits for all work on the device first (V_dev may have been
+ * written on any stream; steps in flight may still read the previous tables), then derives the
+ * bits.  On failure the ctx keeps its previous binding, or has none (CF2_ERR_NO_TABLE on the
+ * next HJ step) if the previous bits were already overwritten.  num_tables * 15^6 must fit in
+ * 32 bits (at most 377 tables). */
 int  cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables,
                         const int32_t* table_of_level /* host, num_levels entries */);
 

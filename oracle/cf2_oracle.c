@@ -32,8 +32,9 @@
 #endif
 #define R(x) ((REAL)(x))
 
+/* libm of the REAL type: R_SQRT is the square root (not a reciprocal square root), RSIN sin, ... */
 #if defined(ORACLE_F32)
-#define RSQRT sqrtf
+#define R_SQRT sqrtf
 #define RSIN sinf
 #define RCOS cosf
 #define RLOG logf
@@ -42,7 +43,7 @@
 #define RFABS fabsf
 #define REXP expf
 #else
-#define RSQRT sqrt
+#define R_SQRT sqrt
 #define RSIN sin
 #define RCOS cos
 #define RLOG log
@@ -83,7 +84,7 @@ static REAL u01(uint32_t x) { return (REAL)(x >> 8) * R(5.9604644775390625e-08);
 static void box_muller(uint32_t a, uint32_t b, REAL* z0, REAL* z1) {
     REAL u1 = ((REAL)(a >> 8) + R(1.0)) * R(5.9604644775390625e-08); /* (0,1] */
     REAL u2 = (REAL)(b >> 8) * R(5.9604644775390625e-08);
-    REAL r = RSQRT(R(-2.0) * RLOG(u1));
+    REAL r = R_SQRT(R(-2.0) * RLOG(u1));
     REAL th = R(6.283185307179586) * u2;
     *z0 = r * RCOS(th);
     *z1 = r * RSIN(th);
@@ -125,7 +126,7 @@ void orc_quat_from_euler(const REAL rpy[3], REAL q[4]) {
     REAL y = cp * st * cs + sp * ct * ss;
     REAL z = cp * ct * ss - sp * st * cs;
     REAL w = cp * ct * cs + sp * st * ss;
-    REAL len = RSQRT(x * x + y * y + z * z + w * w);
+    REAL len = R_SQRT(x * x + y * y + z * z + w * w);
     q[0] = x / len; q[1] = y / len; q[2] = z / len; q[3] = w / len;
 }
 /* pybullet getEulerFromQuaternion (agents.py:446 readback) */
@@ -166,7 +167,7 @@ static void matTvec(const REAL M[9], const REAL v[3], REAL o[3]) {
     o[1] = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
     o[2] = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
 }
-static REAL norm3(const REAL v[3]) { return RSQRT(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+static REAL norm3(const REAL v[3]) { return R_SQRT(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
 static REAL clampr(REAL x, REAL lo, REAL hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 /* ------------------------------------------------------------------------------------ */
@@ -296,7 +297,7 @@ static void apply_action(const orc_ctx* X, orc_env* E, const REAL a[4], const RE
         REAL tn = pwm[j] / R(60000.0);
         REAL noisy;
         if (c->use_motor_dynamics) {
-            REAL rot = RSQRT(tn);
+            REAL rot = R_SQRT(tn);
 #ifdef ORACLE_F32
             /* the HIP kernel's form: x += B (rot - x) with x kept as an unevaluated pair x + xl
              * (TwoSum), so the 5 ms recurrence does not accumulate fp32 rounding.  Equal to
@@ -467,7 +468,7 @@ static void bullet_substep(const orc_ctx* X, orc_env* E, const REAL a[4], const 
         REAL ny = cw * qy + axs[1] * qw + axs[2] * qx - axs[0] * qz;
         REAL nz = cw * qz + axs[2] * qw + axs[0] * qy - axs[1] * qx;
         REAL nw = cw * qw - axs[0] * qx - axs[1] * qy - axs[2] * qz;
-        REAL len = RSQRT(nx * nx + ny * ny + nz * nz + nw * nw);
+        REAL len = R_SQRT(nx * nx + ny * ny + nz * nz + nw * nw);
         E->q[0] = nx / len; E->q[1] = ny / len; E->q[2] = nz / len; E->q[3] = nw / len;
     }
     update_information(E);
@@ -484,8 +485,8 @@ static void simple_substep(const orc_ctx* X, orc_env* E, const REAL a[4], const 
     REAL g = R(c->gravity_world);
     REAL Fw[3] = {Rm[2] * fsum - R(0.0) * E->m, Rm[5] * fsum - R(0.0) * E->m, Rm[8] * fsum - g * E->m};
     /* (..) * self.drone.L / np.sqrt(2), evaluated left to right */
-    REAL tx = (-f[0] - f[1] + f[2] + f[3]) * R(c->arm) / RSQRT(R(2.0));
-    REAL ty = (-f[0] + f[1] + f[2] - f[3]) * R(c->arm) / RSQRT(R(2.0));
+    REAL tx = (-f[0] - f[1] + f[2] + f[3]) * R(c->arm) / R_SQRT(R(2.0));
+    REAL ty = (-f[0] + f[1] + f[2] - f[3]) * R(c->arm) / R_SQRT(R(2.0));
     REAL* w = E->wb;
     REAL Jw[3] = {E->J[0] * w[0], E->J[1] * w[1], E->J[2] * w[2]};
     REAL cr[3] = {w[1] * Jw[2] - w[2] * Jw[1], w[2] * Jw[0] - w[0] * Jw[2], w[0] * Jw[1] - w[1] * Jw[0]};
@@ -580,8 +581,8 @@ static int compute_done(const cf2_config* c, const orc_env* E) {
 static REAL compute_reward(const cf2_config* c, const orc_env* E, const REAL a[4], int done) {
     REAL na[4], ad[4];
     for (int k = 0; k < 4; ++k) { na[k] = R(0.5) * (clampr(a[k], R(-1.0), R(1.0)) + R(1.0)); ad[k] = a[k] - E->last_action[k]; }
-    REAL nna = RSQRT(na[0] * na[0] + na[1] * na[1] + na[2] * na[2] + na[3] * na[3]);
-    REAL nad = RSQRT(ad[0] * ad[0] + ad[1] * ad[1] + ad[2] * ad[2] + ad[3] * ad[3]);
+    REAL nna = R_SQRT(na[0] * na[0] + na[1] * na[1] + na[2] * na[2] + na[3] * na[3]);
+    REAL nad = R_SQRT(ad[0] * ad[0] + ad[1] * ad[1] + ad[2] * ad[2] + ad[3] * ad[3]);
     REAL dr[3], dw[3], dp[3];
     for (int k = 0; k < 3; ++k) {
         dr[k] = E->rpy[k] - R(c->target_rpy[k]);
@@ -669,7 +670,7 @@ REAL orc_downwash(const cf2_config* c, const REAL pn[3], const REAL (*pos)[3], i
         if (j == self) continue;
         const REAL dz = pos[j][2] - pn[2];
         const REAL dx = pos[j][0] - pn[0], dy = pos[j][1] - pn[1];
-        const REAL dxy = RSQRT(dx * dx + dy * dy);
+        const REAL dxy = R_SQRT(dx * dx + dy * dy);
         if (dz > R(0.0) && dxy < R(10.0)) {
             const REAL rr = R(c->prop_radius) / (R(4.0) * dz);
             const REAL alpha = R(c->dw_coeff[0]) * rr * rr;

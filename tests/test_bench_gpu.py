@@ -1,0 +1,106 @@
+"""bench.py's multi-rank measurement path on a GPU box.
+
+- `bench.py --gpus 2` without a launcher starts its own two ranks (CF2_BENCH_BACKEND=gloo: both
+  ranks share the one MI355X of the test box) on BASELINE's metric config, 262 144 envs over the
+  job, and prints one line with n_gpus = world_size = 2, the per-step observation all-gather on,
+  and the no-gather and weak-scaling keys.
+- Under torchrun with one rank and --gather-obs, the RCCL ("nccl") pipelined all-gather runs
+  (PipelinedObsGather on its side stream), the path the 8-GPU run takes.
+- PipelinedObsGather's output equals the observations the env-step wrote, step for step."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHORT = ["--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--rollout-k", "0", "--streaming-ring", "0",
+         "--oc-envs", "0", "--weak-steps", "20"]
+
+
+def _env():
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    return e
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_two_ranks(gpu):
+    env = dict(_env(), CF2_BENCH_BACKEND="gloo")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *SHORT], env=env,
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
+    assert d["config"]["global_envs"] == 262144 and d["config"]["envs_per_gpu"] == 131072
+    assert d["config"]["gather_obs"] is True and d["scaling"] == "strong"
+    assert d["value"] > 0 and d["no_gather"]["value"] > 0
+    assert d["weak_scaling"]["global_envs"] == 2 * 262144 and d["weak_scaling"]["value"] > 0
+    assert d["gather"]["total_bytes_per_step"] == 262144 * 34 * 4
+
+
+def test_bench_rccl_gather_path_one_rank(gpu):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--gather-obs",
+           "--global-envs", "32768", *SHORT]
+    p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    assert d["backend"] == "nccl" and d["world_size"] == 1 and d["config"]["gather_obs"] is True
+    assert d["gather"]["mode"].startswith("pipelined") and d["value"] > 0
+
+
+def _pipe_worker(rank, world, port, out):
+    sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+    import torch.distributed as dist
+    from cf2sim.dist import PipelinedObsGather
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    n = 4096
+    env = BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithGust-v0", n, seed=3, device="cuda:0")
+    ref = BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithGust-v0", n, seed=3, device="cuda:0")
+    env.reset()
+    ref.reset()
+    pipe = PipelinedObsGather(n, env.obs_dim, torch.device("cuda", 0), depth=2)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(5)
+    outs, refs = [], []
+    for k in range(12):
+        a = torch.rand(n, 4, device="cuda:0", generator=g) * 2 - 1
+        buf = pipe.buffer()
+        env.step_raw(a.data_ptr(), obs_ptr=buf.data_ptr())
+        o = pipe.publish()
+        ref.step(a)
+        refs.append(ref.obs.clone())
+        if k % 2:
+            pipe.drain()
+            outs.append((k, o.clone()))
+    pipe.drain()
+    torch.cuda.synchronize()
+    ok = all(torch.equal(o, refs[k]) for k, o in outs)
+    with open(out, "w") as f:
+        f.write("ok" if ok else "mismatch")
+    dist.destroy_process_group()
+
+
+def test_pipelined_gather_matches_env_obs(gpu, tmp_path):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "res.txt")
+    mp.spawn(_pipe_worker, args=(1, _port(), out), nprocs=1, join=True)
+    assert open(out).read() == "ok"

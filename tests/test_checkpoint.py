@@ -44,3 +44,44 @@ def test_resume_from_checkpoint_is_bit_identical(gpu, tmp_path, env_id):
         other.load_checkpoint(path)
     for e in (a_env, b_env, other):
         e.close()
+
+
+@pytest.mark.parametrize("path_kind", ["rollout", "step_into"])
+def test_checkpoint_after_rollout_or_step_into_resumes(gpu, tmp_path, path_kind):
+    """rollout() and step_into() write the observations into caller buffers; the checkpoint then
+    saves those (the latest step's), not the env's own obs buffer, and a resumed batch continues
+    bit-identically (self.obs used to be stale there)."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env_id, n = "DroneHoverBulletFreeEnvWithGust-v0", 2048
+    a_env = BatchedCrazyflieEnv(env_id, n, seed=4)
+    a_env.reset()
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(3)
+    acts = (torch.rand(16, n, 4, device="cuda", generator=gen) * 2 - 1).contiguous()
+    if path_kind == "rollout":
+        obs, _, _, _ = a_env.rollout(acts[:8])
+        latest = obs[7].clone()
+    else:
+        ob = torch.empty(n, a_env.obs_dim, device="cuda")
+        rw = torch.empty(n, device="cuda")
+        dn = torch.empty(n, dtype=torch.uint8, device="cuda")
+        for t in range(8):
+            a_env.step_into(acts[t], ob, rw, dn)
+        latest = ob.clone()
+    path = str(tmp_path / "b.safetensors")
+    a_env.save_checkpoint(path)
+    b_env = BatchedCrazyflieEnv.from_checkpoint(path)
+    np.testing.assert_array_equal(b_env.obs.cpu().numpy(), latest.cpu().numpy())
+    for t in range(8, 16):
+        oa, ra, da, _ = a_env.step(acts[t])
+        ob2, rb, db, _ = b_env.step(acts[t])
+        np.testing.assert_array_equal(ob2.cpu().numpy(), oa.cpu().numpy())
+        np.testing.assert_array_equal(rb.cpu().numpy(), ra.cpu().numpy())
+    # observations sent to a raw pointer: the checkpoint needs them explicitly
+    raw = torch.empty(n, a_env.obs_dim, device="cuda")
+    a_env.step_raw(acts[0].data_ptr(), obs_ptr=raw.data_ptr())
+    with pytest.raises(ValueError, match="obs="):
+        a_env.save_checkpoint(path)
+    a_env.save_checkpoint(path, obs=raw)
+    for e in (a_env, b_env):
+        e.close()

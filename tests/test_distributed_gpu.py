@@ -44,12 +44,20 @@ def _worker(rank, world, port, out_dir, n_total):
     env.reset()
     obs = [env.gather_observations().cpu()]
     rew, done = [], []
+    kept = []
     for t in range(T):
         a = torch.from_numpy(_actions(t, n_total)[off:off + cnt]).cuda()
         o, r, d, _ = env.step(a)
-        obs.append(env.gather_observations().cpu())
+        gobs = env.gather_observations()
+        kept.append(gobs)                       # fresh tensor per call: earlier results stay intact
+        obs.append(gobs.cpu())
         rew.append(gather_rows(r).cpu())
         done.append(gather_rows(d).cpu())
+    for t in range(T):
+        assert torch.equal(kept[t].cpu(), obs[t + 1]), "gather_observations aliased an earlier result"
+    assert not torch.equal(kept[0], kept[-1])
+    buf = torch.empty_like(kept[0])
+    assert env.gather_observations(out=buf) is buf         # opt-in reuse
     env.close()
     if rank == 0:
         np.savez(os.path.join(out_dir, "dist.npz"), obs=torch.stack(obs).numpy(), rew=torch.stack(rew).numpy(),

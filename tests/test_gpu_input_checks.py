@@ -66,3 +66,62 @@ def test_boltzmann_env_needs_one_table_per_level(gpu):
     env.step(torch.zeros(64, 4, device=gpu))
     torch.cuda.synchronize()
     env.close()
+
+
+def _tables(t, gpu):
+    ax = torch.linspace(-1.0, 1.0, 15, device=gpu)
+    g = [ax.view([-1 if i == d else 1 for i in range(6)]) for d in range(6)]
+    return torch.stack([sum((0.3 + 0.1 * k + 0.05 * d) * g[d] ** (1 + (d + k) % 2) for d in range(6))
+                        + 0.1 * torch.sin(3 * g[3] + 2 * g[4] - g[5] + k) for k in range(t)]).reshape(t, -1)
+
+
+def test_bind_tables_written_on_a_side_stream(gpu):
+    """cf2_bind_hj_tables derives the sign bits from V after all device work (it used to
+    run on the null stream, unordered with a torch side stream still writing V).  V is produced on a
+    side stream behind a long queue of work and bound without any host synchronisation; the env
+    then steps exactly like one bound to a V that was complete before binding."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env_id, n = "DroneHoverBulletFreeEnvWithAdversary-v0", 2048
+    ref_V = _tables(1, gpu)
+    torch.cuda.synchronize()
+    ref = BatchedCrazyflieEnv(env_id, n, seed=5)
+    ref.bind_hj_tables(ref_V)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        V = torch.zeros(1, 15 ** 6, device=gpu)
+        x = torch.randn(2048, 2048, device=gpu)
+        for _ in range(40):                        # keep the side stream busy before V is written
+            x = torch.tanh(x @ x * 1e-3)
+        V.copy_(ref_V + 0.0 * x[0, 0])
+    env = BatchedCrazyflieEnv(env_id, n, seed=5)
+    env.bind_hj_tables(V)                          # no synchronisation with `side` by the caller
+    torch.cuda.current_stream().wait_stream(side)
+    env.reset()
+    ref.reset()
+    gen = torch.Generator(device=gpu)
+    gen.manual_seed(1)
+    for _ in range(20):
+        a = torch.rand(n, 4, device=gpu, generator=gen) * 0.3
+        o1, r1, _, _ = env.step(a)
+        o2, r2, _, _ = ref.step(a)
+        assert torch.equal(o1, o2) and torch.equal(r1, r2)
+    env.close()
+    ref.close()
+
+
+def test_rebinding_tables(gpu):
+    """Rebinding grows the sign-bit buffer when more tables are bound; a rejected binding (a level
+    mapped past the bound tables) leaves the previous one in place."""
+    from cf2sim import _native
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env = BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", 512, seed=2)
+    nl = int(env.cfg.num_levels)
+    env.bind_hj_tables(_tables(1, gpu), table_of_level=[0] * nl)
+    env.bind_hj_tables(_tables(3, gpu), table_of_level=[k % 3 for k in range(nl)])   # larger: new buffer
+    env.reset()
+    env.step(torch.zeros(512, 4, device=gpu))
+    with pytest.raises(_native.CF2Error):
+        env.bind_hj_tables(_tables(2, gpu), table_of_level=[2] * nl)    # row 2 of 2 tables
+    env.step(torch.zeros(512, 4, device=gpu))                            # previous binding still valid
+    torch.cuda.synchronize()
+    env.close()

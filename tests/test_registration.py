@@ -98,3 +98,32 @@ def test_make_matches_restatement_and_time_limit(gpu):
         env.step(a)
     env.close()
     ref.close()
+
+
+@pytest.mark.gpu
+def test_make_step_cost_is_recorded(gpu):
+    """The single-env adapter's per-step cost (the reference's batch-1 callers, algs/iwpg/iwpg.py:380,
+    go through it): one kernel, one state snapshot and ONE device->host transfer per step.  The
+    figure is written to gpurun_out/make_step_us.json (DESIGN.md quotes it)."""
+    import json
+    import os
+    import time
+    env = R.make("DroneHoverBulletFreeEnvWithoutAdversary-v0", seed=3)
+    env.reset()
+    a = np.full(4, 0.1111, dtype=np.float32)
+    for _ in range(20):
+        _, _, d, _ = env.step(a)
+        if d:
+            env.reset()
+    n, t0 = 300, time.perf_counter()
+    for _ in range(n):
+        _, _, d, _ = env.step(a)
+        if d:
+            env.reset()
+    us = (time.perf_counter() - t0) / n * 1e6
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "make_step_us.json"), "w") as f:
+        json.dump({"us_per_make_step": us, "steps": n}, f)
+    env.close()
+    assert us < 2000.0, f"{us:.0f} us per make().step()"

@@ -7,6 +7,7 @@ WRITE_SIZE (KiB) into bytes.  Writes profiles/step_kernel_traffic.json for bench
 import csv, glob, json, os, sys
 
 out = sys.argv[1]
+N_STEP = int(sys.argv[2]) if len(sys.argv) > 2 else 262144      # envs of the profiled bench run
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -43,7 +44,7 @@ s_f = mean_counter(os.path.join(out, "step_FETCH_SIZE"), "FETCH_SIZE", "step_ker
 s_w = mean_counter(os.path.join(out, "step_WRITE_SIZE"), "WRITE_SIZE", "step_kernel") * 1024
 kr, kw = calib_rd / c_f, calib_wr / c_w
 res = {
-    "workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}",
+    "workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N_STEP}",
     "hbm_bytes_per_launch": s_f * kr + s_w * kw,
     "read_bytes_per_launch": s_f * kr,
     "write_bytes_per_launch": s_w * kw,
@@ -55,5 +56,13 @@ res = {
     "note": "FETCH_SIZE/WRITE_SIZE count L2 memory-side requests; Infinity-Cache hits are counted "
             "(MI355X_MICROARCH.md HBM section), so this is L2->fabric traffic.",
 }
-json.dump(res, open(os.path.join(out, "step_kernel_traffic.json"), "w"), indent=1)
+# merged into profiles/step_kernel_traffic.json by workload (one entry per measured env count)
+prof = os.path.join(ROOT, "profiles", "step_kernel_traffic.json")
+try:
+    old = json.load(open(prof))
+    entries = old.get("entries", [old])
+except (OSError, ValueError):
+    entries = []
+entries = [e for e in entries if e.get("workload") != res["workload"]] + [res]
+json.dump({"entries": entries}, open(os.path.join(out, "step_kernel_traffic.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
