@@ -808,6 +808,46 @@ __device__ __forceinline__ void omega_noise(const KParams& P, Env& E, const floa
     for (int k = 0; k < 3; ++k) om[k] = E.wb[k] + E.bias[k] + P.gyro_rw * n[3 + k] + P.gyro_ton * n[6 + k];
 }
 
+// A full measurement's held part (noisy position, attitude quaternion and velocity,
+// sensors.py:75-118) and its 9 gyro normals n[6..15) (bias walk, white noise, turn-on noise): what
+// the measurement draws from stream blocks base..base+5.  The gyro part is applied by
+// gyro_update, which needs the body rates, bias and LPF state of the moment.
+template <class G>
+__device__ __forceinline__ void held_measurement(const KParams& P, const Env& E, const G& g, uint32_t base,
+                                                 float held[10], float ng[9]) {
+    float n[18];
+    normals<18>(g, base, n);
+    const U4 ua = g.block(base + 4), ub = g.block(base + 5);
+    const uint32_t up[3] = {ua.z, ua.w, ub.x}, ur[3] = {ub.y, ub.z, ub.w};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float uo = -P.pos_unif + (P.pos_unif - -P.pos_unif) * u01(up[k]);
+        held[k] = E.p[k] + (P.pos_std * n[k] + uo);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) held[7 + k] = E.v[k] + P.vel_std * n[3 + k] + 0.0f;
+    const float lo[3] = {-3.141592653589793f, -1.5707963267948966f, -3.141592653589793f};
+    float rot[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float uo = -P.rot_unif + (P.rot_unif - -P.rot_unif) * u01(ur[k]);
+        const float th = P.rot_std * n[15 + k] + uo;
+        rot[k] = clampf(E.rpy[k] + th, lo[k], -lo[k]);
+    }
+    quat_from_euler_obs(rot, held + 3);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) ng[k] = n[6 + k];
+}
+
+// gyro of one sensor call: bias walk + noise on the body rates, then the gyro low-pass filter
+// (sensors.py:121-134, utils.py:102-105); ng = the call's 9 gyro normals
+__device__ __forceinline__ void gyro_update(const KParams& P, Env& E, const float ng[9]) {
+    float om[3];
+    omega_noise(P, E, ng, om);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) E.lpf[k] = (1.0f - P.lpf_ratio) * E.lpf[k] + P.lpf_gain * P.lpf_ratio * om[k];
+}
+
 // need_held = false: the held measurement of this call is dead (it is overwritten by a later
 // full measurement before any observation is emitted), so a full measurement only advances the
 // gyro (bias walk + LPF) and draws just the gyro normals n[6..15) of its stream positions.
@@ -827,48 +867,22 @@ __device__ __forceinline__ void compute_observation(const KParams& P, Env& E, co
         for (int k = 0; k < 4; ++k) obs[13 + k] = E.la[k];
         return;
     }
-    float om[3];
     const bool full = (uint32_t)iteration % (uint32_t)P.obs_rate == 0u;
     if (full && !need_held) {
         float n[18];
         normals_range<6, 15>(g, base, n);
-        omega_noise(P, E, n + 6, om);
+        gyro_update(P, E, n + 6);
     } else if (full) {
-        float n[18];
-        normals<18>(g, base, n);
-        const U4 ua = g.block(base + 4), ub = g.block(base + 5);
-        const uint32_t up[3] = {ua.z, ua.w, ub.x}, ur[3] = {ub.y, ub.z, ub.w};
-        float pos[3], vel[3], rot[3];
+        float held[10], ng[9];
+        held_measurement(P, E, g, base, held, ng);
+        gyro_update(P, E, ng);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float uo = -P.pos_unif + (P.pos_unif - -P.pos_unif) * u01(up[k]);
-            pos[k] = E.p[k] + (P.pos_std * n[k] + uo);
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) vel[k] = E.v[k] + P.vel_std * n[3 + k] + 0.0f;
-        omega_noise(P, E, n + 6, om);
-        const float lo[3] = {-3.141592653589793f, -1.5707963267948966f, -3.141592653589793f};
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float uo = -P.rot_unif + (P.rot_unif - -P.rot_unif) * u01(ur[k]);
-            const float th = P.rot_std * n[15 + k] + uo;
-            rot[k] = clampf(E.rpy[k] + th, lo[k], -lo[k]);
-        }
-        float qn[4];
-        quat_from_euler_obs(rot, qn);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.held[k] = pos[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) E.held[3 + k] = qn[k];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) E.held[7 + k] = vel[k];
+        for (int k = 0; k < 10; ++k) E.held[k] = held[k];
     } else {
         float n[9];
         normals<9>(g, base, n);
-        omega_noise(P, E, n, om);
+        gyro_update(P, E, n);
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) E.lpf[k] = (1.0f - P.lpf_ratio) * E.lpf[k] + P.lpf_gain * P.lpf_ratio * om[k];
 #pragma unroll
     for (int k = 0; k < 10; ++k) obs[k] = E.held[k];
 #pragma unroll
@@ -1369,21 +1383,22 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     } else {
         compute_observation<NOISE>(P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
     }
-    // the physics state is final now (an auto-reset below overwrites it): store it early so
-    // its registers free up before the epilogue
-    if (STORE) store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
     const bool term = compute_done(P, E);
-    const float r = compute_reward(P, E, a, term);
-    const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
     E.ep_step += 1;
     const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
     const bool done = term || trunc;
+    const bool do_reset = done && P.auto_reset;
+    // the physics state is final now: store it early so its registers free up before the
+    // epilogue.  An env that auto-resets is not stored: its reset writes every group stored here
+    // (reset_role / the small-N reset roles), so no two waves store one group in one launch
+    if (STORE && !do_reset) store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
+    const float r = compute_reward(P, E, a, term);
+    const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
     io.rew[i] = r;
     io.done[i] = (uint8_t)done;
     if (io.trunc) io.trunc[i] = (uint8_t)trunc;
     if (io.cost) io.cost[i] = cost;
     if (io.level) io.level[i] = level_used;
-    const bool do_reset = done && P.auto_reset;
     {
         float o[OD];
         compute_history<NOISE>(P, E, onx, o);
@@ -1404,7 +1419,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         rs.ctr = E.rng;
     }
     E.rng += 1;
-    if (STORE) store_tail<NOISE>(P, io.sf, i, E);
+    if (STORE && !do_reset) store_tail<NOISE>(P, io.sf, i, E);
     TSTAMP(3);   // epilogue issued
     return do_reset;
 }
@@ -1480,13 +1495,60 @@ __device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict
     TSTAMP(8);   // reset stores issued
 }
 
+// The state groups an auto-reset writes, in three sets (their union is store_env(params_dirty)):
+//   kinematics: pose, velocities, counters (rng = ctr + 1), motor state, OU state (inherited from
+//               the finished episode), latency ring, rpy (Simple)       -> groups 0-6(+ring), 12, 28
+//   history:    gyro bias (+ gust_left 0), held measurement, action history, o_{k-1} + gyro LPF
+//                                                                        -> groups 10, 14-19, 21-23
+//   params:     domain randomisation, disturbance, level                -> groups 13, 24-27, 29
+template <int PHYS>
+__device__ __forceinline__ void store_reset_kinematics(const KParams& P, const Tile& T, const Env& E, const float ou[4],
+                                                       uint32_t ctr) {
+    T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
+    T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
+    T.st(2, f4(E.v[1], E.v[2], E.w[0], E.w[1]));
+    const int fl = (E.aidx & 15) | (1 << 4) | (1 << 5) | (E.la_view << 6) | (E.props_on << 7);   // halias0/1 = 1
+    T.st(G_CORE3, f4(E.w[2], ib(0), ib((int)(ctr + 1u)), ib(fl)));
+    T.st(G_MOTOR, f4(E.x[0], E.x[1], E.x[2], E.x[3]));
+    if (P.use_motor_dyn) T.st(G_MOTOR_LO, f4(0.0f, 0.0f, 0.0f, 0.0f));
+    T.st(G_OU, f4(ou[0], ou[1], ou[2], ou[3]));
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (r < P.buf_size) T.st(G_ABUF + r, f4(E.abuf[r][0], E.abuf[r][1], E.abuf[r][2], E.abuf[r][3]));
+    if (PHYS == PHYS_SIMPLE_T) T.st(G_RPY, f4(E.rpy[0], E.rpy[1], E.rpy[2], 0.0f));
+}
+template <bool NOISE>
+__device__ __forceinline__ void store_reset_history(const KParams& P, const Tile& T, const Env& E) {
+    if (NOISE || gust_mode(P))
+        T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(0)));
+    if (NOISE && P.held_persistent) {
+        T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
+        T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
+        T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
+    }
+    T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
+    T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
+    store_obs_prev<NOISE>(T, E);
+}
+template <bool DR>
+__device__ __forceinline__ void store_reset_params(const KParams& P, const Tile& T, const Env& E) {
+    if (dstb_stored(P)) T.st(G_DSTB, f4(E.dstb[0], E.dstb[1], E.dstb[2], 0.0f));
+    if (DR) {
+        T.st(G_PARAM, f4(E.dt, E.m, E.J[0], E.J[1]));
+        T.st(G_PARAM + 1, f4(E.J[2], E.k0, E.k1, E.B[0]));
+        T.st(G_PARAM + 2, f4(E.B[1], E.B[2], E.B[3], E.K[0]));
+    }
+    T.st(G_LEVEL, f4(E.K[1], E.K[2], E.K[3], E.level));
+    T.st(G_LEVEL_IDX, f4(ib(E.level_idx), 0.0f, 0.0f, 0.0f));
+}
+
 // One quarter of an auto-reset (block_epilogue runs the four roles on four waves at once; the
 // union of their stores is store_env(params_dirty) and of their row writes the reset
 // observation, as reset_env + store_env produce them):
-//   0: kinematics, motor state, ring           -> groups 0-6(+ring), 12 (Simple), 28
+//   0: kinematics, motor state, ring           -> store_reset_kinematics
 //   1: kinematics + the first sensor call      -> obs row o_0 | A_0
-//   2: kinematics + the second sensor call     -> obs row o_1 | A_1; groups 10, 14-19 (LPF in 19), 21-23
-//   3: domain randomisation, disturbance, level -> groups 13, 24-27, 29
+//   2: kinematics + the second sensor call     -> obs row o_1 | A_1; store_reset_history
+//   3: domain randomisation, disturbance, level -> store_reset_params
 // Roles 1 and 2 recompute the reset pose from the same table entries, so the critical path is one
 // pose + one sensor call instead of the whole reset.
 template <bool NOISE, bool DR, int PHYS>
@@ -1504,32 +1566,14 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
         E.level = rs.level;
         E.level_idx = rs.level_idx;
         reset_params<DR>(P, E, g);
-        if (dstb_stored(P)) T.st(G_DSTB, f4(E.dstb[0], E.dstb[1], E.dstb[2], 0.0f));
-        if (DR) {
-            T.st(G_PARAM, f4(E.dt, E.m, E.J[0], E.J[1]));
-            T.st(G_PARAM + 1, f4(E.J[2], E.k0, E.k1, E.B[0]));
-            T.st(G_PARAM + 2, f4(E.B[1], E.B[2], E.B[3], E.K[0]));
-        }
-        T.st(G_LEVEL, f4(E.K[1], E.K[2], E.K[3], E.level));
-        T.st(G_LEVEL_IDX, f4(ib(E.level_idx), 0.0f, 0.0f, 0.0f));
+        store_reset_params<DR>(P, T, E);
         return;
     }
     reset_kinematics<PHYS>(P, E, g, gid);
     TREADY("v"(E.q[3]), "v"(E.w[0]));
     TSTAMP(7);   // reset pose computed
     if (role == 0) {
-        T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
-        T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
-        T.st(2, f4(E.v[1], E.v[2], E.w[0], E.w[1]));
-        const int fl = (E.aidx & 15) | (1 << 4) | (1 << 5) | (E.la_view << 6) | (E.props_on << 7);   // halias0/1 = 1
-        T.st(G_CORE3, f4(E.w[2], ib(0), ib((int)(rs.ctr + 1u)), ib(fl)));
-        T.st(G_MOTOR, f4(E.x[0], E.x[1], E.x[2], E.x[3]));
-        if (P.use_motor_dyn) T.st(G_MOTOR_LO, f4(0.0f, 0.0f, 0.0f, 0.0f));
-        T.st(G_OU, f4(rs.ou[0], rs.ou[1], rs.ou[2], rs.ou[3]));
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (r < P.buf_size) T.st(G_ABUF + r, f4(E.abuf[r][0], E.abuf[r][1], E.abuf[r][2], E.abuf[r][3]));
-        if (PHYS == PHYS_SIMPLE_T) T.st(G_RPY, f4(E.rpy[0], E.rpy[1], E.rpy[2], 0.0f));
+        store_reset_kinematics<PHYS>(P, T, E, rs.ou, rs.ctr);
         return;
     }
     if (role == 1) {
@@ -1545,16 +1589,7 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
     for (int k = OL + 4; k < 2 * (OL + 4); ++k) obs_row[k] = o[k];
     TREADY("v"(o[2 * (OL + 4) - 1]));
     TSTAMP(8);   // role 2: second sensor call + history done
-    if (NOISE || gust_mode(P))
-        T.st(G_BIAS, f4(NOISE ? E.bias[0] : 0.0f, NOISE ? E.bias[1] : 0.0f, NOISE ? E.bias[2] : 0.0f, ib(0)));
-    if (NOISE && P.held_persistent) {
-        T.st(G_HELD, f4(E.held[0], E.held[1], E.held[2], E.held[3]));
-        T.st(G_HELD + 1, f4(E.held[4], E.held[5], E.held[6], E.held[7]));
-        T.st(G_HELD + 2, f4(E.held[8], E.held[9], 0.0f, 0.0f));
-    }
-    T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
-    T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
-    store_obs_prev<NOISE>(T, E);
+    store_reset_history<NOISE>(P, T, E);
 }
 
 // End of a block's env-step: list the finished envs (wave ballots into per-wave lists), reset
@@ -1747,6 +1782,164 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, EPB);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
+    if (uint64_t* r = timing_row())
+        if ((threadIdx.x & 63) == 0) r[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+// Block barrier for LDS hand-offs: the calling wave's LDS operations complete first; its global
+// stores keep draining (__syncthreads would also wait for those, vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Small N (<= 32 768 envs): the launch is as long as one wave's env-step chain, and the auto-reset
+// tail used to be ~40 % of it.  Each 256-thread block holds 64 envs.  Wave 0
+// steps them (issue priority 3).  Waves 1-3 meanwhile compute, speculatively for all 64 envs and at
+// priority 0, every part of a potential auto-reset that does not depend on the finished episode:
+// a reset's draws are keyed by the env's RNG counter, which is known when the state loads, so
+// they are the same Philox blocks the reset would draw after the step.
+//   wave 1 (A): reset pose, velocities, motor state, latency ring    (reset_kinematics)
+//   wave 2 (B): the pose again, the first reset sensor call's held measurement and gyro normals
+//   wave 3 (C): domain randomisation, disturbance, level (reset_params); the pose again and the
+//               second sensor call's held part and gyro normals, handed to B in LDS
+// After one LDS barrier only the finished envs' work remains, on their lanes of waves 1-3: the two
+// gyro updates, which need the finished episode's body rates (the gyro LPF seed) and gyro bias,
+// the reset observation row, and the reset's state stores (store_reset_*).  The env wave does not
+// store the state of envs that reset (step_env_body), so no group is stored twice.
+enum { SEED_SMALL = 10 };   // per finished env, wave 0 -> waves 1-3: final body rates, gyro bias, OU state
+enum { C2_WORDS = 19 };     // per env, wave 3 -> wave 2: the second call's held[10] and gyro normals[9]
+
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO io) {
+    const KParams P = shape_view<SPEC>(P0);
+    constexpr int OL = NOISE ? 13 : 17;
+    constexpr int OD = 2 * (OL + 4);
+    __shared__ __align__(16) float s_obs[64 * OD];         // the block's obs rows, global layout
+    __shared__ float s_seed[SEED_SMALL * 64];              // [word][env]
+    __shared__ float s_c2[C2_WORDS * 64];                  // [word][env]
+    __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+#ifdef CF2_TIMING
+    if (uint64_t* r = timing_row()) {
+        if ((threadIdx.x & 63) == 0) {
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);    // HW_ID
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);   // XCC_ID
+            r[0] = ((uint64_t)xcc << 32) | hw;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[3] = __builtin_amdgcn_s_memtime();
+        }
+    }
+#endif
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint32_t base = blockIdx.x * 64u, i = base + lane, gid = P.gid_off + i;
+    const bool live = i < P.N;
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    const Tile T(io.sf, P.N, i);
+    Env H;                         // waves 1-3: the speculative reset (kept across the barrier)
+    float held1[10], ng1[9];       // wave 2: first reset sensor call
+    uint32_t ctr = 0;
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        bool do_reset = false;
+        ResetSeed rs;
+        if (live) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + lane * OD, rs, s_hjgrid);
+        const uint64_t m = __ballot(do_reset);
+        if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
+        if (do_reset) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { s_seed[k * 64 + lane] = rs.wb[k]; s_seed[(3 + k) * 64 + lane] = rs.bias[k]; }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s_seed[(6 + k) * 64 + lane] = rs.ou[k];
+        }
+    } else if (P.auto_reset && live) {
+        __builtin_amdgcn_s_setprio(0);
+        ctr = (uint32_t)bi(T.ld(G_CORE3).z);
+        const Keys K = make_keys(P.key0, P.key1);
+        const Rng g{K, ctr, gid, TAG_RESET};
+        if (wave == 1) {
+            reset_kinematics<PHYS>(P, H, g, gid);
+        } else if (wave == 2) {
+            reset_kinematics<PHYS>(P, H, g, gid);
+            if (NOISE) held_measurement(P, H, g, 32, held1, ng1);
+        } else {
+            const bool need_level = P.need_level || io.level != nullptr;
+            H.level = need_level ? T.ld(G_LEVEL).w : P.level_fixed;
+            H.level_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
+            reset_params<DR>(P, H, g);
+            if (NOISE) {
+                Env H2;
+                reset_kinematics<PHYS>(P, H2, g, gid);
+                float held2[10], ng2[9];
+                held_measurement(P, H2, g, 40, held2, ng2);
+#pragma unroll
+                for (int k = 0; k < 10; ++k) s_c2[k * 64 + lane] = held2[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) s_c2[(10 + k) * 64 + lane] = ng2[k];
+            }
+        }
+    }
+    lds_barrier();
+    TSTAMP(4);   // block barrier passed
+    const uint64_t mask = ((uint64_t)s_mask[1] << 32) | (uint64_t)s_mask[0];
+#ifdef CF2_AB_NO_RESET
+    const bool mine = false;       // A/B only: measures the reset tail's share
+#else
+    const bool mine = wave != 0 && ((mask >> lane) & 1ull);
+#endif
+    if (mine) {
+        TSTAMP(6);
+        if (wave == 1) {
+            const float ou[4] = {s_seed[6 * 64 + lane], s_seed[7 * 64 + lane], s_seed[8 * 64 + lane], s_seed[9 * 64 + lane]};
+            store_reset_kinematics<PHYS>(P, T, H, ou, ctr);
+        } else if (wave == 2) {
+            // the reset observation (reset_observe: two sensor calls, then the history row)
+            Env& E = H;
+            float* row = s_obs + lane * OD;
+            if (NOISE) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { E.lpf[k] = s_seed[k * 64 + lane]; E.bias[k] = s_seed[(3 + k) * 64 + lane]; }
+                gyro_update(P, E, ng1);
+#pragma unroll
+                for (int k = 0; k < 10; ++k) row[k] = held1[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) row[10 + k] = E.lpf[k];
+                float ng2[9];
+#pragma unroll
+                for (int k = 0; k < 10; ++k) E.held[k] = s_c2[k * 64 + lane];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) ng2[k] = s_c2[(10 + k) * 64 + lane];
+                gyro_update(P, E, ng2);
+#pragma unroll
+                for (int k = 0; k < 10; ++k) E.obs_prev[k] = E.held[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) E.obs_prev[10 + k] = E.lpf[k];
+            } else {
+                // noise off: the observation is the state (compute_observation<false>)
+                const float o[17] = {E.p[0], E.p[1], E.p[2], E.q[0], E.q[1], E.q[2], E.q[3], E.v[0], E.v[1],
+                                     E.v[2], E.wb[0], E.wb[1], E.wb[2], E.la[0], E.la[1], E.la[2], E.la[3]};
+#pragma unroll
+                for (int k = 0; k < 17; ++k) { row[k] = o[k]; E.obs_prev[k] = o[k]; }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row[OL + k] = E.la[k];
+#pragma unroll
+            for (int k = 0; k < OL; ++k) row[OL + 4 + k] = E.obs_prev[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row[2 * OL + 4 + k] = E.la[k];
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) E.hact[s2][k] = E.la[k];
+            store_reset_history<NOISE>(P, T, E);
+            TSTAMP(8);
+        } else {
+            store_reset_params<DR>(P, T, H);
+        }
+    }
+    lds_barrier();
+    TSTAMP(12);  // reset rows in LDS
+    write_obs_rows(io.obs + (size_t)base * OD, s_obs, P.N - base < 64u ? P.N - base : 64u, 64u, OD, tid, 256u);
+#ifdef CF2_TIMING
+    TSTAMP(5);
     if (uint64_t* r = timing_row())
         if ((threadIdx.x & 63) == 0) r[2] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2027,8 +2220,15 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
     // small N (<= 32768 envs: at most one 64-env wave per two SIMDs with the helpers) runs 64 envs
-    // per block (C2 at 4096 envs: 17.7 -> 13.2 us); above that the helper waves would cost
-    // residency (65 536 envs: 15.5 -> 24.7 us)
+    // per block, the other three waves computing the envs' potential resets meanwhile
+    // (step_kernel_small); above that the helper waves would cost residency (65 536 envs: 15.5 ->
+    // 24.7 us with 64-env blocks)
+#ifndef CF2_SMALL_OLD
+    if (P.N <= 32768u) {
+        hipLaunchKernelGGL((step_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s, P, io);
+        return hipGetLastError();
+    }
+#endif
     const uint32_t epb = P.N <= 32768u ? 64u : (uint32_t)CF2_STEP_BLOCK;
     const dim3 grid((P.N + epb - 1) / epb), block(CF2_STEP_BLOCK);
     // blocks resident at once = CUs x blocks per CU at this kernel's VGPR/LDS use (queried once)

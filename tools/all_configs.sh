@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 : > "$OUT"
 run() {   # label, bench args...
   local label=$1; shift
-  timeout -k 10 180 python bench.py --steps 2000 --warmup 1000 --no-cpu-baseline --rollout-k 32 --streaming-ring 0 "$@" 2>/dev/null |
+  timeout -k 10 180 python bench.py --steps 2000 --warmup 1000 --no-cpu-baseline --rollout-k 32 --streaming-ring 0 --oc-envs 0 "$@" 2>/dev/null |
     python -c "import json,sys; d=json.loads(sys.stdin.read()); d['label']='$label'; print(json.dumps(d))" >> "$OUT" || exit 1
 }
 run C2 --env-id DroneHoverBulletFreeEnvWithConstWind-v0 --envs-per-gpu 4096
