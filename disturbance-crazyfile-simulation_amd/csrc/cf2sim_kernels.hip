@@ -31,11 +31,13 @@ namespace cf2 {
 // Random-word sources: Rng computes Philox blocks; TableRng reads blocks a whole block of
 // threads precomputed into LDS (auto-reset, see step_kernel).  Counter = (block, rng counter,
 // global env id, tag).
-struct Rng {
-    const Keys& K;
+template <class KT>
+struct RngT {
+    const KT& K;
     uint32_t ctr, gid, tag;
     __device__ __forceinline__ U4 block(uint32_t b) const { return philox(K, b, ctr, gid, tag); }
 };
+using Rng = RngT<Keys>;
 
 // reset-time blocks (reset_env): 0-13 direct, sensor calls at 32-37 and 40-45
 enum { RESET_SLOTS = 26 };
@@ -95,19 +97,31 @@ __device__ __forceinline__ void normals(const TableRng& g, uint32_t b0, float (&
 // parked in the lane's own LDS obs-staging row (which the observation overwrites only after the
 // call): row words 0-17 are the call's 18 normals (Box-Muller already applied), 18-23 the raw words
 // of its uniforms.  block(b) returns row words 4(b-b0)..+3, normals<N> the first N row words.
+// STRIDE: distance between consecutive words (1: the lane's own LDS row; 64: a [word][env] table
+// of the small-N kernel, where the helper waves stage the env-step's later draws)
+template <uint32_t STRIDE = 1>
 struct RowRng {
     const uint32_t* t;
     uint32_t b0;
     __device__ __forceinline__ U4 block(uint32_t b) const {
-        const uint32_t* q = t + 4u * (b - b0);
-        return U4{q[0], q[1], q[2], q[3]};
+        const uint32_t* q = t + 4u * (b - b0) * STRIDE;
+        return U4{q[0], q[STRIDE], q[2 * STRIDE], q[3 * STRIDE]};
     }
 };
-template <int N>
-__device__ __forceinline__ void normals(const RowRng& g, uint32_t b0, float (&z)[N]) {
+template <int N, uint32_t STRIDE>
+__device__ __forceinline__ void normals(const RowRng<STRIDE>& g, uint32_t b0, float (&z)[N]) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) z[k] = __uint_as_float(g.t[4u * (b0 - g.b0) + k]);
+    for (int k = 0; k < N; ++k) z[k] = __uint_as_float(g.t[(4u * (b0 - g.b0) + k) * STRIDE]);
 }
+
+// The small-N kernel's helper-drawn env-step randomness ([word][env] in LDS, stride 64): what the
+// env-step draws after its first physics sub-step in the reference-default shape (SPEC 1 with
+// sensor noise), with Box-Muller already applied to the words that become normals:
+//   words  0-3   OU normals of sub-step 1              (step block 2)
+//   words  4-12  gyro normals of sub-step 1's call      (normals<9> at block 16: blocks 16-18)
+//   words 13-30  final sensor call's 18 normals         (normals<18> at block 24: blocks 24-28)
+//   words 31-36  its uniform words: block 28 .z .w, block 29 .x .y .z .w
+enum { HD_WORDS = 37, HD_OU1 = 0, HD_GYRO1 = 4, HD_FINAL = 13 };
 
 // Normals LO..HI-1 of the sequence normals<N>(g, b0, .) would produce, drawing only the Philox
 // blocks and Box-Muller pairs that cover them (the stream positions of all other draws are
@@ -368,6 +382,10 @@ __device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, u
         for (uint32_t k = tid; k < nvalid * od / 2; k += nthreads) __builtin_nontemporal_store(src2[k], dst2 + k);
     }
 }
+
+// Block barrier for LDS hand-offs: the calling wave's LDS operations complete first; its global
+// stores keep draining (__syncthreads would also wait for those, vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ------------------------------------------------------------------------------------
 // per-env register state
@@ -1252,9 +1270,13 @@ enum { SEED_WORDS = 13 };
 
 // The env-step on a loaded Env.  STORE: write the state back (the one-step kernel: the physics
 // state as soon as it is final, the rest at the end); the fused rollout keeps it in registers.
-template <bool NOISE, bool DR, int PHYS, bool STORE>
+// HD (small-N kernel, reference-default shape with sensor noise): the draws after the first
+// sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
+// env wave joins the helpers' LDS barrier before its second sub-step.
+template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, class KT = Keys>
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
-                                              float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid) {
+                                              float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
+                                              const float* hd = nullptr) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     const uint32_t gid = P.gid_off + i;
@@ -1262,10 +1284,11 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     TREADY("v"(E.p[0]), "v"(E.obs_prev[OL - 1]), "v"(E.hact[1][3]), "v"(E.K[3]), "v"(a4.w), "v"(E.rng));
     TSTAMP(1);   // every state load has landed
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-    const Keys K = make_keys(P.key0, P.key1);
-    const Rng g{K, E.rng, gid, TAG_STEP};
+    const KT K = make_keys_as((const KT*)nullptr, P.key0, P.key1);
+    const RngT<KT> g{K, E.rng, gid, TAG_STEP};
     // reference-default shape: the final (full) sensor call's blocks are drawn up front (RowRng)
-    const bool pre_final = NOISE && P.agg == 2 && P.obs_rate == 2;
+    const bool pre_final = !HD && NOISE && P.agg == 2 && P.obs_rate == 2;
+    const uint32_t* hdw = reinterpret_cast<const uint32_t*>(hd);
     const uint32_t fbase = 8u + 8u * (uint32_t)P.agg;
     if (pre_final) {
         uint32_t* row = reinterpret_cast<uint32_t*>(obs_row);
@@ -1359,7 +1382,12 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
 #pragma unroll 4
     for (int s = 0; s < P.agg; ++s) {
         float on[4];
-        normals<4>(g, 1 + s, on);
+        if (HD && s == 1) {
+            lds_barrier();                                   // the helper waves' draws are in LDS
+            normals<4>(RowRng<64>{hdw + HD_OU1 * 64, 2}, 2, on);
+        } else {
+            normals<4>(g, 1 + s, on);
+        }
         float dw = 0.0f;
         if (PHYS == PHYS_BULLET_T && P.num_drones > 1 && P.downwash_on)
             dw = downwash(P, E.p, gid % (uint32_t)P.num_drones);   // mates' positions before this sub-step
@@ -1368,7 +1396,10 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         float dummy[17];
         // a sub-step's held measurement reaches an observation only if the final measurement
         // of the env-step is not a full one (aggregate_phy_steps % obs_rate != 0)
-        compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy, P.held_persistent != 0);
+        if (HD && s == 1)
+            compute_observation<NOISE>(P, E, RowRng<64>{hdw + HD_GYRO1 * 64, 16}, 16, E.ep_step * P.agg + s, dummy, false);
+        else
+            compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy, P.held_persistent != 0);
     }
     // the history (o_{k-1}, last actions) is only read by compute_history: the one-step kernel
     // loads it after the physics, so its 21 registers are not live across the sub-steps (the final
@@ -1377,8 +1408,10 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     float onx[17];
     TREADY("v"(E.q[3]), "v"(E.lpf[2]));
     TSTAMP(2);   // physics sub-steps done
-    if (pre_final) {
-        const RowRng gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
+    if (HD) {
+        compute_observation<NOISE>(P, E, RowRng<64>{hdw + HD_FINAL * 64, fbase}, fbase, (E.ep_step + 1) * P.agg, onx);
+    } else if (pre_final) {
+        const RowRng<1> gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
         compute_observation<NOISE>(P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
     } else {
         compute_observation<NOISE>(P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
@@ -1389,9 +1422,11 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     const bool done = term || trunc;
     const bool do_reset = done && P.auto_reset;
     // the physics state is final now: store it early so its registers free up before the
-    // epilogue.  An env that auto-resets is not stored: its reset writes every group stored here
-    // (reset_role / the small-N reset roles), so no two waves store one group in one launch
-    if (STORE && !do_reset) store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
+    // epilogue.  SKIP_RESETTING (the small-N kernel, whose reset stores follow an LDS-only
+    // barrier): an env that auto-resets is not stored, its reset writes every group stored here,
+    // so no two waves store one group in one launch.  The large-N kernel stores it anyway (its
+    // resets follow __syncthreads, which drains these stores first; skipping cost 0.6 us there)
+    if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
     const float r = compute_reward(P, E, a, term);
     const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
     io.rew[i] = r;
@@ -1419,20 +1454,20 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         rs.ctr = E.rng;
     }
     E.rng += 1;
-    if (STORE && !do_reset) store_tail<NOISE>(P, io.sf, i, E);
+    if (STORE && !(SKIP_RESETTING && do_reset)) store_tail<NOISE>(P, io.sf, i, E);
     TSTAMP(3);   // epilogue issued
     return do_reset;
 }
 
-template <bool NOISE, bool DR, int PHYS>
+template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false>
 __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
-                                         ResetSeed& rs, const double* hj_grid) {
+                                         ResetSeed& rs, const double* hj_grid, const float* hd = nullptr) {
     Env E;
     // every state load is issued before the first state store: on gfx9 vmcnt also counts stores,
     // so a load issued after the state stores would wait for the whole store burst to drain (the
     // history is loaded after the physics sub-steps, still ahead of store_core, in step_env_body)
     load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
-    return step_env_body<NOISE, DR, PHYS, true>(P, io, i, E, obs_row, rs, hj_grid);
+    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD>(P, io, i, E, obs_row, rs, hj_grid, hd);
 }
 
 // Reset one env in place: reads only what a reset consumes from the finished episode (the
@@ -1787,10 +1822,6 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 #endif
 }
 
-// Block barrier for LDS hand-offs: the calling wave's LDS operations complete first; its global
-// stores keep draining (__syncthreads would also wait for those, vmcnt(0)).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
 // Small N (<= 32 768 envs): the launch is as long as one wave's env-step chain, and the auto-reset
 // tail used to be ~40 % of it.  Each 256-thread block holds 64 envs.  Wave 0
 // steps them (issue priority 3).  Waves 1-3 meanwhile compute, speculatively for all 64 envs and at
@@ -1818,6 +1849,10 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     __shared__ float s_c2[C2_WORDS * 64];                  // [word][env]
     __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
     __shared__ double s_hjgrid[6 * HJ_PTS];
+    // reference-default shape with sensor noise: the helpers also draw the env-step's randomness
+    // after its first sub-step (HD_* layout), handed over at an LDS barrier before sub-step 1
+    constexpr bool HD = SPEC == 1 && NOISE;
+    __shared__ float s_draw[HD ? HD_WORDS * 64 : 1];
 #ifdef CF2_TIMING
     if (uint64_t* r = timing_row()) {
         if ((threadIdx.x & 63) == 0) {
@@ -1837,11 +1872,51 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     Env H;                         // waves 1-3: the speculative reset (kept across the barrier)
     float held1[10], ng1[9];       // wave 2: first reset sensor call
     uint32_t ctr = 0;
+    if (HD && wave != 0) {
+        // the env-step's draws after sub-step 0 (step tag, the env's counter), split over the
+        // three helper waves; Box-Muller applied where the env-step turns words into normals
+        if (live) {
+            const uint32_t sctr = (uint32_t)bi(T.ld(G_CORE3).z);
+            const Keys K = make_keys(P.key0, P.key1);
+            const Rng g{K, sctr, gid, TAG_STEP};
+            float* d = s_draw + lane;
+            auto bm4 = [&](uint32_t blk, int w) {          // 4 normals of one block -> words w..w+3
+                const U4 u = g.block(blk);
+                float z0, z1, z2, z3;
+                box_muller(u.x, u.y, z0, z1);
+                box_muller(u.z, u.w, z2, z3);
+                d[(w + 0) * 64] = z0; d[(w + 1) * 64] = z1; d[(w + 2) * 64] = z2; d[(w + 3) * 64] = z3;
+            };
+            if (wave == 1) {
+                bm4(2, HD_OU1);                             // OU of sub-step 1
+                bm4(16, HD_GYRO1);                          // sub-step 1 sensor call: normals 0-8
+                bm4(17, HD_GYRO1 + 4);
+                const U4 u = g.block(18);
+                float z0, z1;
+                box_muller(u.x, u.y, z0, z1);
+                d[(HD_GYRO1 + 8) * 64] = z0;
+            } else if (wave == 2) {
+                bm4(24, HD_FINAL);                          // final sensor call: normals 0-11
+                bm4(25, HD_FINAL + 4);
+                bm4(26, HD_FINAL + 8);
+            } else {
+                bm4(27, HD_FINAL + 12);                     // normals 12-15
+                const U4 u = g.block(28), v = g.block(29);
+                float z0, z1;
+                box_muller(u.x, u.y, z0, z1);               // normals 16-17, then the six uniform words
+                d[(HD_FINAL + 16) * 64] = z0; d[(HD_FINAL + 17) * 64] = z1;
+                d[(HD_FINAL + 18) * 64] = __uint_as_float(u.z); d[(HD_FINAL + 19) * 64] = __uint_as_float(u.w);
+                d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
+                d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
+            }
+        }
+        lds_barrier();   // joined by the env wave before its second sub-step (step_env_body)
+    }
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);
         bool do_reset = false;
         ResetSeed rs;
-        if (live) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + lane * OD, rs, s_hjgrid);
+        if (live) do_reset = step_env<NOISE, DR, PHYS, true, HD>(P, io, i, s_obs + lane * OD, rs, s_hjgrid, s_draw + lane);
         const uint64_t m = __ballot(do_reset);
         if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
         if (do_reset) {
@@ -1876,6 +1951,8 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
                 for (int k = 0; k < 9; ++k) s_c2[(10 + k) * 64 + lane] = ng2[k];
             }
         }
+        TREADY("v"(H.p[0]), "v"(H.K[3]), "v"(H.la[3]));
+        TSTAMP(9);   // helper: speculative reset computed
     }
     lds_barrier();
     TSTAMP(4);   // block barrier passed
@@ -1998,6 +2075,15 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
 #ifndef CF2_ROLL_MIN_WAVES
 #define CF2_ROLL_MIN_WAVES 2   // the whole state stays live across the loop (~270 registers at peak)
 #endif
+// Round keys of the fused rollout.  With all 20 in SGPRs (Keys) the kernel spills 28 B/lane of
+// VGPRs (7 registers); re-deriving them per Philox call (KeysBase, -DCF2_ROLL_BASE_KEYS) removes
+// every VGPR spill but was slower on MI355X (K = 32 per env-step: 27.9 -> 30.0 us at 262 144 envs,
+// 8.5 -> 10.1 us at 4096): the SALU adds sit in each Philox chain, the spills do not.
+#ifdef CF2_ROLL_BASE_KEYS
+typedef KeysBase RollKeys;
+#else
+typedef Keys RollKeys;
+#endif
 template <bool NOISE, bool DR, int PHYS, int SPEC, uint32_t EPB>
 __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_kernel(KParams P0, StepIO io0, uint32_t K,
                                                                                   uint32_t act_stride) {
@@ -2033,7 +2119,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
         if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
         bool do_reset = false;
         ResetSeed rs;
-        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false>(P, io, i, E, obs_row, rs, s_hjgrid);
+        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false, RollKeys>(P, io, i, E, obs_row, rs, s_hjgrid);
         __syncthreads();             // s_cnt initialised
         uint32_t pos = 0;
         const uint64_t m = __ballot(do_reset);
@@ -2049,7 +2135,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
         for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
             const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
             {
-                const Keys Kk = make_keys(P.key0, P.key1);
+                const RollKeys Kk = make_keys_as((const RollKeys*)nullptr, P.key0, P.key1);
                 for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
                     const uint32_t sl = w / nc, e = w - sl * nc, p2 = c0 + e;
                     U4 u = philox(Kk, reset_block_of_slot((int)sl), s_ctr[p2], P.gid_off + base + s_list[p2], TAG_RESET);

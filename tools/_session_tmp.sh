@@ -1,5 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/r03b
-timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/r03b/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r03b/pytest_gpu.log; exit 1; }
-tail -2 gpurun_out/r03b/pytest_gpu.log
-timeout -k 10 600 bash tools/ab_envs.sh "DroneHoverBulletFreeEnvWithConstWind-v0:4096 DroneHoverBulletFreeEnvWithGust-v0:16384 DroneHoverBulletFreeEnvWithGust-v0:32768 DroneHoverBulletFreeEnvWithGust-v0:262144" build_ab/small_old.so build_ab/small_new.so 2>&1 | tee gpurun_out/r03b/ab_small.txt
+O=gpurun_out/r03e
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for n in 32768 4096 65536; do
+  CF2SIM_LIB=build_ab/timing.so timeout -k 10 120 python tools/timeline.py --envs $n --warmup 1000 > $O/timeline_$n.txt 2>&1 || { echo "timeline $n failed"; tail -20 $O/timeline_$n.txt; exit 1; }
+  grep -v "reset waves\|role-2\|amdgpu.ids" $O/timeline_$n.txt
+done

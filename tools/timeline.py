@@ -31,7 +31,8 @@ def main():
     env.reset()
     lib = env.lib
     lib.cf2_debug_timing_buffer.argtypes = [ctypes.c_void_p]
-    n_waves = (args.envs + 63) // 64
+    # the small-N kernel (<= 32768 envs) runs 4 waves per 64-env block: one timing row per wave
+    n_waves = (args.envs + 63) // 64 * (4 if args.envs <= 32768 else 1)
     buf = torch.zeros(n_waves, 16, dtype=torch.int64, device=env.device)
     acts = torch.rand(8, args.envs, 4, device=env.device) * 2 - 1
     for k in range(args.warmup):
@@ -77,8 +78,21 @@ def main():
         print(f"  role-2 waves {int(r2.sum())}: draws+barrier {np.mean(r6 - a4):.0f}, pose {np.mean(r7 - r6):.0f}, "
               f"sensor call+history {np.mean(r8 - r7):.0f}, stores+barrier {np.mean(e12 - r8):.0f}, "
               f"obs copy {np.mean(e5 - e12):.0f} cycles")
+    envw = t[:, 4] != 0                     # small-N kernel: env waves stamp 1..3, helper waves 9
+    if (~envw).any() and (t[~envw, 12] != 0).any():
+        hw_ = ~envw & (t[:, 12] != 0)
+        e = {k: t[envw, 3 + k].astype(np.float64) for k in (0, 1, 2, 3, 4, 2 + 10)}
+        print(f"  small-N env waves {int(envw.sum())}: loads {np.mean(e[1] - e[0]):.0f}, physics {np.mean(e[2] - e[1]):.0f}, "
+              f"obs/history/stores {np.mean(e[3] - e[2]):.0f}, -> barrier passed {np.mean(e[4] - e[3]):.0f}, "
+              f"-> rows in LDS {np.mean(e[12] - e[4]):.0f}, -> end {np.mean(t[envw, 8] - t[envw, 15]):.0f}; "
+              f"lifetime {np.mean(t[envw, 8] - t[envw, 3]):.0f} (p90 {np.percentile(t[envw, 8] - t[envw, 3], 90):.0f})")
+        h0, h9, h4 = (t[hw_, 3 + k].astype(np.float64) for k in (0, 9, 1 + 3))
+        print(f"  small-N helper waves {int(hw_.sum())}: speculative reset {np.mean(h9 - h0):.0f} "
+              f"(p90 {np.percentile(h9 - h0, 90):.0f}), wait at barrier {np.mean(h4 - h9):.0f}")
     print(f"waves {n_waves}; span {rend.max():.0f} cycles (realtime x24); per XCD end: " +
           " ".join(f"{x}:{rend[xcc == x].max():.0f}" for x in range(8) if (xcc == x).any()))
+    print("  per XCD first/last wave start: " +
+          " ".join(f"{x}:{rstart[xcc == x].min():.0f}/{rstart[xcc == x].max():.0f}" for x in range(8) if (xcc == x).any()))
     for k, v in dur.items():
         print(f"  {names[k]:24s} mean {v.mean():8.0f}  p10 {np.percentile(v, 10):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}")
         res[names[k]] = float(v.mean())
