@@ -387,6 +387,39 @@ __device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, u
 // stores keep draining (__syncthreads would also wait for those, vmcnt(0)).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// write_obs_rows for the small-N kernel: row r comes from rrow (the reset observations the helper
+// waves staged) where bit r of mask is set, else from obs (the env-step's observations)
+template <uint32_t OD>
+__device__ __forceinline__ void write_obs_rows_merged(float* dst, const float* s_obs, const float* s_rrow, uint64_t mask,
+                                                      uint32_t nvalid, uint32_t tid, uint32_t nthreads) {
+    typedef float f4x __attribute__((ext_vector_type(4)));
+    typedef float f2x __attribute__((ext_vector_type(2)));
+    if (nvalid == 64u && (64u * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
+        const f4x* a4 = reinterpret_cast<const f4x*>(s_obs);
+        const f4x* b4 = reinterpret_cast<const f4x*>(s_rrow);
+        f4x* dst4 = reinterpret_cast<f4x*>(dst);
+        for (uint32_t k = tid; k < 64u * OD / 4; k += nthreads) {
+            f4x v = a4[k];
+            if (mask) {
+                const f4x w = b4[k];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((mask >> ((4u * k + (uint32_t)j) / OD)) & 1ull) v[j] = w[j];
+            }
+            __builtin_nontemporal_store(v, dst4 + k);
+        }
+    } else {
+        const f2x* a2 = reinterpret_cast<const f2x*>(s_obs);
+        const f2x* b2 = reinterpret_cast<const f2x*>(s_rrow);
+        f2x* dst2 = reinterpret_cast<f2x*>(dst);
+        for (uint32_t k = tid; k < nvalid * OD / 2; k += nthreads) {
+            f2x v = a2[k];
+            if ((mask >> ((2u * k) / OD)) & 1ull) v = b2[k];      // OD is even: a pair never spans rows
+            __builtin_nontemporal_store(v, dst2 + k);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // per-env register state
 // ------------------------------------------------------------------------------------
@@ -416,21 +449,32 @@ __device__ __forceinline__ F4 f4(float x, float y, float z, float w) { return F4
 __device__ __forceinline__ float ib(int v) { return __int_as_float(v); }       // int field -> slot bits
 __device__ __forceinline__ int bi(float v) { return __float_as_int(v); }
 
-struct Tile {
+#ifndef CF2_STATE_LD_AUX
+#define CF2_STATE_LD_AUX 0     // cache-policy bits of the state loads (A/B: 2 = nt)
+#endif
+#ifndef CF2_STATE_ST_AUX
+#define CF2_STATE_ST_AUX 0     // ... and stores
+#endif
+// ST_AUX: cache-policy bits of the state stores.  2 = nt: the step kernel's stores when the
+// working set exceeds the Infinity Cache (launch_step_t) -- at 1 Mi envs 185 -> 144 us, while at
+// 262 144 envs (cache-resident) nt stores cost +3 us, as nt loads do at both sizes.
+template <int ST_AUX = CF2_STATE_ST_AUX>
+struct TileT {
     __amdgpu_buffer_rsrc_t r;
     uint32_t voff;
-    __device__ __forceinline__ Tile(const void* base, uint32_t N, uint32_t i)
+    __device__ __forceinline__ TileT(const void* base, uint32_t N, uint32_t i)
         : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(uint32_t)state_bytes(N), 0x00020000)),
           voff((i >> 6) * (uint32_t)(NG * 1024) + (i & 63u) * 16u) {}
     __device__ __forceinline__ F4 ld(int g) const {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + (uint32_t)g * 1024u), 0, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + (uint32_t)g * 1024u), 0, CF2_STATE_LD_AUX);
         return F4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
     }
     __device__ __forceinline__ void st(int g, F4 f) const {
         const u32x4 v = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(voff + (uint32_t)g * 1024u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(voff + (uint32_t)g * 1024u), 0, ST_AUX);
     }
 };
+using Tile = TileT<>;
 
 // G_LPF: with sensor noise the gyro LPF state shares the last o_{k-1} group (13 of its 16 slots
 // are o_{k-1}): that group is read with the state, the other three with the history
@@ -538,9 +582,9 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
 
 // state the physics sub-steps update (stored as soon as the last sub-step is done; group 3,
 // which carries the counters, is stored with the history at the end of the step)
-template <bool NOISE, bool DR, int PHYS>
+template <bool NOISE, bool DR, int PHYS, int ST_AUX = CF2_STATE_ST_AUX>
 __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
-    const Tile T(sf, P.N, i);
+    const TileT<ST_AUX> T(sf, P.N, i);
     T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
     T.st(1, f4(E.q[1], E.q[2], E.q[3], E.v[0]));
     T.st(2, f4(E.v[1], E.v[2], E.w[0], E.w[1]));
@@ -562,8 +606,8 @@ __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__
 }
 
 // the o_{k-1} groups; with sensor noise the last one carries the gyro LPF state
-template <bool NOISE>
-__device__ __forceinline__ void store_obs_prev(const Tile& T, const Env& E) {
+template <bool NOISE, class TT>
+__device__ __forceinline__ void store_obs_prev(const TT& T, const Env& E) {
     constexpr int OL = NOISE ? 13 : 17;
 #pragma unroll
     for (int g = 0; g < (OL + 3) / 4; ++g) {
@@ -576,9 +620,9 @@ __device__ __forceinline__ void store_obs_prev(const Tile& T, const Env& E) {
 }
 
 // end of the step: history, counters (group 3 with the last angular-rate component)
-template <bool NOISE>
+template <bool NOISE, int ST_AUX = CF2_STATE_ST_AUX>
 __device__ __forceinline__ void store_tail(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
-    const Tile T(sf, P.N, i);
+    const TileT<ST_AUX> T(sf, P.N, i);
     T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
     T.st(G_HACT + 1, f4(E.hact[1][0], E.hact[1][1], E.hact[1][2], E.hact[1][3]));
     store_obs_prev<NOISE>(T, E);
@@ -1273,10 +1317,14 @@ enum { SEED_WORDS = 13 };
 // HD (small-N kernel, reference-default shape with sensor noise): the draws after the first
 // sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
 // env wave joins the helpers' LDS barrier before its second sub-step.
-template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, class KT = Keys>
+// fin (small-N kernel, HD): this env's column of the [word][env] LDS table the outputs are
+// finished from (FIN_* layout), or null to finish them here.
+enum { FIN_P = 0, FIN_V = 3, FIN_RPY = 6, FIN_WB = 9, FIN_FLAGS = 12, FIN_LEVEL = 13, FIN_WORDS = 14 };
+template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, class KT = Keys,
+          int ST_AUX = CF2_STATE_ST_AUX>
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
                                               float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
-                                              const float* hd = nullptr) {
+                                              const float* hd = nullptr, float* fin = nullptr) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     const uint32_t gid = P.gid_off + i;
@@ -1426,14 +1474,25 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     // barrier): an env that auto-resets is not stored, its reset writes every group stored here,
     // so no two waves store one group in one launch.  The large-N kernel stores it anyway (its
     // resets follow __syncthreads, which drains these stores first; skipping cost 0.6 us there)
-    if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS>(P, io.sf, i, E);
-    const float r = compute_reward(P, E, a, term);
-    const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
-    io.rew[i] = r;
-    io.done[i] = (uint8_t)done;
-    if (io.trunc) io.trunc[i] = (uint8_t)trunc;
-    if (io.cost) io.cost[i] = cost;
-    if (io.level) io.level[i] = level_used;
+    if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS, ST_AUX>(P, io.sf, i, E);
+    if (HD && fin != nullptr) {
+        // small-N kernel: reward, cost and the per-env outputs are finished by a helper wave after
+        // the block barrier (finish_outputs), off this wave's chain; it gets what they read
+        fin[FIN_P * 64] = E.p[0]; fin[(FIN_P + 1) * 64] = E.p[1]; fin[(FIN_P + 2) * 64] = E.p[2];
+        fin[FIN_V * 64] = E.v[0]; fin[(FIN_V + 1) * 64] = E.v[1]; fin[(FIN_V + 2) * 64] = E.v[2];
+        fin[FIN_RPY * 64] = E.rpy[0]; fin[(FIN_RPY + 1) * 64] = E.rpy[1]; fin[(FIN_RPY + 2) * 64] = E.rpy[2];
+        fin[FIN_WB * 64] = E.wb[0]; fin[(FIN_WB + 1) * 64] = E.wb[1]; fin[(FIN_WB + 2) * 64] = E.wb[2];
+        fin[FIN_FLAGS * 64] = __uint_as_float((term ? 1u : 0u) | (trunc ? 2u : 0u));
+        fin[FIN_LEVEL * 64] = level_used;
+    } else {
+        const float r = compute_reward(P, E, a, term);
+        const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
+        io.rew[i] = r;
+        io.done[i] = (uint8_t)done;
+        if (io.trunc) io.trunc[i] = (uint8_t)trunc;
+        if (io.cost) io.cost[i] = cost;
+        if (io.level) io.level[i] = level_used;
+    }
     {
         float o[OD];
         compute_history<NOISE>(P, E, onx, o);
@@ -1454,20 +1513,22 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         rs.ctr = E.rng;
     }
     E.rng += 1;
-    if (STORE && !(SKIP_RESETTING && do_reset)) store_tail<NOISE>(P, io.sf, i, E);
+    if (STORE && !(SKIP_RESETTING && do_reset)) store_tail<NOISE, ST_AUX>(P, io.sf, i, E);
     TSTAMP(3);   // epilogue issued
     return do_reset;
 }
 
-template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false>
+template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = CF2_STATE_ST_AUX>
 __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
-                                         ResetSeed& rs, const double* hj_grid, const float* hd = nullptr) {
+                                         ResetSeed& rs, const double* hj_grid, const float* hd = nullptr,
+                                         float* fin = nullptr) {
     Env E;
     // every state load is issued before the first state store: on gfx9 vmcnt also counts stores,
     // so a load issued after the state stores would wait for the whole store burst to drain (the
     // history is loaded after the physics sub-steps, still ahead of store_core, in step_env_body)
     load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
-    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD>(P, io, i, E, obs_row, rs, hj_grid, hd);
+    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD, Keys, ST_AUX>(P, io, i, E, obs_row, rs, hj_grid, hd,
+                                                                                 fin);
 }
 
 // Reset one env in place: reads only what a reset consumes from the finished episode (the
@@ -1765,7 +1826,7 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
 // barrier; their state rows were just written by this block and are still in L2, so the reset's
 // scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
 // 4-byte field access for them).
-template <bool NOISE, bool DR, int PHYS, int SPEC>
+template <bool NOISE, bool DR, int PHYS, int SPEC, int ST_AUX = CF2_STATE_ST_AUX>
 #ifndef CF2_STEP_BLOCK
 #define CF2_STEP_BLOCK 256     // envs per block = auto-reset compaction group
 #endif
@@ -1813,7 +1874,8 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     ResetSeed rs;
     __shared__ double s_hjgrid[6 * HJ_PTS];
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    if (tid < EPB && i < P.N) do_reset = step_env<NOISE, DR, PHYS>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
+    if (tid < EPB && i < P.N)
+        do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, EPB);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
@@ -1828,16 +1890,43 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 // priority 0, every part of a potential auto-reset that does not depend on the finished episode:
 // a reset's draws are keyed by the env's RNG counter, which is known when the state loads, so
 // they are the same Philox blocks the reset would draw after the step.
-//   wave 1 (A): reset pose, velocities, motor state, latency ring    (reset_kinematics)
-//   wave 2 (B): the pose again, the first reset sensor call's held measurement and gyro normals
-//   wave 3 (C): domain randomisation, disturbance, level (reset_params); the pose again and the
-//               second sensor call's held part and gyro normals, handed to B in LDS
+//   wave 1 (A): reset pose, velocities, motor state, latency ring    (reset_kinematics), domain
+//               randomisation, disturbance, level (reset_params)
+//   wave 2 (B): the pose again, the first reset sensor call's held measurement and gyro normals;
+//               stages the reset observation row but for its two gyro-LPF triples
+//   wave 3 (C): the pose again and the second sensor call's held part (into the staged row) and
+//               gyro normals (handed to B in LDS); after the barrier it finishes every env's reward,
+//               cost and outputs (finish_outputs), off the env wave's chain
 // After one LDS barrier only the finished envs' work remains, on their lanes of waves 1-3: the two
 // gyro updates, which need the finished episode's body rates (the gyro LPF seed) and gyro bias,
 // the reset observation row, and the reset's state stores (store_reset_*).  The env wave does not
 // store the state of envs that reset (step_env_body), so no group is stored twice.
+// reward, cost and the per-env outputs of step_env_body, from the FIN_* table (the small-N
+// kernel's helper wave 3, after the block barrier)
+__device__ __forceinline__ void finish_outputs(const KParams& P, const StepIO& io, uint32_t i, const float* fin,
+                                               const float4 a4) {
+    Env F;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        F.p[k] = fin[(FIN_P + k) * 64]; F.v[k] = fin[(FIN_V + k) * 64];
+        F.rpy[k] = fin[(FIN_RPY + k) * 64]; F.wb[k] = fin[(FIN_WB + k) * 64];
+    }
+    const uint32_t fl = __float_as_uint(fin[FIN_FLAGS * 64]);
+    const bool term = fl & 1u, trunc = (fl & 2u) != 0u;
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) F.la[k] = a[k];      // apply_action's drone.last_action
+    const float r = compute_reward(P, F, a, term);
+    const float cost = io.cost ? compute_cost(P, F) : 0.0f;
+    io.rew[i] = r;
+    io.done[i] = (uint8_t)(term || trunc);
+    if (io.trunc) io.trunc[i] = (uint8_t)trunc;
+    if (io.cost) io.cost[i] = cost;
+    if (io.level) io.level[i] = fin[FIN_LEVEL * 64];
+}
+
 enum { SEED_SMALL = 10 };   // per finished env, wave 0 -> waves 1-3: final body rates, gyro bias, OU state
-enum { C2_WORDS = 19 };     // per env, wave 3 -> wave 2: the second call's held[10] and gyro normals[9]
+enum { C2_WORDS = 9 };      // per env, wave 3 -> wave 2: the second reset sensor call's gyro normals
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO io) {
@@ -1847,12 +1936,21 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     __shared__ __align__(16) float s_obs[64 * OD];         // the block's obs rows, global layout
     __shared__ float s_seed[SEED_SMALL * 64];              // [word][env]
     __shared__ float s_c2[C2_WORDS * 64];                  // [word][env]
+    __shared__ __align__(16) float s_rrow[64 * OD];        // speculative reset observation rows
     __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
     __shared__ double s_hjgrid[6 * HJ_PTS];
     // reference-default shape with sensor noise: the helpers also draw the env-step's randomness
     // after its first sub-step (HD_* layout), handed over at an LDS barrier before sub-step 1
     constexpr bool HD = SPEC == 1 && NOISE;
     __shared__ float s_draw[HD ? HD_WORDS * 64 : 1];
+#ifdef CF2_SMALL_OFFLOAD
+    constexpr bool FIN = HD;         // A/B: reward / cost / outputs finished by helper wave 3
+#else
+    // measured slower (32 768 envs 10.3 -> 11.0 us): wave 3's post-barrier outputs lengthened
+    // the reset tail more than they shortened the env wave's epilogue
+    constexpr bool FIN = false;
+#endif
+    __shared__ float s_fin[FIN ? FIN_WORDS * 64 : 1];
 #ifdef CF2_TIMING
     if (uint64_t* r = timing_row()) {
         if ((threadIdx.x & 63) == 0) {
@@ -1869,6 +1967,16 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     const bool live = i < P.N;
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     const Tile T(io.sf, P.N, i);
+    // wave 3: this env's action, loaded at entry for finish_outputs after the barrier
+    float4 act_fin = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (FIN && wave == 3 && live) act_fin = reinterpret_cast<const float4*>(io.act)[i];
+    // domain randomisation / disturbance / level draws of the reset: on wave 1 with wave 3 busy
+    // finishing the outputs, else on wave 3
+#ifndef CF2_SMALL_PARAMS_WAVE
+    constexpr uint32_t PARAMS_WAVE = FIN ? 1u : 3u;
+#else
+    constexpr uint32_t PARAMS_WAVE = CF2_SMALL_PARAMS_WAVE;
+#endif
     Env H;                         // waves 1-3: the speculative reset (kept across the barrier)
     float held1[10], ng1[9];       // wave 2: first reset sensor call
     uint32_t ctr = 0;
@@ -1916,7 +2024,9 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
         __builtin_amdgcn_s_setprio(3);
         bool do_reset = false;
         ResetSeed rs;
-        if (live) do_reset = step_env<NOISE, DR, PHYS, true, HD>(P, io, i, s_obs + lane * OD, rs, s_hjgrid, s_draw + lane);
+        if (live)
+            do_reset = step_env<NOISE, DR, PHYS, true, HD>(P, io, i, s_obs + lane * OD, rs, s_hjgrid, s_draw + lane,
+                                                          FIN ? s_fin + lane : nullptr);
         const uint64_t m = __ballot(do_reset);
         if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
         if (do_reset) {
@@ -1930,25 +2040,42 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
         ctr = (uint32_t)bi(T.ld(G_CORE3).z);
         const Keys K = make_keys(P.key0, P.key1);
         const Rng g{K, ctr, gid, TAG_RESET};
-        if (wave == 1) {
-            reset_kinematics<PHYS>(P, H, g, gid);
-        } else if (wave == 2) {
-            reset_kinematics<PHYS>(P, H, g, gid);
-            if (NOISE) held_measurement(P, H, g, 32, held1, ng1);
-        } else {
+        if (wave == PARAMS_WAVE) {
             const bool need_level = P.need_level || io.level != nullptr;
             H.level = need_level ? T.ld(G_LEVEL).w : P.level_fixed;
             H.level_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
             reset_params<DR>(P, H, g);
+        }
+        if (wave == 1) {
+            reset_kinematics<PHYS>(P, H, g, gid);
+        } else if (wave == 2) {
+            reset_kinematics<PHYS>(P, H, g, gid);
+            // the reset observation row [o_0, A_0, o_1, A_1] as far as it does not depend on the
+            // finished episode: all of it but the two gyro-LPF triples (o_1's held part: wave 3)
+            float* row = s_rrow + lane * OD;
+            if (NOISE) {
+                held_measurement(P, H, g, 32, held1, ng1);
+#pragma unroll
+                for (int k = 0; k < 10; ++k) row[k] = held1[k];
+            } else {
+                const float o[17] = {H.p[0], H.p[1], H.p[2], H.q[0], H.q[1], H.q[2], H.q[3], H.v[0], H.v[1],
+                                     H.v[2], H.wb[0], H.wb[1], H.wb[2], H.la[0], H.la[1], H.la[2], H.la[3]};
+#pragma unroll
+                for (int k = 0; k < 17; ++k) { row[k] = o[k]; row[OL + 4 + k] = o[k]; }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { row[OL + k] = H.la[k]; row[2 * OL + 4 + k] = H.la[k]; }
+        } else {
             if (NOISE) {
                 Env H2;
                 reset_kinematics<PHYS>(P, H2, g, gid);
                 float held2[10], ng2[9];
                 held_measurement(P, H2, g, 40, held2, ng2);
+                float* row = s_rrow + lane * OD;
 #pragma unroll
-                for (int k = 0; k < 10; ++k) s_c2[k * 64 + lane] = held2[k];
+                for (int k = 0; k < 10; ++k) row[OL + 4 + k] = held2[k];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) s_c2[(10 + k) * 64 + lane] = ng2[k];
+                for (int k = 0; k < 9; ++k) s_c2[k * 64 + lane] = ng2[k];
             }
         }
         TREADY("v"(H.p[0]), "v"(H.K[3]), "v"(H.la[3]));
@@ -1968,53 +2095,46 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
             const float ou[4] = {s_seed[6 * 64 + lane], s_seed[7 * 64 + lane], s_seed[8 * 64 + lane], s_seed[9 * 64 + lane]};
             store_reset_kinematics<PHYS>(P, T, H, ou, ctr);
         } else if (wave == 2) {
-            // the reset observation (reset_observe: two sensor calls, then the history row)
+            // the reset observation (reset_observe: two sensor calls, then the history row): the
+            // gyro-LPF triples of o_0 and o_1 complete the staged row
             Env& E = H;
-            float* row = s_obs + lane * OD;
+            float* row = s_rrow + lane * OD;
             if (NOISE) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) { E.lpf[k] = s_seed[k * 64 + lane]; E.bias[k] = s_seed[(3 + k) * 64 + lane]; }
-                gyro_update(P, E, ng1);
-#pragma unroll
-                for (int k = 0; k < 10; ++k) row[k] = held1[k];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) row[10 + k] = E.lpf[k];
                 float ng2[9];
 #pragma unroll
-                for (int k = 0; k < 10; ++k) E.held[k] = s_c2[k * 64 + lane];
+                for (int k = 0; k < 9; ++k) ng2[k] = s_c2[k * 64 + lane];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) ng2[k] = s_c2[(10 + k) * 64 + lane];
+                for (int k = 0; k < 10; ++k) E.held[k] = row[OL + 4 + k];
+                gyro_update(P, E, ng1);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) row[10 + k] = E.lpf[k];
                 gyro_update(P, E, ng2);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) row[OL + 4 + 10 + k] = E.lpf[k];
 #pragma unroll
                 for (int k = 0; k < 10; ++k) E.obs_prev[k] = E.held[k];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) E.obs_prev[10 + k] = E.lpf[k];
             } else {
-                // noise off: the observation is the state (compute_observation<false>)
-                const float o[17] = {E.p[0], E.p[1], E.p[2], E.q[0], E.q[1], E.q[2], E.q[3], E.v[0], E.v[1],
-                                     E.v[2], E.wb[0], E.wb[1], E.wb[2], E.la[0], E.la[1], E.la[2], E.la[3]};
 #pragma unroll
-                for (int k = 0; k < 17; ++k) { row[k] = o[k]; E.obs_prev[k] = o[k]; }
+                for (int k = 0; k < OL; ++k) E.obs_prev[k] = row[OL + 4 + k];
             }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) row[OL + k] = E.la[k];
-#pragma unroll
-            for (int k = 0; k < OL; ++k) row[OL + 4 + k] = E.obs_prev[k];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) row[2 * OL + 4 + k] = E.la[k];
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) E.hact[s2][k] = E.la[k];
             store_reset_history<NOISE>(P, T, E);
             TSTAMP(8);
-        } else {
-            store_reset_params<DR>(P, T, H);
         }
+        if (wave == PARAMS_WAVE) store_reset_params<DR>(P, T, H);
     }
+    if (FIN && wave == 3 && live) finish_outputs(P, io, i, s_fin + lane, act_fin);
     lds_barrier();
     TSTAMP(12);  // reset rows in LDS
-    write_obs_rows(io.obs + (size_t)base * OD, s_obs, P.N - base < 64u ? P.N - base : 64u, 64u, OD, tid, 256u);
+    write_obs_rows_merged<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, P.N - base < 64u ? P.N - base : 64u,
+                              tid, 256u);
 #ifdef CF2_TIMING
     TSTAMP(5);
     if (uint64_t* r = timing_row())
@@ -2303,6 +2423,9 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 // ------------------------------------------------------------------------------------
 // host-side launch table
 // ------------------------------------------------------------------------------------
+#ifndef CF2_NT_STATE_BYTES
+#define CF2_NT_STATE_BYTES (240u << 20)   // working-set bytes (762 B per env-step) above which state stores are nt
+#endif
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
     // small N (<= 32768 envs: at most one 64-env wave per two SIMDs with the helpers) runs 64 envs
@@ -2331,6 +2454,14 @@ static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t 
     KParams Pl = P;
     Pl.late_block = (uint32_t)round_blocks;
     Pl.epb = epb;
+#ifndef CF2_NO_NT_STATE
+    // the env state (480 B per env) plus the step's I/O no longer fit the 256 MB Infinity Cache
+    // between env-steps: stream the state stores past it (nt), HBM-bound regime
+    if ((uint64_t)P.N * 762u > (uint64_t)CF2_NT_STATE_BYTES) {
+        hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC, 2>), grid, block, 0, s, Pl, io);
+        return hipGetLastError();
+    }
+#endif
     hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, Pl, io);
     return hipGetLastError();
 }
