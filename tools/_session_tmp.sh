@@ -1,10 +1,9 @@
 set -o pipefail
-O=gpurun_out/r03g
+O=gpurun_out/r03h
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for v in full_pw1 full_pw3; do
-  CF2SIM_LIB=build_ab/$v.so timeout -k 10 300 python -u -m pytest tests/test_rollout_fused.py tests/test_gpu_parity.py -q --timeout 120 --timeout-method thread > $O/pytest_$v.log 2>&1; echo "$v rc=$?"; tail -3 $O/pytest_$v.log
-done
-timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; echo "intree rc=$?"; tail -3 $O/pytest_gpu.log
-timeout -k 10 900 bash tools/ab_envs.sh "DroneHoverBulletFreeEnvWithConstWind-v0:4096 DroneHoverBulletFreeEnvWithGust-v0:32768" build_ab/hd_prev.so build_ab/nofin.so build_ab/bal.so 2>&1 | tee $O/ab.txt
-timeout -k 10 900 bash tools/ab_envs.sh "DroneHoverBulletFreeEnvWithGust-v0:262144 DroneHoverBulletFreeEnvWithGust-v0:1048576" build_ab/bal.so build_ab/nt_ld.so build_ab/nt_st.so build_ab/nt_both.so 2>&1 | tee $O/ab_nt.txt
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 900 bash tools/ab_envs.sh "DroneHoverBulletFreeEnvWithGust-v0:393216 DroneHoverBulletFreeEnvWithGust-v0:327680" build_ab/cur.so build_ab/nt_st.so 2>&1 | tee $O/ab_nt2.txt
