@@ -399,12 +399,16 @@ __device__ __forceinline__ void write_obs_rows_merged(float* dst, const float* s
         const f4x* b4 = reinterpret_cast<const f4x*>(s_rrow);
         f4x* dst4 = reinterpret_cast<f4x*>(dst);
         for (uint32_t k = tid; k < 64u * OD / 4; k += nthreads) {
-            f4x v = a4[k];
-            if (mask) {
-                const f4x w = b4[k];
+            // the chunk's 4 floats lie in row r0, or straddle rows r0 and r0 + 1 (OD > 4)
+            const uint32_t r0 = 4u * k / OD, r1 = (4u * k + 3u) / OD;
+            const bool s0 = (mask >> r0) & 1ull, s1 = (mask >> r1) & 1ull;
+            f4x v = (s0 ? b4 : a4)[k];
+            if (s0 != s1) {
+                const f4x w = (s1 ? b4 : a4)[k];
+                const uint32_t cut = r1 * OD - 4u * k;        // first component of row r1
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if ((mask >> ((4u * k + (uint32_t)j) / OD)) & 1ull) v[j] = w[j];
+                for (uint32_t j = 1; j < 4; ++j)
+                    if (j >= cut) v[j] = w[j];
             }
             __builtin_nontemporal_store(v, dst4 + k);
         }
@@ -873,10 +877,14 @@ __device__ __forceinline__ void omega_noise(const KParams& P, Env& E, const floa
 // A full measurement's held part (noisy position, attitude quaternion and velocity,
 // sensors.py:75-118) and its 9 gyro normals n[6..15) (bias walk, white noise, turn-on noise): what
 // the measurement draws from stream blocks base..base+5.  The gyro part is applied by
-// gyro_update, which needs the body rates, bias and LPF state of the moment.
+// gyro_update, which needs the body rates, bias and LPF state of the moment.  Split in two so the
+// draws can run before the state they perturb is known (the small-N kernel's helper waves):
+// held_noise turns the draws into the position / velocity / rpy perturbations, held_combine adds
+// them.  The velocity perturbation is rounded on its own (no fma into the sum), as the fp32
+// restatement computes v + vel_std * n.
+struct HeldNoise { float pn[3], vn[3], th[3]; };
 template <class G>
-__device__ __forceinline__ void held_measurement(const KParams& P, const Env& E, const G& g, uint32_t base,
-                                                 float held[10], float ng[9]) {
+__device__ __forceinline__ void held_noise(const KParams& P, const G& g, uint32_t base, HeldNoise& h, float ng[9]) {
     float n[18];
     normals<18>(g, base, n);
     const U4 ua = g.block(base + 4), ub = g.block(base + 5);
@@ -884,21 +892,35 @@ __device__ __forceinline__ void held_measurement(const KParams& P, const Env& E,
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float uo = -P.pos_unif + (P.pos_unif - -P.pos_unif) * u01(up[k]);
-        held[k] = E.p[k] + (P.pos_std * n[k] + uo);
+        h.pn[k] = P.pos_std * n[k] + uo;
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) held[7 + k] = E.v[k] + P.vel_std * n[3 + k] + 0.0f;
-    const float lo[3] = {-3.141592653589793f, -1.5707963267948966f, -3.141592653589793f};
-    float rot[3];
+    for (int k = 0; k < 3; ++k) h.vn[k] = opaque(P.vel_std * n[3 + k]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const float uo = -P.rot_unif + (P.rot_unif - -P.rot_unif) * u01(ur[k]);
-        const float th = P.rot_std * n[15 + k] + uo;
-        rot[k] = clampf(E.rpy[k] + th, lo[k], -lo[k]);
+        h.th[k] = P.rot_std * n[15 + k] + uo;
     }
-    quat_from_euler_obs(rot, held + 3);
 #pragma unroll
     for (int k = 0; k < 9; ++k) ng[k] = n[6 + k];
+}
+__device__ __forceinline__ void held_combine(const Env& E, const HeldNoise& h, float held[10]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) held[k] = E.p[k] + h.pn[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) held[7 + k] = E.v[k] + h.vn[k] + 0.0f;
+    const float lo[3] = {-3.141592653589793f, -1.5707963267948966f, -3.141592653589793f};
+    float rot[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rot[k] = clampf(E.rpy[k] + h.th[k], lo[k], -lo[k]);
+    quat_from_euler_obs(rot, held + 3);
+}
+template <class G>
+__device__ __forceinline__ void held_measurement(const KParams& P, const Env& E, const G& g, uint32_t base,
+                                                 float held[10], float ng[9]) {
+    HeldNoise h;
+    held_noise(P, g, base, h, ng);
+    held_combine(E, h, held);
 }
 
 // gyro of one sensor call: bias walk + noise on the body rates, then the gyro low-pass filter
@@ -1973,20 +1995,41 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     // domain randomisation / disturbance / level draws of the reset: on wave 1 with wave 3 busy
     // finishing the outputs, else on wave 3
 #ifndef CF2_SMALL_PARAMS_WAVE
-    constexpr uint32_t PARAMS_WAVE = FIN ? 1u : 3u;
+    constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
 #else
     constexpr uint32_t PARAMS_WAVE = CF2_SMALL_PARAMS_WAVE;
 #endif
+#ifdef CF2_SMALL_PARAMS_EARLY
+    constexpr bool PARAMS_EARLY = HD;    // A/B: the DR draws before the draw barrier
+#else
+    constexpr bool PARAMS_EARLY = false;
+#endif
     Env H;                         // waves 1-3: the speculative reset (kept across the barrier)
     float held1[10], ng1[9];       // wave 2: first reset sensor call
+    HeldNoise hn;                  // waves 2 / 3: the noise of the first / second reset sensor call
+    float ngs[9];                  //   and its gyro normals
     uint32_t ctr = 0;
+    if (wave != 0 && live) ctr = (uint32_t)bi(T.ld(G_CORE3).z);      // the env's counter (step and reset draws)
+    const Keys K = make_keys(P.key0, P.key1);
+    const Rng gr{K, ctr, gid, TAG_RESET};
+    // the speculative reset's work that needs no reset pose: DR / disturbance / level draws (wave
+    // PARAMS_WAVE) and the two reset sensor calls' noise (waves 2, 3).  Measured: all of it before
+    // the draw barrier (in the time the helpers wait there) made the env wave wait at that barrier
+    // (32 768 envs 10.6 -> 11.2 us); CF2_SMALL_PARAMS_EARLY moves only the DR draws there
+    auto reset_prework = [&](bool before_draw_barrier) {
+        if (wave == PARAMS_WAVE && before_draw_barrier == PARAMS_EARLY) {
+            const bool need_level = P.need_level || io.level != nullptr;
+            H.level = need_level ? T.ld(G_LEVEL).w : P.level_fixed;
+            H.level_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
+            reset_params<DR>(P, H, gr);
+        }
+        if (NOISE && wave >= 2 && !before_draw_barrier) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
+    };
     if (HD && wave != 0) {
         // the env-step's draws after sub-step 0 (step tag, the env's counter), split over the
         // three helper waves; Box-Muller applied where the env-step turns words into normals
         if (live) {
-            const uint32_t sctr = (uint32_t)bi(T.ld(G_CORE3).z);
-            const Keys K = make_keys(P.key0, P.key1);
-            const Rng g{K, sctr, gid, TAG_STEP};
+            const Rng g{K, ctr, gid, TAG_STEP};
             float* d = s_draw + lane;
             auto bm4 = [&](uint32_t blk, int w) {          // 4 normals of one block -> words w..w+3
                 const U4 u = g.block(blk);
@@ -2017,8 +2060,11 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
                 d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
                 d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
             }
+            if (P.auto_reset && PARAMS_EARLY) reset_prework(true);
         }
+        TSTAMP(10);      // helper: step draws in LDS
         lds_barrier();   // joined by the env wave before its second sub-step (step_env_body)
+        TSTAMP(11);
     }
     if (wave == 0) {
         __builtin_amdgcn_s_setprio(3);
@@ -2037,24 +2083,18 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
         }
     } else if (P.auto_reset && live) {
         __builtin_amdgcn_s_setprio(0);
-        ctr = (uint32_t)bi(T.ld(G_CORE3).z);
-        const Keys K = make_keys(P.key0, P.key1);
-        const Rng g{K, ctr, gid, TAG_RESET};
-        if (wave == PARAMS_WAVE) {
-            const bool need_level = P.need_level || io.level != nullptr;
-            H.level = need_level ? T.ld(G_LEVEL).w : P.level_fixed;
-            H.level_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
-            reset_params<DR>(P, H, g);
-        }
+        reset_prework(false);
         if (wave == 1) {
-            reset_kinematics<PHYS>(P, H, g, gid);
+            reset_kinematics<PHYS>(P, H, gr, gid);
         } else if (wave == 2) {
-            reset_kinematics<PHYS>(P, H, g, gid);
+            reset_kinematics<PHYS>(P, H, gr, gid);
             // the reset observation row [o_0, A_0, o_1, A_1] as far as it does not depend on the
             // finished episode: all of it but the two gyro-LPF triples (o_1's held part: wave 3)
             float* row = s_rrow + lane * OD;
             if (NOISE) {
-                held_measurement(P, H, g, 32, held1, ng1);
+                held_combine(H, hn, held1);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) ng1[k] = ngs[k];
 #pragma unroll
                 for (int k = 0; k < 10; ++k) row[k] = held1[k];
             } else {
@@ -2065,18 +2105,16 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) { row[OL + k] = H.la[k]; row[2 * OL + 4 + k] = H.la[k]; }
-        } else {
-            if (NOISE) {
-                Env H2;
-                reset_kinematics<PHYS>(P, H2, g, gid);
-                float held2[10], ng2[9];
-                held_measurement(P, H2, g, 40, held2, ng2);
-                float* row = s_rrow + lane * OD;
+        } else if (NOISE) {
+            Env H2;
+            reset_kinematics<PHYS>(P, H2, gr, gid);
+            float held2[10];
+            held_combine(H2, hn, held2);
+            float* row = s_rrow + lane * OD;
 #pragma unroll
-                for (int k = 0; k < 10; ++k) row[OL + 4 + k] = held2[k];
+            for (int k = 0; k < 10; ++k) row[OL + 4 + k] = held2[k];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) s_c2[k * 64 + lane] = ng2[k];
-            }
+            for (int k = 0; k < 9; ++k) s_c2[k * 64 + lane] = ngs[k];
         }
         TREADY("v"(H.p[0]), "v"(H.K[3]), "v"(H.la[3]));
         TSTAMP(9);   // helper: speculative reset computed

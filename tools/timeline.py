@@ -89,6 +89,18 @@ def main():
         h0, h9, h4 = (t[hw_, 3 + k].astype(np.float64) for k in (0, 9, 1 + 3))
         print(f"  small-N helper waves {int(hw_.sum())}: speculative reset {np.mean(h9 - h0):.0f} "
               f"(p90 {np.percentile(h9 - h0, 90):.0f}), wait at barrier {np.mean(h4 - h9):.0f}")
+        if (t[hw_, 13] != 0).all():
+            h10, h11 = t[hw_, 13].astype(np.float64), t[hw_, 14].astype(np.float64)
+            e_a = t[envw, 3:8].astype(np.float64)
+            print(f"  small-N helpers: entry->draws in LDS {np.mean(h10 - h0):.0f} (p90 {np.percentile(h10 - h0, 90):.0f}), "
+                  f"wait at draw barrier {np.mean(h11 - h10):.0f}, after it -> reset computed {np.mean(h9 - h11):.0f} "
+                  f"(p90 {np.percentile(h9 - h11, 90):.0f})")
+        b2 = hw_ & (t[:, 11] != 0)          # wave-2 helpers that finished a reset row (stamps 6, 8)
+        if b2.any():
+            c4, c6, c8, c12, c5 = (t[b2, 3 + k].astype(np.float64) for k in (4, 6, 8, 12, 2))
+            print(f"  small-N wave-2 resets {int(b2.sum())}: barrier->start {np.mean(c6 - c4):.0f}, "
+                  f"gyro+rows+stores {np.mean(c8 - c6):.0f} (p90 {np.percentile(c8 - c6, 90):.0f}), "
+                  f"->barrier passed {np.mean(c12 - c8):.0f}, write-out {np.mean(t[b2, 8] - t[b2, 15]):.0f}")
     print(f"waves {n_waves}; span {rend.max():.0f} cycles (realtime x24); per XCD end: " +
           " ".join(f"{x}:{rend[xcc == x].max():.0f}" for x in range(8) if (xcc == x).any()))
     print("  per XCD first/last wave start: " +
