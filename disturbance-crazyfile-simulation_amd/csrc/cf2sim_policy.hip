@@ -99,26 +99,45 @@ __device__ float w_l3(const float* __restrict__ W, int n, int in) {
     return n == 4 ? W[L::V_W3 + in - 64] : 0.0f;
 }
 
+#ifndef CF2_POLICY_SLOT1
+#define CF2_POLICY_SLOT1 0     // measured 35.0 vs 34.2 us at 262 144 rows: the kernel is VALU-, not MFMA-bound
+#endif
 // Packed block layout (floats).  fp32 fragments: 64 floats (lane l: A[16nt + (l&15)][k slot l>>4]).
 // bf16 fragments: 512 floats = hi[64 lanes][8 bf16] then lo[64 lanes][8 bf16] (lane l: k slots
 // 8(l>>4) .. 8(l>>4)+7).  Layer 1 in bf16x3 mode: D/32 bf16 blocks + fp32 k-steps for the rest.
 template <int D, int PREC>
 struct Packed {
     static constexpr bool BF = PREC == CF2_POLICY_BF16X3;
-    static constexpr int KS1 = BF ? (D % 32 + 3) / 4 : (D + 3) / 4;     // fp32 k-steps of layer 1
     static constexpr int KB1 = BF ? D / 32 : 0;                          // bf16 k-blocks of layer 1
-    static constexpr int K1R = 32 * KB1;                                 // first fp32 input of layer 1
+    static constexpr int K1R = 32 * KB1;                                 // first input past them
+    static constexpr int R1 = D - K1R;                                   // layer-1 inputs left over
+    // bf16x3 with <= 2 left-over inputs (D = 34): their three split products hi*hi, lo_x*hi_w,
+    // hi_x*lo_w share ONE bf16 MFMA per n-tile (k slots 0..3 R1-1 of lane group 0; a hi-only
+    // fragment, FS floats) instead of fp32 k-steps (16 against 32 cycles per n-tile)
+    static constexpr bool SL = BF && R1 > 0 && 3 * R1 <= 8 && CF2_POLICY_SLOT1;
+    static constexpr int KS1 = SL ? 0 : (BF ? (R1 + 3) / 4 : (D + 3) / 4);   // fp32 k-steps of layer 1
     static constexpr int KSP = ksteps(50), KSV = ksteps(64);
-    static constexpr int FB = 512, FF = 64;
-    static constexpr int O_L1B = 0, O_L1F = O_L1B + KB1 * 8 * FB, O_L2P = O_L1F + KS1 * 8 * FF;
+    static constexpr int FB = 512, FF = 64, FS = 256;
+    static constexpr int O_L1B = 0, O_L1F = O_L1B + KB1 * 8 * FB, O_L2P = O_L1F + KS1 * 8 * FF + (SL ? 8 * FS : 0);
     static constexpr int N_L2 = BF ? 2 * 4 * FB : 0;
     static constexpr int O_L2V = O_L2P + (BF ? N_L2 : KSP * 4 * FF);
     static constexpr int O_L3 = O_L2V + (BF ? N_L2 : KSV * 4 * FF);
     static constexpr int O_BIAS = O_L3 + (BF ? 4 * FB : (KSP + KSV) * FF);
     static constexpr int B_L1 = 0, B_L2P = 128, B_L2V = 192, B_L3 = 256, NB = 272;   // neuron-ordered biases
-    static constexpr int O_LOGSTD = O_BIAS + NB, O_MEAN = O_LOGSTD + 4, O_SCALE = O_MEAN + D;
+    static constexpr int O_LOGSTD = O_BIAS + NB, O_MEAN = O_LOGSTD + 4, O_SCALE = O_MEAN + (D + 3) / 4 * 4;
     static constexpr int TOTAL = (O_SCALE + D + 3) / 4 * 4;
 };
+
+// bf16x3 mode packs the v network's layer-1 and layer-2 weights and biases multiplied by
+// TANH_PRESCALE = -2 log2(e), so that its tanh needs no scaling (tanh_prescaled below)
+#ifndef CF2_POLICY_TANH_PRESCALE
+#define CF2_POLICY_TANH_PRESCALE 1
+#endif
+constexpr float TANH_PRESCALE = -2.8853900817779268f;
+template <int PREC>
+__device__ __forceinline__ float v_prescale(bool v_pre_tanh) {
+    return (PREC == CF2_POLICY_BF16X3 && CF2_POLICY_TANH_PRESCALE && v_pre_tanh) ? TANH_PRESCALE : 1.0f;
+}
 
 template <int D>
 __device__ float bias_value(const float* __restrict__ W, int k) {
@@ -158,8 +177,9 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, 
         const int f = rel / P::FB, w = rel % P::FB, half = w / 256, lw = w % 256, l = lw / 4, pr = lw % 4;
         const int kb = f / nblk, nt = f % nblk;
         uint32_t bits = 0;
+        const bool vt = layer == 3 || (layer == 1 && nt >= 4);     // v neurons before a tanh
         for (int e = 0; e < 2; ++e) {
-            const float x = bf16_weight<D>(W, layer, kb, nt, l, 2 * pr + e);
+            const float x = bf16_weight<D>(W, layer, kb, nt, l, 2 * pr + e) * v_prescale<PREC>(vt);
             const float hi = (float)(__bf16)x;
             bits |= (half ? bf16_bits(x - hi) : bf16_bits(x)) << (16 * e);
         }
@@ -167,9 +187,21 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, 
     };
     if (k < P::O_L1F) {
         v = bfword(1, k - P::O_L1B, 8);
+    } else if (k < P::O_L2P && P::SL) {
+        // slot s of lane group 0: s < R1 hi(w), s < 2 R1 hi(w) (times lo(x)), s < 3 R1 lo(w)
+        const int r = k - P::O_L1F, nt = r / P::FS, w = r % P::FS, l = w / 4, pr = w % 4;
+        uint32_t bits = 0;
+        for (int e = 0; e < 2; ++e) {
+            const int sl = 2 * pr + e;
+            if ((l >> 4) != 0 || sl >= 3 * P::R1) continue;
+            const float x = w_l1<D>(W, 16 * nt + (l & 15), P::K1R + sl % P::R1) * v_prescale<PREC>(nt >= 4);
+            const float hi = (float)(__bf16)x;
+            bits |= (sl < 2 * P::R1 ? bf16_bits(x) : bf16_bits(x - hi)) << (16 * e);
+        }
+        v = __uint_as_float(bits);
     } else if (k < P::O_L2P) {
         const int r = k - P::O_L1F, f = r / 64, l = r % 64, ks = f / 8, nt = f % 8;
-        v = w_l1<D>(W, 16 * nt + (l & 15), P::K1R + 4 * ks + (l >> 4));
+        v = w_l1<D>(W, 16 * nt + (l & 15), P::K1R + 4 * ks + (l >> 4)) * v_prescale<PREC>(nt >= 4);
     } else if (k < P::O_L2V) {
         const int r = k - P::O_L2P;
         if (P::BF) {
@@ -196,11 +228,12 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, 
                             : w_l3<D>(W, n, 64 + 16 * kstep_t(64, ks - P::KSP) + 4 * g + kstep_i(64, ks - P::KSP));
         }
     } else if (k < P::O_LOGSTD) {
-        v = bias_value<D>(W, k - P::O_BIAS);
+        const int b = k - P::O_BIAS;
+        v = bias_value<D>(W, b) * v_prescale<PREC>((b >= 64 && b < 128) || (b >= P::B_L2V && b < P::B_L3));
     } else if (k < P::O_MEAN) {
         v = W[PolicyLayout<D>::P_LOGSTD + (k - P::O_LOGSTD)];
     } else if (k < P::O_SCALE) {
-        v = W[PolicyLayout<D>::O_MEAN + (k - P::O_MEAN)];
+        v = k - P::O_MEAN < D ? W[PolicyLayout<D>::O_MEAN + (k - P::O_MEAN)] : 0.0f;     // 16-B aligned rows
     } else if (k < P::O_SCALE + D) {
         v = W[PolicyLayout<D>::O_SCALE + (k - P::O_SCALE)];
     }
@@ -217,12 +250,34 @@ __device__ __forceinline__ f4v mfma3(const bf8v& ah, const bf8v& al, const bf8v&
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
 }
 // x -> (hi, lo) bf16 operands
+#ifndef CF2_POLICY_PAIRCVT
+#define CF2_POLICY_PAIRCVT 1
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void split8(const float (&x)[8], bf8v& hi, bf8v& lo) {
+#if CF2_POLICY_PAIRCVT
+    // two values per v_cvt_pk_bf16_f32: hi pair, its two fp32 values by shift / mask, the two
+    // remainders, lo pair (6 VALU per pair; per-value conversions cost ~8)
+    u4v h, o;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const f2v v = {x[2 * p], x[2 * p + 1]};
+        const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf2v));
+        const f2v r = {v.x - __uint_as_float(hb << 16), v.y - __uint_as_float(hb & 0xffff0000u)};
+        h[p] = hb;
+        o[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf2v));
+    }
+    hi = __builtin_bit_cast(bf8v, h);
+    lo = __builtin_bit_cast(bf8v, o);
+#else
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         hi[j] = (__bf16)x[j];
         lo[j] = (__bf16)(x[j] - (float)hi[j]);
     }
+#endif
 }
 // B operand of k-block (t0, t0 + 1) from two C-layout tiles
 __device__ __forceinline__ void split_tiles(const f4v& a, const f4v& b, bf8v& hi, bf8v& lo) {
@@ -240,6 +295,22 @@ __device__ __forceinline__ void ld_frag(const float* sw, int off, int l, bf8v& h
 __device__ __forceinline__ float tanh_fast(float x) {
     const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * fabsf(x));   // exp(2|x|)
     return __builtin_copysignf(1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f), x);
+}
+// tanh(z) from y = -2 log2(e) z (the v network's layer-1 and layer-2 weights and biases are packed
+// pre-multiplied by TANH_PRESCALE in bf16x3 mode): 2 / (1 + 2^y) - 1, 4 VALU against 6.  Saturates
+// correctly (2^y -> inf: -1; 2^y -> 0: 1); absolute error ~2e-7 near 0, as tanh_fast.
+__device__ __forceinline__ float tanh_prescaled(float y) {
+    return fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y)), -1.0f);
+}
+// ReLU as an integer max on the bits (negative floats, -0 included, are negative integers): one
+// v_max_i32; fmaxf(x, 0) on an MFMA result costs two v_max_f32 (IEEE-mode NaN quieting first)
+__device__ __forceinline__ float relu(float x) {
+    return __int_as_float(__builtin_elementwise_max(__float_as_int(x), 0));
+}
+template <int PREC>
+__device__ __forceinline__ float tanh_act(float x) {
+    if constexpr (PREC == CF2_POLICY_BF16X3 && CF2_POLICY_TANH_PRESCALE) return tanh_prescaled(x);
+    else return tanh_fast(x);
 }
 
 enum : uint32_t { TAG_POLICY = 3 };
@@ -269,7 +340,8 @@ template <int D, int PREC>
 struct ObsRegs {
     using P = Packed<D, PREC>;
     float x8[RT][P::KB1 > 0 ? P::KB1 : 1][8];
-    float x1[RT][P::KS1];
+    float x1[RT][P::KS1 > 0 ? P::KS1 : 1];
+    float xr[RT][P::SL ? P::R1 : 1];
 };
 template <int D, int PREC>
 __device__ __forceinline__ void load_obs(const float* __restrict__ obs, uint32_t n, uint32_t r0, int l,
@@ -290,6 +362,9 @@ __device__ __forceinline__ void load_obs(const float* __restrict__ obs, uint32_t
 #pragma unroll
         for (int ks = 0; ks < P::KS1; ++ks)
             X.x1[rt][ks] = src[__builtin_elementwise_min(P::K1R + 4 * ks + (l >> 4), D - 1)];
+        if constexpr (P::SL)
+#pragma unroll
+            for (int r = 0; r < P::R1; ++r) X.xr[rt][r] = src[P::K1R + r];
     }
 }
 
@@ -341,7 +416,20 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
         sd[k] = __builtin_amdgcn_exp2f(1.4426950408889634f * ls[k]);
     }
     // this lane's standardisation constants (its input indices do not change between chunks)
-    float mean8[P::KB1 > 0 ? P::KB1 : 1][8], scale8[P::KB1 > 0 ? P::KB1 : 1][8], mean1[P::KS1], scale1[P::KS1];
+    // (the k-block constants are re-read from LDS per chunk, CF2_POLICY_STD_LDS: 16 fewer live VGPRs)
+#ifndef CF2_POLICY_STD_LDS
+#define CF2_POLICY_STD_LDS 1
+#endif
+    float mean8[P::KB1 > 0 ? P::KB1 : 1][8], scale8[P::KB1 > 0 ? P::KB1 : 1][8], mean1[P::KS1 > 0 ? P::KS1 : 1],
+        scale1[P::KS1 > 0 ? P::KS1 : 1], meanr[P::SL ? P::R1 : 1], scaler[P::SL ? P::R1 : 1];
+    if constexpr (P::SL)
+#pragma unroll
+        for (int r = 0; r < P::R1; ++r) {
+            meanr[r] = s_w[P::O_MEAN + P::K1R + r];
+            scaler[r] = s_w[P::O_SCALE + P::K1R + r];
+        }
+    const uint32_t g0 = g == 0 ? 0xffffffffu : 0u;      // slot-mode B operand lives in lane group 0
+#if !CF2_POLICY_STD_LDS
 #pragma unroll
     for (int kb = 0; kb < P::KB1; ++kb)
 #pragma unroll
@@ -349,6 +437,7 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
             mean8[kb][j] = s_w[P::O_MEAN + 32 * kb + 8 * g + j];
             scale8[kb][j] = s_w[P::O_SCALE + 32 * kb + 8 * g + j];
         }
+#endif
 #pragma unroll
     for (int ks = 0; ks < P::KS1; ++ks) {
         const int k = __builtin_elementwise_min(P::K1R + 4 * ks + g, D - 1);
@@ -372,6 +461,17 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
         asm volatile("" : "+v"(off));
         const float* sw = s_w + off;
         ObsRegs<D, PREC> Xc = X;
+#if CF2_POLICY_STD_LDS
+#pragma unroll
+        for (int kb = 0; kb < P::KB1; ++kb)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float4 m = *reinterpret_cast<const float4*>(&sw[P::O_MEAN + 32 * kb + 8 * g + 4 * q]);
+                const float4 sc = *reinterpret_cast<const float4*>(&sw[P::O_SCALE + 32 * kb + 8 * g + 4 * q]);
+                mean8[kb][4 * q] = m.x; mean8[kb][4 * q + 1] = m.y; mean8[kb][4 * q + 2] = m.z; mean8[kb][4 * q + 3] = m.w;
+                scale8[kb][4 * q] = sc.x; scale8[kb][4 * q + 1] = sc.y; scale8[kb][4 * q + 2] = sc.z; scale8[kb][4 * q + 3] = sc.w;
+            }
+#endif
         // observation standardisation (obs - mean) * scale, per input index of this lane
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
@@ -381,6 +481,9 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
                 for (int j = 0; j < 8; ++j) Xc.x8[rt][kb][j] = (Xc.x8[rt][kb][j] - mean8[kb][j]) * scale8[kb][j];
 #pragma unroll
             for (int ks = 0; ks < P::KS1; ++ks) Xc.x1[rt][ks] = (Xc.x1[rt][ks] - mean1[ks]) * scale1[ks];
+            if constexpr (P::SL)
+#pragma unroll
+                for (int r = 0; r < P::R1; ++r) Xc.xr[rt][r] = (Xc.xr[rt][r] - meanr[r]) * scaler[r];
         }
         // prefetch the next chunk's observations while this one runs on the matrix cores
         if (MODE == 0 && c + nwaves < nchunks) load_obs<D, PREC>(obs, n, (c + nwaves) * CHUNK, l, X);
@@ -414,12 +517,45 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = mfma4(a, Xc.x1[rt][ks], h1[nt][rt]);
             }
+        if constexpr (P::SL) {
+            bf8v bs[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                uint16_t hb[P::R1], lb[P::R1];
+#pragma unroll
+                for (int r = 0; r < P::R1; ++r) {
+                    const __bf16 h = (__bf16)Xc.xr[rt][r];
+                    hb[r] = __builtin_bit_cast(uint16_t, h);
+                    lb[r] = __builtin_bit_cast(uint16_t, (__bf16)(Xc.xr[rt][r] - (float)h));
+                }
+                u4v wds;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t wq = 0;
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int sl = 2 * q + e;
+                        const uint32_t v = sl < P::R1 ? hb[sl] : sl < 2 * P::R1 ? lb[sl - P::R1]
+                                         : sl < 3 * P::R1 ? hb[sl - 2 * P::R1] : 0u;
+                        wq |= v << (16 * e);
+                    }
+                    wds[q] = wq & g0;
+                }
+                bs[rt] = __builtin_bit_cast(bf8v, wds);
+            }
+#pragma unroll
+            for (int nt = NT0; nt < 8; ++nt) {
+                const bf8v a = __builtin_bit_cast(bf8v, *reinterpret_cast<const float4*>(sw + P::O_L1F + nt * P::FS + 4 * l));
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bs[rt], h1[nt][rt], 0, 0, 0);
+            }
+        }
 #pragma unroll
         for (int nt = NT0; nt < 8; ++nt)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) h1[nt][rt][i] = nt < 4 ? fmaxf(h1[nt][rt][i], 0.0f) : tanh_fast(h1[nt][rt][i]);
+                for (int i = 0; i < 4; ++i) h1[nt][rt][i] = nt < 4 ? relu(h1[nt][rt][i]) : tanh_act<PREC>(h1[nt][rt][i]);
         // ---- layer 2: pi 50 -> 50 (ReLU), v 64 -> 64 (tanh); inputs straight from the layer-1 accumulators
         f4v h2p[4][RT], h2v[4][RT];
 #pragma unroll
@@ -468,8 +604,8 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    if (PI) h2p[nt][rt][i] = fmaxf(h2p[nt][rt][i], 0.0f);
-                    h2v[nt][rt][i] = tanh_fast(h2v[nt][rt][i]);
+                    if (PI) h2p[nt][rt][i] = relu(h2p[nt][rt][i]);
+                    h2v[nt][rt][i] = tanh_act<PREC>(h2v[nt][rt][i]);
                 }
         // ---- layer 3: one n-tile, rows 0..3 = mu, row 4 = v
         f4v o[RT];
@@ -538,7 +674,11 @@ static int policy_grid(uint32_t n) {
     const uint32_t want = (n + PW * CHUNK - 1) / (PW * CHUNK);
     // resident blocks per CU: LDS (~58-62 KB of fragments per block) and the wave budget
     const uint32_t by_waves = (uint32_t)(4 * CF2_POLICY_WAVES / PW);
-    const uint32_t per_cu = by_waves < 2u ? (by_waves ? by_waves : 1u) : 2u;
+#ifndef CF2_POLICY_PER_CU
+#define CF2_POLICY_PER_CU 2u     // resident blocks per CU the persistent grid is sized for
+#endif
+    const uint32_t cap_cu = CF2_POLICY_PER_CU;
+    const uint32_t per_cu = by_waves < cap_cu ? (by_waves ? by_waves : 1u) : cap_cu;
     const uint32_t cap = per_cu * (uint32_t)cus;
     return (int)(want < cap ? want : cap);
 }
