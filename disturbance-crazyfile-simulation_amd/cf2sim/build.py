@@ -21,7 +21,14 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
 # that cost more than they save in the env-step kernels: +3 us).  The policy kernel gained 2 us
 # from SLP at 2 waves/SIMD, but at its current 4 waves/SIMD shape SLP makes it spill (56 B/lane,
 # bf16x3 40.0 us vs 38.3 us without)
-SOURCE_FLAGS = {"cf2sim_kernels.hip": ["-fno-slp-vectorize"], "cf2sim_api.cpp": ["-fno-slp-vectorize"],
+# The env kernels contract a*b+c only within one source expression (-ffp-contract=on, after the
+# global fast): with "fast" the backend also fused across statements wherever the surrounding code
+# allowed, so the small-N and the large-N step kernels rounded some sums differently (gyro bias,
+# reset pose: 1-ulp differences, then chaotic growth) and a run's results depended on the envs per
+# context, i.e. on the rank count.  "on" makes every launch geometry bit-identical
+# (tests/test_gpu_fullsize.py, contexts of 131 072 / 65 536 / 2 x 32 768 against one of 262 144) at
+# no measured cost (262 144 envs 36.08-36.19 vs 36.06-36.13 us, 32 768 envs within noise).
+SOURCE_FLAGS = {"cf2sim_kernels.hip": ["-fno-slp-vectorize", "-ffp-contract=on"], "cf2sim_api.cpp": ["-fno-slp-vectorize"],
                 "cf2sim_policy.hip": ["-fno-slp-vectorize"]}
 
 

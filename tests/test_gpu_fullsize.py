@@ -6,9 +6,10 @@ through size-independent properties (the restatement cannot step 262 144 envs in
   alone (env_id_offset = slice start), at the small-case tolerance (5e-4 mixed abs/rel, done
   exact).  The slices sit at the start, at a block boundary in the middle, and at the end of the
   grid, whose blocks run in the partial last residency round with raised issue priority;
-* launch-geometry invariance: the same envs stepped as one context of N or as two contexts of
-  N/2 (different grids, rounds and priorities) give bit-identical observations, rewards, dones
-  and state;
+* launch-geometry invariance: the same envs stepped as one context of N or as contexts of
+  131 072, 65 536 and 2 x 32 768 envs (different grids, rounds and priorities, and at 32 768 envs
+  the small-N kernel, as on an 8-GPU node) give bit-identical observations, rewards, dones and
+  state, so results do not depend on the rank count;
 * sanity of the whole batch: finite observations, non-positive rewards, a plausible done rate.
 """
 import numpy as np
@@ -23,6 +24,8 @@ pytestmark = pytest.mark.gpu
 N = 262144
 SLICE = 512
 SLICES = [0, N // 2 - SLICE // 2, N - SLICE]
+SPLIT_N = [131072, 65536, 32768, 32768]
+SPLIT_OFF = [0, 131072, 196608, 229376]
 # (env id, env-steps): the bench config (C4), the formations with downwash (C5; a 5 cm Gaussian
 # amplifies ulp differences chaotically on longer horizons, as in test_gpu_parity), the
 # per-step uniform torque (C3) and the constant wind (C2) at the full size
@@ -38,10 +41,12 @@ def _nerr(g, r):
 def test_full_size_slices_and_sharding(gpu, env_id, T):
     from cf2sim.vec_env import BatchedCrazyflieEnv
     full = BatchedCrazyflieEnv(env_id, N, seed=3, want_final_obs=True)
-    halves = [BatchedCrazyflieEnv(env_id, N // 2, seed=3, env_id_offset=h * (N // 2)) for h in range(2)]
+    # the same envs in four contexts: two above the small-N limit (step_kernel) and two of 32 768
+    # (step_kernel_small, an 8-GPU node shard): every launch geometry gives bit-identical results
+    parts = [BatchedCrazyflieEnv(env_id, n, seed=3, env_id_offset=o) for o, n in zip(SPLIT_OFF, SPLIT_N)]
     refs = [O.OracleEnv(build_config(env_id, SLICE, seed=3, env_id_offset=k), precision="f32") for k in SLICES]
     go = full.reset().cpu().numpy()
-    ho = np.concatenate([h.reset().cpu().numpy() for h in halves])
+    ho = np.concatenate([h.reset().cpu().numpy() for h in parts])
     np.testing.assert_array_equal(go, ho)
     for k, r in zip(SLICES, refs):
         assert _nerr(go[k:k + SLICE], r.reset()) < 2e-5
@@ -51,7 +56,7 @@ def test_full_size_slices_and_sharding(gpu, env_id, T):
     for t in range(T):
         a = (torch.rand(N, 4, device="cuda", generator=gen) * 2 - 1).contiguous()
         g_o, g_r, g_d, g_i = full.step(a)
-        outs = [h.step(a[i * (N // 2):(i + 1) * (N // 2)].contiguous()) for i, h in enumerate(halves)]
+        outs = [h.step(a[o:o + n].contiguous()) for o, n, h in zip(SPLIT_OFF, SPLIT_N, parts)]
         g_o, g_r, g_d = g_o.cpu().numpy(), g_r.cpu().numpy(), g_d.cpu().numpy().astype(bool)
         np.testing.assert_array_equal(g_o, np.concatenate([o[0].cpu().numpy() for o in outs]))
         np.testing.assert_array_equal(g_r, np.concatenate([o[1].cpu().numpy() for o in outs]))
@@ -67,10 +72,10 @@ def test_full_size_slices_and_sharding(gpu, env_id, T):
     # random uniform(-1, 1) actions crash a few % of the drones per env-step once they tumble
     assert 0.002 < dones / (N * T) < 0.2
     sf, si = full.get_state()
-    hs = [h.get_state() for h in halves]
+    hs = [h.get_state() for h in parts]
     np.testing.assert_array_equal(sf.cpu().numpy(), np.concatenate([x[0].cpu().numpy() for x in hs], 1))
     np.testing.assert_array_equal(si.cpu().numpy(), np.concatenate([x[1].cpu().numpy() for x in hs], 1))
-    for e in [full] + halves:
+    for e in [full] + parts:
         e.close()
 
 

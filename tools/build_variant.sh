@@ -11,7 +11,7 @@ mkdir -p "$ROOT/build_ab"
 # only the bench workload's kernel instance unless CF2_FULL=1
 ONLY=-DCF2_BENCH_ONLY; [ -n "$CF2_FULL" ] && ONLY=
 [ -f "$OBJ/cf2sim_policy.o" ] || { echo "build the in-tree library first"; exit 1; }
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=fast -fgpu-approx-transcendentals \
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=on -fgpu-approx-transcendentals \
   -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -Wall -Wno-pass-failed -Wno-unused-function -I "$ROOT/include" \
   -I "$ROOT/disturbance-crazyfile-simulation_amd/csrc" $ONLY $KFLAGS "$@" -c -o "/tmp/variant_$name.o" "$KSRC" &&
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -I "$ROOT/include" "$@" -c -o "/tmp/variant_api_$name.o" \

@@ -2,7 +2,7 @@
 # Kernel resource usage (VGPRs / scratch / occupancy) of the gfx950 code object, per kernel.
 # usage: tools/kres.sh [extra hipcc flags...]
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -fgpu-approx-transcendentals \
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=on -fgpu-approx-transcendentals \
   -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -I "$ROOT/include" --cuda-device-only -c \
   -Rpass-analysis=kernel-resource-usage "$@" "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_kernels.hip" \
   -o /tmp/kres.o 2>&1 | python3 -c '

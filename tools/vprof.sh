@@ -2,7 +2,7 @@
 # Where the step kernel's VGPR pressure peaks: max VGPR index per 100 ISA lines (spill lanes
 # excluded), plus markers for the phase fences.  usage: tools/vprof.sh [hipcc -D flags]
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -fgpu-approx-transcendentals \
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=on -fgpu-approx-transcendentals \
   -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -I "$ROOT/include" --cuda-device-only -S "$@" \
   "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_kernels.hip" -o /tmp/vprof_all.s 2>/dev/null || exit 1
 awk '/^_ZN3cf211step_kernel/,/s_endpgm/' /tmp/vprof_all.s > /tmp/vprof.s
