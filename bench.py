@@ -481,7 +481,8 @@ def main(argv=None):
     if gather:
         rx = (global_envs - n) * env.obs_dim * 4          # bytes this rank receives per step
         gather_info = {"mode": gather_mode, "bytes_in_per_rank_per_step": rx, "total_bytes_per_step": global_envs * env.obs_dim * 4,
-                       "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS}
+                       "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
+                       "rx_frac_of_xgmi": rx / (elapsed / args.steps) / 1e9 / XGMI_PEAK_GBS}
 
     if rank == 0:
         cpu = None

@@ -1907,7 +1907,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 }
 
 // Small N (<= 32 768 envs): the launch is as long as one wave's env-step chain, and the auto-reset
-// tail used to be ~40 % of it.  Each 256-thread block holds 64 envs.  Wave 0
+// tail used to be ~40 % of it (section 3 describes this kernel).  Each 256-thread block holds 64 envs.  Wave 0
 // steps them (issue priority 3).  Waves 1-3 meanwhile compute, speculatively for all 64 envs and at
 // priority 0, every part of a potential auto-reset that does not depend on the finished episode:
 // a reset's draws are keyed by the env's RNG counter, which is known when the state loads, so
