@@ -152,6 +152,22 @@ def load_traffic(workload_key: str):
     return None
 
 
+def load_valu_issue(workload_key: str):
+    """VALU issue fractions of the step and rollout kernels from tools/pmc_valu.sh (PMC), used only
+    if measured on this workload with this very kernel build; otherwise (None, None)."""
+    p = os.path.join(ROOT, "profiles", "valu_issue.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        key = step_kernel_key()
+        for e in d.get("entries", []):
+            if e.get("workload") == workload_key and e.get("kernel_key") == key:
+                return e["step_kernel"]["valu_issue_frac"], e["rollout_kernel"]["valu_issue_frac"]
+    except (OSError, ValueError, ImportError, KeyError):
+        pass
+    return None, None
+
+
 def bytes_per_env_step(env) -> int:
     return algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
 
@@ -417,7 +433,9 @@ def main(argv=None):
         torch.cuda.synchronize()
         us = f0.elapsed_time(f1) * 1e3 / (reps * K)
         fused = {"value": n / (us * 1e-6), "unit": "env-steps/s", "us_per_env_step": us, "k": K,
-                 "outputs": "obs, rew, done, trunc, cost, level per step (K slabs)"}
+                 "outputs": "obs, rew, done, trunc, cost, level per step (K slabs)",
+                 # fraction of the kernel's cycles its SIMDs spend issuing VALU (PMC, tools/pmc_valu.sh)
+                 "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[1]}
         del racts
 
     streaming = None
@@ -512,6 +530,7 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS,
                          "traffic": traffic,
+                         "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[0],
                          "algorithmic_bytes_per_env_step": bytes_per,
                          "kernel_ms_per_launch": kern_ms,
                          "working_set_bytes": wset,

@@ -3,7 +3,7 @@
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 pat=$1; n=${2:-1}; d=${3:-1}; p=${4:-0}
 b() { [ "$1" = 1 ] && echo Lb1 || echo Lb0; }
-K="_ZN3cf211step_kernelI$(b $n)E$(b $d)ELi${p}ELi${SPEC:-1}EEEvNS_7KParamsENS_6StepIOE"
+K="_ZN3cf211step_kernelI$(b $n)E$(b $d)ELi${p}ELi${SPEC:-1}ELi${ST:-0}EEEvNS_7KParamsENS_6StepIOE"
 cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -gline-tables-only -std=c++17 -ffp-contract=on -fgpu-approx-transcendentals \
   -fno-hip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -I "$ROOT/include" --cuda-device-only -S $EXTRA \
   "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_kernels.hip" -o /tmp/kloc_all.s 2>/dev/null || exit 1

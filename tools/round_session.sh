@@ -28,6 +28,8 @@ if has prof; then
   head -4 $OUT/kernel_stats.csv | cut -c1-200
 fi
 if has traffic; then
+  bash tools/pmc_valu.sh ${TAG}_valu 262144 > $OUT/valu.log 2>&1 || { echo "valu pass failed"; tail -20 $OUT/valu.log; exit 1; }
+  cp profiles/valu_issue.json $OUT/valu_issue.json
   for N in 262144 1048576; do
     bash tools/pmc_traffic.sh ${TAG}_traffic_$N $N > $OUT/traffic_$N.log 2>&1 || { echo "traffic $N failed"; tail -20 $OUT/traffic_$N.log; exit 1; }
     cp gpurun_out/${TAG}_traffic_$N/step_kernel_traffic.json profiles/step_kernel_traffic.json
