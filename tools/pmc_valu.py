@@ -1,11 +1,14 @@
 """VALU issue fraction from the PMC pass of tools/pmc_valu.sh.
 
-valu_issue_frac = VALU issue cycles per SIMD / kernel busy cycles, where
+valu_issue_frac = VALU issue cycles per SIMD / (profiled kernel duration x 2.4 GHz), where
   VALU issue cycles per SIMD = (SQ_INSTS_VALU + SQ_INSTS_VALU_TRANS_F32) * 2 / SIMDs
     (a wave64 VALU instruction occupies a SIMD-32 for 2 cycles; a transcendental twice that,
-    MI355X_MICROARCH.md 'vector-instruction ISSUE cost')
-  kernel busy cycles = GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs).
-1.0 would mean every SIMD issued VALU work on every cycle of the kernel.  Step kernel: the last
+    MI355X_MICROARCH.md 'vector-instruction ISSUE cost').
+1.0 would mean every SIMD issued VALU work on every cycle of the kernel at the 2.4 GHz peak
+clock; under load the clock is lower, so the true fraction is somewhat higher.  The
+GRBM_GUI_ACTIVE-based variant (busy cycles = GRBM_GUI_ACTIVE / 8) is kept as
+valu_issue_frac_grbm: on short dispatches it implies clocks above 2.4 GHz (2.8 GHz on the 38-us
+step kernel), i.e. it counts time outside the waves' lifetime, and reads low.  Step kernel: the last
 30 dispatches (bench.py --steps 30 after 1000 warm-up steps); rollout kernel: every dispatch of
 bench.py's fused-rollout measurement (K = 32, residency-sized slices).  Writes
 profiles/valu_issue.json for bench.py."""
@@ -29,7 +32,17 @@ def per_dispatch(kern):
     return [per[k] for k in sorted(per)]
 
 
-def summarize(rows, label, env_steps_per_dispatch):
+def durations(kern):
+    """Profiled dispatch durations (ns) of kern from the kernel trace of the same pass."""
+    d = []
+    for f in glob.glob(os.path.join(out, "pmc", "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kern in row.get("Kernel_Name", ""):
+                d.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    return [x for _, x in sorted(d)]
+
+
+def summarize(rows, label, env_steps_per_dispatch, dur_ns=None):
     s = {k: sum(r[k] for r in rows) for k in NAMES}
     issue = (s["SQ_INSTS_VALU"] + s["SQ_INSTS_VALU_TRANS_F32"]) * 2 / SIMDS
     busy = s["GRBM_GUI_ACTIVE"] / 8
@@ -37,7 +50,11 @@ def summarize(rows, label, env_steps_per_dispatch):
             "valu_per_wave": s["SQ_INSTS_VALU"] / s["SQ_WAVES"],
             "trans_per_wave": s["SQ_INSTS_VALU_TRANS_F32"] / s["SQ_WAVES"],
             "valu_per_wave_per_env_step": s["SQ_INSTS_VALU"] / s["SQ_WAVES"] / env_steps_per_dispatch,
-            "issue_cycles_per_simd": issue, "busy_cycles": busy, "valu_issue_frac": issue / busy}
+            "issue_cycles_per_simd": issue, "busy_cycles": busy, "valu_issue_frac_grbm": issue / busy,
+            "valu_issue_frac": (issue / (sum(dur_ns) * 1e-9 * 2.4e9)) if dur_ns else None,
+            # sanity: the clock implied by GRBM_GUI_ACTIVE over the profiled durations
+            "implied_clock_GHz": (busy / (sum(dur_ns) * 1e-9) / 1e9) if dur_ns else None,
+            "profiled_us_per_dispatch": (sum(dur_ns) / len(dur_ns) / 1e3) if dur_ns else None}
 
 
 sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
@@ -46,8 +63,8 @@ key = _obj_key("cf2sim_kernels.hip")
 step = per_dispatch("step_kernel")[-30:]
 roll = per_dispatch("rollout_kernel")
 res = {"workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}", "kernel_key": key,
-       "step_kernel": summarize(step, "step_kernel", 1),
-       "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32),
+       "step_kernel": summarize(step, "step_kernel", 1, durations("step_kernel")[-30:]),
+       "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations("rollout_kernel")),
        "note": __doc__.split("\n\n")[1]}
 prof = os.path.join(ROOT, "profiles", "valu_issue.json")
 try:
