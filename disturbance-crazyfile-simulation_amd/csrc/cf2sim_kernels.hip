@@ -1863,7 +1863,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     // experiment: the g-th block of each CU in the first round starts g * CF2_STAGGER cycles late
     if (blockIdx.x < P0.late_block) {
         const uint32_t g = blockIdx.x / (P0.late_block / 3u);
-        for (uint32_t k = 0; k < g * (CF2_STAGGER / 8000); ++k) __builtin_amdgcn_s_sleep(125);
+        for (uint32_t k = 0; k < g * (CF2_STAGGER / 512); ++k) __builtin_amdgcn_s_sleep(8);   // ~512 cycles each
     }
 #endif
 #ifdef CF2_TIMING
