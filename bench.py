@@ -486,10 +486,26 @@ def main(argv=None):
         out_of_cache = {"envs": on, "working_set_bytes": working_set_bytes(oenv, ring), "cache_resident": False,
                         "kernel_us_per_launch": ous, "value": on / (ous * 1e-6), "unit": "env-steps/s",
                         "achieved": oach, "frac": oach / HBM_PEAK_GBS,
-                        "frac_of_measured_hbm": oach / 6290.0,
                         "traffic": otraffic, "traffic_ratio": (otraffic / (bytes_per * on)) if otraffic else None}
         oenv.close()
         del oacts
+        # the box's own HBM copy rate (the peak re-measured with a STREAM-style
+        # copy): 2 GiB -> 2 GiB, far beyond the 256 MB Infinity Cache, 4 GiB of traffic per copy
+        src = torch.empty(1 << 29, dtype=torch.float32, device=dev).fill_(1.0)
+        dstc = torch.empty_like(src)
+        for _ in range(3):
+            dstc.copy_(src)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        c0.record(stream)
+        for _ in range(10):
+            dstc.copy_(src)
+        c1.record(stream)
+        torch.cuda.synchronize()
+        copy_gbs = 10 * 2 * src.numel() * 4 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        del src, dstc
+        out_of_cache["measured_hbm_copy_GBs"] = copy_gbs
+        out_of_cache["frac_of_measured_hbm"] = oach / copy_gbs
 
     value = global_envs * args.steps / elapsed
     achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
@@ -530,6 +546,8 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS,
                          "traffic": traffic,
+                         "traffic_source": "rocprofv3 PMC FETCH_SIZE/WRITE_SIZE passes of this kernel build "
+                                           "(tools/pmc_traffic.sh -> profiles/step_kernel_traffic.json)" if traffic else None,
                          "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[0],
                          "algorithmic_bytes_per_env_step": bytes_per,
                          "kernel_ms_per_launch": kern_ms,
