@@ -2331,6 +2331,248 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
     if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
 }
 
+// Small-N fused rollout (N <= 32 768): 64 envs per 256-thread block, their state in wave 0's
+// registers for all K steps, as rollout_kernel<.., 64>.  Waves 1-3 do for the rollout what they do
+// for one step in step_kernel_small: while wave 0 steps, they draw the step's randomness after
+// sub-step 0 (reference-default shape with sensor noise, the HD_* layout) and compute every env's
+// potential auto-reset speculatively (its draws are keyed by the env's RNG counter, which advances
+// by one per env-step), leaving the parts that do not depend on the finished episode in LDS
+// records: the reset pose, velocities, motor state, latency ring (RK_*), the domain randomisation,
+// disturbance and level (RP_*), and the two reset sensor calls' held measurements and gyro normals
+// (RO_*).  After one LDS barrier wave 0 only copies a record into a finishing env's registers and
+// runs the two gyro updates that need the finished episode's body rates and gyro bias.  Per step:
+// barrier A (wave 0 in sub-step 1 with HD, else at the top of the step; helpers write step k's
+// records only after it, so wave 0 has read step k-1's) and barrier B (records and the finished
+// envs' ballot in LDS).
+enum { RK_P = 0, RK_Q = 3, RK_V = 7, RK_W = 10, RK_RPY = 13, RK_WB = 16, RK_X = 19, RK_ABUF = 23, RK_LA = 39,
+       RK_WORDS = 43 };
+enum { RP_DT = 0, RP_M = 1, RP_J = 2, RP_K0 = 5, RP_K1 = 6, RP_B = 7, RP_K = 11, RP_DSTB = 15, RP_LEVEL = 18,
+       RP_LEVEL_IDX = 19, RP_WORDS = 20 };
+enum { RO_HELD1 = 0, RO_NG1 = 10, RO_HELD2 = 19, RO_NG2 = 29, RO_WORDS = 38 };
+
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepIO io0, uint32_t K, uint32_t act_stride) {
+    const KParams P = shape_view<SPEC>(P0);
+    constexpr int OL = NOISE ? 13 : 17;
+    constexpr int OD = 2 * (OL + 4);
+    constexpr bool HD = SPEC == 1 && NOISE;
+    constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
+    __shared__ __align__(16) float s_obs[64 * OD];
+    __shared__ float s_kin[RK_WORDS * 64];                 // [word][env]
+    __shared__ float s_par[RP_WORDS * 64];
+    __shared__ float s_ho[NOISE ? RO_WORDS * 64 : 1];
+    __shared__ float s_draw[HD ? HD_WORDS * 64 : 1];
+    __shared__ uint32_t s_mask[2];
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint32_t base = blockIdx.x * 64u, i = base + lane, gid = P.gid_off + i;
+    const bool live = i < P.N;
+    const bool need_level = P.need_level || io0.level != nullptr;
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    const size_t n = P0.out_stride;              // rows per output slab (the whole population)
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        Env E;
+        if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, need_level, /*with_hist=*/true);
+        float* obs_row = s_obs + lane * OD;
+        for (uint32_t k = 0; k < K; ++k) {
+            StepIO io = io0;
+            io.act = io0.act + (size_t)k * act_stride;
+            io.rew = io0.rew + (size_t)k * n;
+            io.done = io0.done + (size_t)k * n;
+            if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
+            if (io0.cost) io.cost = io0.cost + (size_t)k * n;
+            if (io0.level) io.level = io0.level + (size_t)k * n;
+            if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+            if (!HD) lds_barrier();                  // A_k (HD: inside the env-step, before sub-step 1)
+            bool do_reset = false;
+            ResetSeed rs;
+            if (live)
+                do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD, RollKeys>(P, io, i, E, obs_row, rs, s_hjgrid,
+                                                                                     s_draw + lane);
+            const uint64_t m = __ballot(do_reset);
+            if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
+            lds_barrier();                           // B_k: the helpers' records of step k are in LDS
+            if (do_reset) {
+                const float stale[3] = {rs.wb[0], rs.wb[1], rs.wb[2]};   // the gyro LPF seed
+                const float* kin = s_kin + lane;
+                const float* par = s_par + lane;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    E.p[c] = kin[(RK_P + c) * 64]; E.v[c] = kin[(RK_V + c) * 64]; E.w[c] = kin[(RK_W + c) * 64];
+                    E.rpy[c] = kin[(RK_RPY + c) * 64]; E.wb[c] = kin[(RK_WB + c) * 64];
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    E.q[c] = kin[(RK_Q + c) * 64]; E.x[c] = kin[(RK_X + c) * 64]; E.xl[c] = 0.0f;
+                    E.la[c] = kin[(RK_LA + c) * 64];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) E.abuf[r][c] = r < P.buf_size ? kin[(RK_ABUF + 4 * r + c) * 64] : 0.0f;
+                E.ep_step = 0; E.aidx = 0; E.props_on = 0; E.la_view = 1;
+                E.dt = par[RP_DT * 64]; E.m = par[RP_M * 64];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { E.J[c] = par[(RP_J + c) * 64]; E.dstb[c] = par[(RP_DSTB + c) * 64]; }
+                E.k0 = par[RP_K0 * 64]; E.k1 = par[RP_K1 * 64];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { E.B[c] = par[(RP_B + c) * 64]; E.K[c] = par[(RP_K + c) * 64]; }
+                E.level = par[RP_LEVEL * 64];
+                E.level_idx = bi(par[RP_LEVEL_IDX * 64]);
+                E.gust_left = 0;
+                // the reset observation (reset_observe): two sensor calls, then the history row
+                float o0[17], o1[17];
+                if (NOISE) {
+                    const float* ho = s_ho + lane;
+                    float ng1[9], ng2[9];
+#pragma unroll
+                    for (int c = 0; c < 9; ++c) { ng1[c] = ho[(RO_NG1 + c) * 64]; ng2[c] = ho[(RO_NG2 + c) * 64]; }
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) E.lpf[c] = stale[c];
+#pragma unroll
+                    for (int c = 0; c < 10; ++c) { o0[c] = ho[(RO_HELD1 + c) * 64]; o1[c] = ho[(RO_HELD2 + c) * 64]; }
+#pragma unroll
+                    for (int c = 0; c < 10; ++c) E.held[c] = o1[c];
+                    gyro_update(P, E, ng1);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) o0[10 + c] = E.lpf[c];
+                    gyro_update(P, E, ng2);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) o1[10 + c] = E.lpf[c];
+                } else {
+                    const float o[17] = {E.p[0], E.p[1], E.p[2], E.q[0], E.q[1], E.q[2], E.q[3], E.v[0], E.v[1],
+                                         E.v[2], E.wb[0], E.wb[1], E.wb[2], E.la[0], E.la[1], E.la[2], E.la[3]};
+#pragma unroll
+                    for (int c = 0; c < 17; ++c) { o0[c] = o[c]; o1[c] = o[c]; }
+                }
+                float row[OD];
+#pragma unroll
+                for (int c = 0; c < OL; ++c) { row[c] = o0[c]; row[OL + 4 + c] = o1[c]; E.obs_prev[c] = o1[c]; }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    row[OL + c] = E.la[c]; row[2 * OL + 4 + c] = E.la[c];
+                    E.hact[0][c] = E.la[c]; E.hact[1][c] = E.la[c];
+                }
+                E.halias0 = E.halias1 = 1;
+#pragma unroll
+                for (int c = 0; c < OD; c += 2) *reinterpret_cast<float2*>(obs_row + c) = make_float2(row[c], row[c + 1]);
+            }
+            // this wave's 64 rows, written by this wave only: its LDS writes land before its reads
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            write_obs_rows(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs, P.N - base < 64u ? P.N - base : 64u,
+                           64u, OD, lane, 64u);
+        }
+        if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
+        return;
+    }
+    // helper waves 1-3
+    __builtin_amdgcn_s_setprio(0);
+    uint32_t ctr = 0;
+    float lvl = 0.0f;
+    int lvl_idx = 0;
+    if (live) {
+        const Tile T(io0.sf, P.N, i);
+        ctr = (uint32_t)bi(T.ld(G_CORE3).z);
+        if (wave == PARAMS_WAVE) {
+            lvl = need_level ? T.ld(G_LEVEL).w : P.level_fixed;
+            lvl_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
+        }
+    }
+    const Keys Kh = make_keys(P.key0, P.key1);
+    for (uint32_t k = 0; k < K; ++k, ++ctr) {
+        if (HD) {
+            if (live) {
+                const Rng g{Kh, ctr, gid, TAG_STEP};
+                float* d = s_draw + lane;
+                auto bm4 = [&](uint32_t blk, int w) {
+                    const U4 u = g.block(blk);
+                    float z0, z1, z2, z3;
+                    box_muller(u.x, u.y, z0, z1);
+                    box_muller(u.z, u.w, z2, z3);
+                    d[(w + 0) * 64] = z0; d[(w + 1) * 64] = z1; d[(w + 2) * 64] = z2; d[(w + 3) * 64] = z3;
+                };
+                if (wave == 1) {
+                    bm4(2, HD_OU1);
+                    bm4(16, HD_GYRO1);
+                    bm4(17, HD_GYRO1 + 4);
+                    const U4 u = g.block(18);
+                    float z0, z1;
+                    box_muller(u.x, u.y, z0, z1);
+                    d[(HD_GYRO1 + 8) * 64] = z0;
+                } else if (wave == 2) {
+                    bm4(24, HD_FINAL);
+                    bm4(25, HD_FINAL + 4);
+                    bm4(26, HD_FINAL + 8);
+                } else {
+                    bm4(27, HD_FINAL + 12);
+                    const U4 u = g.block(28), v = g.block(29);
+                    float z0, z1;
+                    box_muller(u.x, u.y, z0, z1);
+                    d[(HD_FINAL + 16) * 64] = z0; d[(HD_FINAL + 17) * 64] = z1;
+                    d[(HD_FINAL + 18) * 64] = __uint_as_float(u.z); d[(HD_FINAL + 19) * 64] = __uint_as_float(u.w);
+                    d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
+                    d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
+                }
+            }
+        }
+        lds_barrier();                               // A_k
+        Env H;
+        if (P.auto_reset && live) {
+            const Rng gr{Kh, ctr, gid, TAG_RESET};
+            HeldNoise hn;
+            float ngs[9];
+            if (NOISE && wave >= 2) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
+            reset_kinematics<PHYS, true>(P, H, gr, gid);
+            if (wave == 1) {
+                float* kin = s_kin + lane;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    kin[(RK_P + c) * 64] = H.p[c]; kin[(RK_V + c) * 64] = H.v[c]; kin[(RK_W + c) * 64] = H.w[c];
+                    kin[(RK_RPY + c) * 64] = H.rpy[c]; kin[(RK_WB + c) * 64] = H.wb[c];
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    kin[(RK_Q + c) * 64] = H.q[c]; kin[(RK_X + c) * 64] = H.x[c]; kin[(RK_LA + c) * 64] = H.la[c];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        if (r < P.buf_size) kin[(RK_ABUF + 4 * r + c) * 64] = H.abuf[r][c];
+            } else if (NOISE) {
+                float held[10];
+                held_combine(H, hn, held);
+                float* ho = s_ho + lane;
+                const int hb = wave == 2 ? RO_HELD1 : RO_HELD2, nb = wave == 2 ? RO_NG1 : RO_NG2;
+#pragma unroll
+                for (int c = 0; c < 10; ++c) ho[(hb + c) * 64] = held[c];
+#pragma unroll
+                for (int c = 0; c < 9; ++c) ho[(nb + c) * 64] = ngs[c];
+            }
+            if (wave == PARAMS_WAVE) {
+                H.level = lvl;
+                H.level_idx = lvl_idx;
+                reset_params<DR, true>(P, H, gr);
+                float* par = s_par + lane;
+                par[RP_DT * 64] = H.dt; par[RP_M * 64] = H.m;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) { par[(RP_J + c) * 64] = H.J[c]; par[(RP_DSTB + c) * 64] = H.dstb[c]; }
+                par[RP_K0 * 64] = H.k0; par[RP_K1 * 64] = H.k1;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { par[(RP_B + c) * 64] = H.B[c]; par[(RP_K + c) * 64] = H.K[c]; }
+                par[RP_LEVEL * 64] = H.level;
+                par[RP_LEVEL_IDX * 64] = ib(H.level_idx);
+            }
+        }
+        lds_barrier();                               // B_k
+        if (P.auto_reset && live && wave == PARAMS_WAVE) {
+            const uint64_t mask = ((uint64_t)s_mask[1] << 32) | (uint64_t)s_mask[0];
+            if ((mask >> lane) & 1ull) { lvl = H.level; lvl_idx = H.level_idx; }   // the new episode's level
+        }
+    }
+}
+
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __global__ void __launch_bounds__(256) reset_kernel(KParams P0, float* __restrict__ sf,
                                                     const uint8_t* __restrict__ mask, float* __restrict__ obs) {
@@ -2546,9 +2788,15 @@ static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t 
         if (io.level) ios.level = io.level + e0;
         if (io.final_obs) ios.final_obs = io.final_obs + (size_t)e0 * OD;
         Ps.out_stride = P.N;
+#ifndef CF2_ROLL_SMALL_OLD
+        if (epb == 64u)
+            hipLaunchKernelGGL((rollout_kernel_small<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(256), 0, s, Ps, ios, K,
+                               act_stride);
+#else
         if (epb == 64u)
             hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC, 64u>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s, Ps, ios,
                                K, act_stride);
+#endif
         else
             hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC, CF2_STEP_BLOCK>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s,
                                Ps, ios, K, act_stride);

@@ -21,11 +21,29 @@ CASES = [
 
 @pytest.mark.parametrize("env_id,n,kw", CASES)
 def test_fused_rollout_equals_step_loop(gpu, env_id, n, kw):
+    _compare(gpu, env_id, n, kw)
+
+
+@pytest.mark.parametrize("n", [2000, 40000])
+def test_fused_rollout_boltzmann_hj_levels(gpu, n):
+    """The Boltzmann-level HJ env: a reset redraws the episode's level, which the small-N
+    rollout's helper waves track from step to step for their speculative resets."""
+    from test_gpu_parity import _synthetic_tables
+    V = torch.from_numpy(_synthetic_tables(tuple(range(3)), seed=1)).cuda()
+    tol = [lv % 3 for lv in range(21)]
+    _compare(gpu, "DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", n, dict(max_episode_steps=6),
+             setup=lambda e: e.bind_hj_tables(V, tol))
+
+
+def _compare(gpu, env_id, n, kw, setup=None):
     from cf2sim.vec_env import BatchedCrazyflieEnv
     K = 24
     a = (torch.rand(K, n, 4, device=gpu, generator=torch.Generator(device=gpu).manual_seed(3)) * 2 - 1).contiguous()
     ref = BatchedCrazyflieEnv(env_id, n, seed=9, want_final_obs=True, **kw)
     fus = BatchedCrazyflieEnv(env_id, n, seed=9, want_final_obs=True, **kw)
+    if setup is not None:
+        setup(ref)
+        setup(fus)
     ref.reset()
     fus.reset()
     outs = {k: [] for k in ("obs", "rew", "done", "trunc", "cost", "level", "fin")}
