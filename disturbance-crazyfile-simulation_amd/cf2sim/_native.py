@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "cf2_set_ground_effect",
     "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
     "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
+    "cf2_hbm_probe",
 )
 
 
@@ -82,6 +83,7 @@ def load() -> ctypes.CDLL:
     lib.cf2_value_forward_masked.argtypes = [vp, u32, u32, ctypes.c_int, vp, vp, vp, vp]
     lib.cf2_gae.argtypes = [u32, u32, vp, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp,
                             vp, vp]
+    lib.cf2_hbm_probe.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
                         "cf2_policy_weights_count", "cf2_policy_packed_count"):

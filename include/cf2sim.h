@@ -302,6 +302,12 @@ int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev,
              const uint8_t* trunc_dev, const float* trunc_val_dev, const float* last_val_dev, float gamma,
              float lam, float rew_den, float* adv_dev, float* ret_dev, float* disc_ret_dev, void* stream);
 
+/* Measurement support (no reference counterpart): streaming kernels over `bytes` (a multiple of
+ * 16, both pointers 16-B aligned) with non-temporal accesses.  mode 0: copy src -> dst; mode 1:
+ * read src only (bytes >= 4096; dst must hold 4 KB and is normally left untouched).  bench.py times
+ * them on 2 GiB to measure the box's HBM rates. */
+int  cf2_hbm_probe(void* dst_dev, const void* src_dev, size_t bytes, int mode, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

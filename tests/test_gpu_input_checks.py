@@ -125,3 +125,23 @@ def test_rebinding_tables(gpu):
     env.step(torch.zeros(512, 4, device=gpu))                            # previous binding still valid
     torch.cuda.synchronize()
     env.close()
+
+
+def test_hbm_probe(gpu):
+    """cf2_hbm_probe (bench.py's HBM-rate probe): exact copy with a ragged tail, the read mode
+    leaves dst alone, argument checks."""
+    from cf2sim import _native
+    lib = _native.load()
+    s = torch.cuda.current_stream().cuda_stream
+    src = torch.arange(1_000_004, dtype=torch.float32, device="cuda")      # 4 000 016 B: 16-B multiple
+    dst = torch.zeros_like(src)
+    assert lib.cf2_hbm_probe(dst.data_ptr(), src.data_ptr(), src.numel() * 4, 0, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    sink = torch.zeros(1024, dtype=torch.float32, device="cuda")
+    assert lib.cf2_hbm_probe(sink.data_ptr(), src.data_ptr(), src.numel() * 4, 1, s) == 0
+    torch.cuda.synchronize()
+    assert lib.cf2_hbm_probe(dst.data_ptr(), src.data_ptr(), 10, 0, s) != 0            # not a 16-B multiple
+    assert lib.cf2_hbm_probe(dst.data_ptr() + 4, src.data_ptr(), 16, 0, s) != 0        # misaligned
+    assert lib.cf2_hbm_probe(None, src.data_ptr(), 16, 0, s) != 0
+    assert lib.cf2_hbm_probe(dst.data_ptr(), src.data_ptr(), 16, 2, s) != 0            # no such mode

@@ -10,4 +10,4 @@ cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-c
   -fno-hip-fp32-correctly-rounded-divide-sqrt ${SLP:--fno-slp-vectorize} -Wall -Wno-pass-failed -I "$ROOT/include" "$@" \
   -c -o "/tmp/pvariant_$name.o" "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_policy.hip" &&
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/build_ab/$name.so" "$OBJ/cf2sim_kernels.o" \
-  "/tmp/pvariant_$name.o" "$OBJ/cf2sim_api.o"
+  "/tmp/pvariant_$name.o" "$OBJ/cf2sim_util.o" "$OBJ/cf2sim_api.o"

@@ -17,4 +17,4 @@ cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-c
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -I "$ROOT/include" "$@" -c -o "/tmp/variant_api_$name.o" \
   "$ROOT/disturbance-crazyfile-simulation_amd/csrc/cf2sim_api.cpp" &&
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/build_ab/$name.so" "/tmp/variant_$name.o" \
-  "$OBJ/cf2sim_policy.o" "/tmp/variant_api_$name.o"
+  "$OBJ/cf2sim_policy.o" "$OBJ/cf2sim_util.o" "/tmp/variant_api_$name.o"
