@@ -99,6 +99,9 @@ __device__ float w_l3(const float* __restrict__ W, int n, int in) {
     return n == 4 ? W[L::V_W3 + in - 64] : 0.0f;
 }
 
+#ifndef CF2_POLICY_L3F32
+#define CF2_POLICY_L3F32 0
+#endif
 #ifndef CF2_POLICY_SLOT1
 #define CF2_POLICY_SLOT1 0     // measured 35.0 vs 34.2 us at 262 144 rows: the kernel is VALU-, not MFMA-bound
 #endif
@@ -122,7 +125,11 @@ struct Packed {
     static constexpr int N_L2 = BF ? 2 * 4 * FB : 0;
     static constexpr int O_L2V = O_L2P + (BF ? N_L2 : KSP * 4 * FF);
     static constexpr int O_L3 = O_L2V + (BF ? N_L2 : KSV * 4 * FF);
-    static constexpr int O_BIAS = O_L3 + (BF ? 4 * FB : (KSP + KSV) * FF);
+    // layer 3 (5 outputs) on fp32 k-steps also in bf16x3 mode (CF2_POLICY_L3F32): its inputs need
+    // no hi/lo split then (-97 VALU per chunk), for 30 fp32 MFMAs instead of 12 bf16 ones; measured
+    // 38.7 vs 34.1 us, so the matrix pipe is as close to the limit as the VALU
+    static constexpr bool L3F = !BF || CF2_POLICY_L3F32;
+    static constexpr int O_BIAS = O_L3 + (L3F ? (KSP + KSV) * FF : 4 * FB);
     static constexpr int B_L1 = 0, B_L2P = 128, B_L2V = 192, B_L3 = 256, NB = 272;   // neuron-ordered biases
     static constexpr int O_LOGSTD = O_BIAS + NB, O_MEAN = O_LOGSTD + 4, O_SCALE = O_MEAN + (D + 3) / 4 * 4;
     static constexpr int TOTAL = (O_SCALE + D + 3) / 4 * 4;
@@ -220,7 +227,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, 
         }
     } else if (k < P::O_BIAS) {
         const int r = k - P::O_L3;
-        if (P::BF) {
+        if (!P::L3F) {
             v = bfword(4, r, 1);
         } else {
             const int ks = r / 64, l = r % 64, n = l & 15, g = l >> 4;
@@ -617,7 +624,7 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
 #pragma unroll
         for (int half = PI ? 0 : 1; half < 2; ++half) {
             f4v(&h)[4][RT] = half ? h2v : h2p;
-            if constexpr (BF) {
+            if constexpr (!P::L3F) {
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb) {
                     bf8v ah, al;
