@@ -26,7 +26,7 @@ __device__ __forceinline__ void record(uint64_t* out, float spin) {
 }
 __global__ void __launch_bounds__(256) k_small(uint64_t* out, float spin) { record(out, spin); }
 template <int NB>
-__global__ void __launch_bounds__(256) k_big(uint64_t* out, Big<NB> b) { record(out, b.f[3]); }
+__global__ void __launch_bounds__(1024) k_big(uint64_t* out, Big<NB> b) { record(out, b.f[3]); }
 
 static void report(const char* name, const std::vector<uint64_t>& h, int waves) {
     uint64_t t0 = UINT64_MAX, t1 = 0;
@@ -46,13 +46,14 @@ static void report(const char* name, const std::vector<uint64_t>& h, int waves) 
 }
 
 template <int NB>
-static double spread_us(uint64_t* d, std::vector<uint64_t>& h, int blocks, float spin, int reps, double* tput_us) {
+static double spread_us(uint64_t* d, std::vector<uint64_t>& h, int blocks, float spin, int reps, double* tput_us,
+                        int threads = 256) {
     Big<NB> b{};
     b.f[3] = spin;
-    const int waves = blocks * 4;
+    const int waves = blocks * threads / 64;
     std::vector<double> sp;
     for (int r = 0; r < reps; ++r) {
-        hipLaunchKernelGGL(k_big<NB>, dim3(blocks), dim3(256), 0, 0, d, b);
+        hipLaunchKernelGGL(k_big<NB>, dim3(blocks), dim3(threads), 0, 0, d, b);
         (void)hipDeviceSynchronize();
         (void)hipMemcpy(h.data(), d, (size_t)waves * 16, hipMemcpyDeviceToHost);
         uint64_t t0 = UINT64_MAX, t1 = 0;
@@ -65,9 +66,9 @@ static double spread_us(uint64_t* d, std::vector<uint64_t>& h, int blocks, float
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    for (int r = 0; r < 20; ++r) hipLaunchKernelGGL(k_big<NB>, dim3(blocks), dim3(256), 0, 0, d, b);
+    for (int r = 0; r < 20; ++r) hipLaunchKernelGGL(k_big<NB>, dim3(blocks), dim3(threads), 0, 0, d, b);
     (void)hipEventRecord(e0);
-    for (int r = 0; r < 200; ++r) hipLaunchKernelGGL(k_big<NB>, dim3(blocks), dim3(256), 0, 0, d, b);
+    for (int r = 0; r < 200; ++r) hipLaunchKernelGGL(k_big<NB>, dim3(blocks), dim3(threads), 0, 0, d, b);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -77,22 +78,22 @@ static double spread_us(uint64_t* d, std::vector<uint64_t>& h, int blocks, float
 }
 
 int main() {
-    const int blocks = 512, waves = blocks * 4;
+    const int waves = 2048;
     uint64_t* d;
     (void)hipMalloc(&d, (size_t)waves * 16);
     std::vector<uint64_t> h((size_t)waves * 2);
     for (int pass = 0; pass < 2; ++pass) {
         double t;
-        double s16 = spread_us<16>(d, h, blocks, 2000.0f, 15, &t);
+        double s16 = spread_us<16>(d, h, 512, 2000.0f, 15, &t);
         printf("kernarg %5d B: median start spread %.2f us, back-to-back %.2f us per launch\n", 16 + 8, s16, t);
-        double s96 = spread_us<96>(d, h, blocks, 2000.0f, 15, &t);
-        printf("kernarg %5d B: median start spread %.2f us, back-to-back %.2f us per launch\n", 96 + 8, s96, t);
-        double s256 = spread_us<256>(d, h, blocks, 2000.0f, 15, &t);
-        printf("kernarg %5d B: median start spread %.2f us, back-to-back %.2f us per launch\n", 256 + 8, s256, t);
-        double s688 = spread_us<688>(d, h, blocks, 2000.0f, 15, &t);
+        double s688 = spread_us<688>(d, h, 512, 2000.0f, 15, &t);
         printf("kernarg %5d B: median start spread %.2f us, back-to-back %.2f us per launch\n", 688 + 8, s688, t);
-        double s1k = spread_us<1024>(d, h, blocks, 2000.0f, 15, &t);
-        printf("kernarg %5d B: median start spread %.2f us, back-to-back %.2f us per launch\n", 1024 + 8, s1k, t);
+        for (int threads : {64, 128, 512, 1024}) {
+            const int blocks = waves * 64 / threads;
+            double sp = spread_us<688>(d, h, blocks, 2000.0f, 15, &t, threads);
+            printf("2048 waves as %4d blocks x %4d threads: median start spread %.2f us, back-to-back %.2f us per launch\n",
+                   blocks, threads, sp, t);
+        }
     }
     (void)hipFree(d);
     return 0;
