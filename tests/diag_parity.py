@@ -1,4 +1,5 @@
-"""Print GPU-vs-oracle divergence per env id over T env-steps (diagnostic, GPU box)."""
+"""Print GPU-vs-oracle divergence per env id over T env-steps (diagnostic, GPU box; kept under
+tests/ because it runs the oracle: python tests/diag_parity.py)."""
 import os, sys, time
 import numpy as np
 import torch

@@ -1,5 +1,5 @@
 """Per-step GPU-vs-fp32-oracle error of one parity case (diagnostic, GPU box):
-python tools/parity_trace.py [case_index]; CF2SIM_LIB selects the library build."""
+python tests/diag_parity_trace.py [case_index]; CF2SIM_LIB selects the library build."""
 import os, sys
 import numpy as np
 import torch

@@ -312,3 +312,32 @@ def test_zero_envs_is_rejected(gpu):
     from cf2sim.vec_env import BatchedCrazyflieEnv
     with pytest.raises((CF2Error, ValueError)):
         BatchedCrazyflieEnv("DroneHoverBulletFreeEnvWithoutAdversary-v0", 0)
+
+
+def test_downwash_formations_long_horizon_closed_loop(gpu):
+    """f4 over 240 env-steps (round-2 review: the 25-step horizon above is short).  Closed loop:
+    every drone's PD controller acts on its own observation, on the HIP kernel and on the fp32
+    restatement, so the formations keep flying.  The 5 cm downwash Gaussian amplifies ulp-level
+    differences chaotically in a few formations whose drones pass through each other's wake, so
+    the bound is on the distribution over drones (still flying on both sides), not on its maximum:
+    at every 20th env-step the median error stays < 2e-5 and >= 93 % of the drones within 5e-4
+    (measured: median 8e-7 -> 9e-6, 96-100 % within 5e-4; tests/diag_downwash_horizon.py)."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env_id, n, T = "DroneHoverBulletFreeEnvWithDownwash-v0", 512, 240
+    env = BatchedCrazyflieEnv(env_id, n, seed=3, want_final_obs=True)
+    cfg = build_config(env_id, n, seed=3)
+    ref = O.OracleEnv(cfg, precision="f32")
+    go, ro = env.reset().cpu().numpy(), ref.reset()
+    alive = np.ones(n, bool)
+    for t in range(T):
+        g_o, _, g_d, _ = env.step(torch.from_numpy(pd_actions(go[:, 17:30], cfg.hover_action)).cuda())
+        r_o, _, r_d, _ = ref.step(pd_actions(ro[:, 17:30], cfg.hover_action))
+        go, ro = g_o.cpu().numpy(), r_o
+        alive &= ~g_d.cpu().numpy().astype(bool) & ~r_d
+        if (t + 1) % 20 == 0:
+            e = (np.abs(go - ro) / (1 + np.abs(ro))).max(1)[alive]
+            assert alive.sum() >= 150, (t, int(alive.sum()))
+            assert float(np.median(e)) < 2e-5, (t, float(np.median(e)))
+            assert float((e < 5e-4).mean()) >= 0.93, (t, float((e < 5e-4).mean()))
+    env.close()
+    ref.close()
