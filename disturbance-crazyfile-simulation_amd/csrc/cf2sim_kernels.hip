@@ -383,8 +383,10 @@ __device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, u
     }
 }
 
-// Block barrier for LDS hand-offs: the calling wave's LDS operations complete first; its global
-// stores keep draining (__syncthreads would also wait for those, vmcnt(0)).
+// Block barrier for LDS hand-offs: the calling wave's LDS operations complete first, then
+// s_barrier.  (On gfx950 __syncthreads lowers to the same two instructions -- its workgroup-scope
+// fence needs no vmcnt wait -- but this form is explicit about what the hand-off relies on, and it
+// has no fence semantics the compiler could move memory operations around.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // write_obs_rows for the small-N kernel: row r comes from rrow (the reset observations the helper
@@ -1494,8 +1496,9 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     // the physics state is final now: store it early so its registers free up before the
     // epilogue.  SKIP_RESETTING (the small-N kernel, whose reset stores follow an LDS-only
     // barrier): an env that auto-resets is not stored, its reset writes every group stored here,
-    // so no two waves store one group in one launch.  The large-N kernel stores it anyway (its
-    // resets follow __syncthreads, which drains these stores first; skipping cost 0.6 us there)
+    // so no two waves store one group in one launch.  The large-N kernel stores it anyway: its
+    // resets follow __syncthreads, whose workgroup-scope release/acquire orders these stores before
+    // the reset waves' stores to the same groups (skipping them cost 0.6 us there)
     if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS, ST_AUX>(P, io.sf, i, E);
     if (HD && fin != nullptr) {
         // small-N kernel: reward, cost and the per-env outputs are finished by a helper wave after
