@@ -343,9 +343,12 @@ class Rollout:
 
 @torch.no_grad()
 def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float = 0.99,
-            lam: float = 0.95, generator: torch.Generator | None = None) -> Rollout:
+            lam: float = 0.95, generator: torch.Generator | None = None, fuse: bool = True) -> Rollout:
     """``roll_out`` for all envs of a BatchedCrazyflieEnv at once; everything stays on the GPU.
-    ``ac`` is an MLPActorCritic (torch layers) or a FusedActorCritic (one HIP launch per step).
+    ``ac`` is an MLPActorCritic (torch layers) or a FusedActorCritic (HIP kernels).  With a
+    FusedActorCritic and ``fuse`` each env-step and the policy forward on its observations are one
+    launch (cf2_collect_step) where the config has a fused instance, else two launches; the
+    results are bit-identical either way.
     ``envs`` must have been created with want_final_obs=True (time-out bootstrapping)."""
     if envs.final_obs is None:
         raise ValueError("collect() needs BatchedCrazyflieEnv(..., want_final_obs=True)")
@@ -371,15 +374,23 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         # final observations kept per step (rows written only where an episode ended), so that the
         # time-out values are one masked launch over all T*N rows after the loop
         fin = torch.empty(steps, n, d, device=dev)
+        # the policy of step t + 1 runs right behind the env-step of step t (fused: in its launch);
+        # the last one gives V(obs_T), its sampled action and logp are not used
+        last_val = torch.empty(n, device=dev)
+        a_last, lp_last = torch.empty(n, 4, device=dev), torch.empty(n, device=dev)
+        ac.step_into(obs_buf[0], buf_a[0], buf_v[0], buf_lp[0])
         for t in range(steps):
-            ac.step_into(obs_buf[t], buf_a[t], buf_v[t], buf_lp[t])
+            nxt = (buf_a[t + 1], buf_v[t + 1], buf_lp[t + 1]) if t + 1 < steps else (a_last, last_val, lp_last)
+            if fuse and envs.collect_step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], fin[t], ac, *nxt):
+                continue
+            fuse = False
             envs.step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], final_obs_out=fin[t])
+            ac.step_into(obs_buf[t + 1], *nxt)
         per = max(1, (2**31 - 1) // n)                      # row counts of the C ABI are 32-bit
         for t0 in range(0, steps, per):                      # V(final obs) of the time-outs only
             t1 = min(steps, t0 + per)
             ac.value_masked(fin[t0:t1].view(-1, d), tr8[t0:t1].view(-1), trunc_val[t0:t1].view(-1))
         o = obs_buf[steps]
-        last_val = ac.value(o)
         adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True)
         buf_o, buf_d, buf_tr = obs_buf[:steps], d8.view(torch.bool), tr8.view(torch.bool)   # 0/1 bytes
         return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val, disc)

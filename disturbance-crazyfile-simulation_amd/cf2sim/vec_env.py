@@ -184,6 +184,39 @@ class BatchedCrazyflieEnv:
         self._state_version += 1
         self._obs_latest = obs_out
 
+    def collect_step_into(self, actions: torch.Tensor, obs_out: torch.Tensor, rew_out: torch.Tensor,
+                          done_out: torch.Tensor, trunc_out: torch.Tensor | None, final_obs_out: torch.Tensor | None,
+                          policy, act_out: torch.Tensor, val_out: torch.Tensor, logp_out: torch.Tensor) -> bool:
+        """step_into() followed by policy.step_into(obs_out, act_out, val_out, logp_out) in one launch
+        (cf2_collect_step: the collect loop's env.step + ac.step, algs/iwpg/iwpg.py:377-380).  The
+        outputs are bit-identical to the two calls.  Returns False, having launched nothing, where
+        no fused instance is built (cf2sim.h); the caller then makes the two calls."""
+        n, od, dev = self.num_envs, self.obs_dim, self.device
+        _check_buf(actions, "actions", (n, 4), torch.float32, dev, 16)
+        _check_buf(obs_out, "obs_out", (n, od), torch.float32, dev, 16)
+        _check_buf(rew_out, "rew_out", (n,), torch.float32, dev)
+        _check_buf(done_out, "done_out", (n,), torch.uint8, dev, 1)
+        _check_buf(trunc_out, "trunc_out", (n,), torch.uint8, dev, 1)
+        _check_buf(final_obs_out, "final_obs_out", (n, od), torch.float32, dev, 8)
+        _check_buf(act_out, "act_out", (n, 4), torch.float32, dev, 16)
+        _check_buf(val_out, "val_out", (n,), torch.float32, dev)
+        _check_buf(logp_out, "logp_out", (n,), torch.float32, dev)
+        if self.cfg.disturbance == DSTB_EXTERNAL:
+            raise ValueError("this env takes an external disturbance tensor: use step(actions, dstb)")
+        if policy.obs_dim != od:
+            raise ValueError(f"policy obs_dim {policy.obs_dim} != env obs_dim {od}")
+        st = self.lib.cf2_collect_step(
+            self._ctx, actions.data_ptr(), obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
+            _native.ptr(trunc_out), _native.ptr(final_obs_out), policy.w.data_ptr(), od, policy.prec, policy.seed,
+            policy.counter & 0xFFFFFFFF, 0, act_out.data_ptr(), val_out.data_ptr(), logp_out.data_ptr(), self.stream)
+        if st == _native.CF2_ERR_UNSUPPORTED:
+            return False
+        _native.check(st, "cf2_collect_step")
+        policy.counter += 1
+        self._state_version += 1
+        self._obs_latest = obs_out
+        return True
+
     def rollout(self, actions: torch.Tensor, obs_out: torch.Tensor | None = None, rew_out=None, done_out=None,
                 trunc_out=None, cost_out=None, level_out=None, final_obs_out=None):
         """K env-steps in one fused launch (cf2_rollout): actions [K, N, 4]; returns (obs [K, N, D],

@@ -131,6 +131,19 @@ struct StepIO {
 };
 
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
+// The collect loop's policy half, fused behind the env-step (collect_kernel): the actor-critic
+// forward on the new observations (packed bf16x3 fragments of cf2_policy_pack, obs_dim 34)
+struct PolicyIO {
+    const float* w;                 // packed fragments
+    uint32_t key0, key1, counter;   // sampling noise: Philox(seed, counter, row_offset + row)
+    uint32_t row_offset;
+    float* act;                     // [N, 4] sampled actions for the next env-step
+    float* val;                     // [N] V(obs)
+    float* logp;                    // [N] log-probabilities of act
+};
+// returns hipErrorNotSupported when the config has no fused instance (the caller then launches
+// cf2_step and cf2_policy_forward)
+hipError_t launch_collect(const KParams& P, const StepIO& io, const PolicyIO& pio, hipStream_t s);
 // K fused env-steps (state in registers); outputs [K][N][...] slabs, actions at act + k * act_stride
 hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s);
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s);

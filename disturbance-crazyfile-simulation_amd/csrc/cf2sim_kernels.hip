@@ -25,6 +25,7 @@
 #include <stdint.h>
 #include "cf2sim_internal.h"
 #include "cf2sim_rng.h"
+#include "cf2sim_policy.h"
 
 namespace cf2 {
 
@@ -1909,6 +1910,101 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 #endif
 }
 
+// Fused collect step: step_kernel's env-step, then the actor-critic
+// forward on the block's new observations, one launch per env-step of the collect loop.  It
+// replaces the pair env.step (algs/iwpg/iwpg.py:380) + ac.step (:377, algs/core.py:371-395) of
+// IWPGAlgorithm.roll_out as the loop runs them back to back (policy of step t+1 right after the
+// env-step of step t).  With two launches the policy kernel re-reads the obs rows from memory
+// and runs alone, bound by vector issue, while the env-step leaves ~70 % of the issue slots idle
+// waiting on memory; here a block's policy phase runs beside the env phases
+// of the blocks sharing its CU.
+//   * env phase: exactly step_kernel's (same device code: the obs, rewards, flags, final obs and
+//     state are bit-identical to cf2_step's);
+//   * the block's 256 obs rows are still in LDS after the write-out: each wave reads its 64 rows
+//     (4 row tiles) as MFMA B operands into registers, then the block's LDS is re-used for the
+//     packed fragments (52.6 KB: all but layer 3's 8 KB, which the waves read from global memory,
+//     L1/L2-resident), so the kernel keeps step_kernel's 3 blocks per CU (<= 53 KB each);
+//   * policy phase: policy_layers / policy_emit of cf2sim_policy.h on each of the wave's 4 row
+//     tiles: the same instructions as policy_kernel, so act / val / logp are bit-identical to
+//     cf2_policy_forward on the same observations.
+// Built for the bench workload's shape (noise on: 34-wide observations; bf16x3 products) at
+// N > 32 768 (256 envs per block); other configs return hipErrorNotSupported and the caller runs
+// the two launches.
+#ifndef CF2_COLLECT_MIN_WAVES
+#define CF2_COLLECT_MIN_WAVES CF2_STEP_MIN_WAVES
+#endif
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect_kernel(KParams P0, StepIO io,
+                                                                                       PolicyIO pio) {
+    static_assert(NOISE, "the fused collect kernel is built for the 34-wide observation");
+    static_assert(RT == 1, "one 16-row tile per policy chunk");
+    const KParams P = shape_view<SPEC>(P0);
+    if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
+    constexpr int OD = 34;
+    constexpr uint32_t B = CF2_STEP_BLOCK, C = CF2_RESET_CHUNK, W = B / 64u;
+    static_assert(B == 256, "one 64-row wave per SIMD quarter of the block");
+    using PK = Packed<OD, CF2_POLICY_BF16X3>;
+    // LDS: the env phase's arrays, then the fragments but layer 3 (the tail from O_BIAS on moves
+    // down to O_L3)
+    constexpr uint32_t L3N = PK::O_BIAS - PK::O_L3, POL_WORDS = PK::TOTAL - L3N;
+    constexpr uint32_t HJ_AT = (B * OD + B + RESET_SLOTS * 4 * C + W + 1) & ~1u;     // 8-B aligned
+    constexpr uint32_t ENV_WORDS = HJ_AT + 2 * 6 * HJ_PTS;
+    constexpr uint32_t LDS_WORDS = POL_WORDS > ENV_WORDS ? POL_WORDS : ENV_WORDS;
+    static_assert(PK::O_L3 % 4 == 0 && PK::O_BIAS % 4 == 0 && PK::TOTAL % 4 == 0, "float4 staging");
+    __shared__ __align__(16) float s_mem[LDS_WORDS];
+    float* s_obs = s_mem;
+    uint32_t* s_list = reinterpret_cast<uint32_t*>(s_mem + B * OD);
+    uint32_t* s_rand = s_list + B;
+    uint32_t* s_wcnt = s_rand + RESET_SLOTS * 4 * C;
+    double* s_hjgrid = reinterpret_cast<double*>(s_mem + HJ_AT);
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
+    bool do_reset = false;
+    ResetSeed rs;
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
+    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, B);
+    // ---- policy phase.  Lane l of wave wv holds, for row tile c, row 64 wv + 16 c + (l & 15):
+    // inputs 8 g .. 8 g + 7 (k-block 0) and 32 + g (the fp32 k-step; clamped, zero weight past D)
+    const uint32_t l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
+    const int g = (int)(l >> 4);
+    ObsRegs<OD, CF2_POLICY_BF16X3> X[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float* row = s_obs + (64u * wv + 16u * (uint32_t)c + r16) * OD;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float2 v = *reinterpret_cast<const float2*>(row + 8 * g + 2 * q);
+            X[c].x8[0][0][2 * q] = v.x;
+            X[c].x8[0][0][2 * q + 1] = v.y;
+        }
+        X[c].x1[0][0] = row[__builtin_elementwise_min(32 + g, OD - 1)];
+    }
+    __syncthreads();         // every wave holds its rows: the LDS takes the fragments
+    {
+        const float4* src = reinterpret_cast<const float4*>(pio.w);
+        float4* dst = reinterpret_cast<float4*>(s_mem);
+        for (uint32_t k = tid; k < POL_WORDS / 4; k += B) dst[k] = src[k < PK::O_L3 / 4 ? k : k + L3N / 4];
+    }
+    __syncthreads();
+    PolicyLane<OD, CF2_POLICY_BF16X3> CL;
+    policy_lane_init<OD, CF2_POLICY_BF16X3>(s_mem + PK::O_L3, g, CL);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {            // unrolled: X[c] stays in registers
+        int off = 0;
+        asm volatile("" : "+v"(off));        // keep the fragment reads inside the loop (policy_kernel)
+        const float* sw = s_mem + off;
+        ObsRegs<OD, CF2_POLICY_BF16X3> Xc = X[c];
+        policy_standardize<OD, CF2_POLICY_BF16X3>(sw + PK::O_L3, g, CL, Xc);
+        f4v o[1];
+        policy_layers<OD, CF2_POLICY_BF16X3, 0>(sw, sw + PK::O_L3, pio.w + PK::O_L3, (int)l, Xc, o);
+        const uint32_t row = base + 64u * wv + 16u * (uint32_t)c + r16;
+        if (row < P.N)
+            policy_emit<OD, CF2_POLICY_BF16X3, 0>(o[0], row, g, CL, pio.key0, pio.key1, pio.counter, pio.row_offset, 1,
+                                                  pio.act, pio.val, pio.logp, nullptr);
+    }
+}
+
 // Small N (<= 32 768 envs): the launch is as long as one wave's env-step chain, and the auto-reset
 // tail used to be ~40 % of it (section 3 describes this kernel).  Each 256-thread block holds 64 envs.  Wave 0
 // steps them (issue priority 3).  Waves 1-3 meanwhile compute, speculatively for all 64 envs and at
@@ -2749,6 +2845,31 @@ static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t 
     return hipGetLastError();
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
+static hipError_t launch_collect_t(const KParams& P, const StepIO& io, const PolicyIO& pio, hipStream_t s) {
+    if constexpr (!NOISE || SPEC != 1 || PHYS != PHYS_BULLET_T) {
+        return hipErrorNotSupported;
+    } else {
+        if (P.N <= 32768u) return hipErrorNotSupported;     // small N: 64-env blocks (step_kernel_small)
+        static int round_blocks = -1;
+        if (round_blocks < 0) {
+            int dev = 0, cus = 0, per_cu = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, collect_kernel<NOISE, DR, PHYS, SPEC>,
+                                                                 CF2_STEP_BLOCK, 0);
+            if (e != hipSuccess) return e;
+            round_blocks = cus * (per_cu > 0 ? per_cu : 1);
+        }
+        KParams Pl = P;
+        Pl.late_block = (uint32_t)round_blocks;
+        Pl.epb = CF2_STEP_BLOCK;
+        hipLaunchKernelGGL((collect_kernel<NOISE, DR, PHYS, SPEC>), dim3((P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK),
+                           dim3(CF2_STEP_BLOCK), 0, s, Pl, io, pio);
+        return hipGetLastError();
+    }
+}
+template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
     // envs are processed in slices that fit one residency round (blocks resident at once =
     // CUs x blocks per CU): a slice's blocks run all K steps together, so no block waits K steps
@@ -2867,6 +2988,9 @@ extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
 hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
     CF2_DISPATCH(launch_rollout_t, P, io, K, act_stride, s);
+}
+hipError_t launch_collect(const KParams& P, const StepIO& io, const PolicyIO& pio, hipStream_t s) {
+    CF2_DISPATCH(launch_collect_t, P, io, pio, s);
 }
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     CF2_DISPATCH(launch_reset_t, P, sf, mask, obs, s);

@@ -292,6 +292,20 @@ int  cf2_policy_forward(const float* packed_dev, uint32_t n, uint32_t obs_dim, i
 int  cf2_value_forward_masked(const float* packed_dev, uint32_t n, uint32_t obs_dim, int precision,
                               const float* obs_dev, const uint8_t* mask_dev, float* val_dev, void* stream);
 
+/* One step of the collect loop in one launch: the env-step of cf2_step (act_dev -> obs_dev, rew,
+ * done, trunc, final_obs; same arguments, no disturbance tensor, no cost/level outputs), then
+ * cf2_policy_forward(sample = 1) on the new observations -> act_out_dev [N,4] (16-B aligned, the
+ * next env-step's actions; must not be act_dev), val_out_dev [N], logp_out_dev [N].  Replaces the
+ * pair env.step + ac.step of IWPGAlgorithm.roll_out (phoenix_drone_simulation/algs/iwpg/iwpg.py:
+ * 377-380; ActorCritic.step algs/core.py:371-395).  Every output is bit-identical to the two
+ * calls.  Fused only where built (precision CF2_POLICY_BF16X3, obs_dim 34 = sensor noise on, the
+ * default Bullet env-step shape, one drone per formation, N > 32 768); elsewhere it returns
+ * CF2_ERR_UNSUPPORTED and launches nothing, and the caller makes the two calls. */
+int  cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
+                      uint8_t* trunc_dev, float* final_obs_dev, const float* packed_dev, uint32_t obs_dim,
+                      int precision, uint64_t seed, uint32_t counter, uint32_t row_offset, float* act_out_dev,
+                      float* val_out_dev, float* logp_out_dev, void* stream);
+
 /* Batched GAE over [T, n] rollout buffers (algs/core.py:459-535 finish_path on every env's
  * episode slices): done/trunc uint8 (terminal -> bootstrap 0, time-out -> trunc_val), the end of
  * the buffer bootstraps last_val [n].  rew_den > 0: reward scaling, delta uses

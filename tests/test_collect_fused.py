@@ -1,0 +1,118 @@
+"""cf2_collect_step: the collect loop's env-step and the policy forward on its observations in one
+launch (collect_kernel) must equal the two launches (cf2_step + cf2_policy_forward) bit for bit --
+observations, actions, values, log-probabilities, rewards, flags, final observations, the GAE
+outputs and the env state afterwards -- across auto-resets, time-outs, a partial last block and the
+HJ path; configs without a fused instance must fall back to the two launches.
+The collect loop being restated is IWPGAlgorithm.roll_out (algs/iwpg/iwpg.py:372-410)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("DroneHoverBulletFreeEnvWithGust-v0", 40000, {}),                                    # bench workload, partial block
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", 33024, dict(max_episode_steps=7, domain_randomization=0)),
+    ("DroneHoverBulletFreeEnvWithRandomAdversary-v0", 65536, dict(max_episode_steps=11)),
+]
+
+
+def _pair(env_id, n, kw, setup=None):
+    from cf2sim.rollout import FusedActorCritic, MLPActorCritic
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    envs = [BatchedCrazyflieEnv(env_id, n, seed=11, want_final_obs=True, **kw) for _ in range(2)]
+    torch.manual_seed(5)
+    ac = MLPActorCritic(obs_dim=envs[0].obs_dim).cuda()
+    with torch.no_grad():                    # non-trivial standardisation, as after a few epochs
+        ac.obs_oms.mean.uniform_(-0.2, 0.2)
+        ac.obs_oms.std.uniform_(0.5, 2.0)
+        ac.ret_oms.std.fill_(3.0)
+    out = []
+    for e in envs:
+        if setup is not None:
+            setup(e)
+        out.append((e, FusedActorCritic(ac, seed=7, precision="bf16x3")))
+    return out
+
+
+def _check_equal(ra, rb):
+    for f in ("obs", "act", "rew", "val", "logp", "done", "trunc", "adv", "ret", "last_obs", "last_val", "trunc_val",
+              "discounted_ret"):
+        a, b = getattr(ra, f), getattr(rb, f)
+        assert torch.equal(a, b), f"{f}: max |diff| {(a.float() - b.float()).abs().max().item()}"
+
+
+def _run(env_id, n, kw, setup=None, T=24):
+    from cf2sim.rollout import collect
+    (ea, pa), (eb, pb) = _pair(env_id, n, kw, setup)
+    oa, ob = ea.reset(), eb.reset()
+    launched = []
+    orig = ea.collect_step_into
+
+    def spy(*args, **kwargs):
+        ok = orig(*args, **kwargs)
+        launched.append(ok)
+        return ok
+    ea.collect_step_into = spy
+    ra = collect(ea, pa, T, obs=oa.clone(), fuse=True)
+    rb = collect(eb, pb, T, obs=ob.clone(), fuse=False)
+    torch.cuda.synchronize()
+    assert ra.done.any(), "no auto-reset inside the window"
+    _check_equal(ra, rb)
+    gs, gi = ea.get_state()
+    rs, ri = eb.get_state()
+    assert torch.equal(gi, ri) and torch.equal(gs, rs)
+    assert pa.counter == pb.counter
+    # a second collect continues from the first one's last observation
+    ra2 = collect(ea, pa, 5, obs=ra.last_obs, fuse=True)
+    rb2 = collect(eb, pb, 5, obs=rb.last_obs, fuse=False)
+    _check_equal(ra2, rb2)
+    ea.close()
+    eb.close()
+    return launched
+
+
+@pytest.mark.parametrize("env_id,n,kw", CASES)
+def test_fused_collect_equals_two_launches(gpu, env_id, n, kw):
+    launched = _run(env_id, n, kw)
+    assert launched and all(launched), "the fused kernel did not run"
+
+
+def test_fused_collect_hj_boltzmann(gpu):
+    from test_gpu_parity import _synthetic_tables
+    V = torch.from_numpy(_synthetic_tables(tuple(range(3)), seed=1)).cuda()
+    tol = [lv % 3 for lv in range(21)]
+    launched = _run("DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", 40000, dict(max_episode_steps=6),
+                    setup=lambda e: e.bind_hj_tables(V, tol), T=12)
+    assert launched and all(launched)
+
+
+@pytest.mark.parametrize("env_id,n,kw", [
+    ("DroneHoverBulletFreeEnvWithGust-v0", 4096, {}),                         # small N: no fused instance
+    ("DroneHoverBulletFreeEnvWithGust-v0", 40000, dict(observation_noise=0)),  # 42-wide obs
+    ("DroneHoverSimpleEnv-v0", 40000, {}),
+])
+def test_unfused_configs_fall_back(gpu, env_id, n, kw):
+    launched = _run(env_id, n, kw, T=8)
+    assert launched == [False, False], "an unsupported config launches nothing and is probed once per collect"
+
+
+def test_collect_step_rejects_bad_args(gpu):
+    from cf2sim import _native
+    (e, p), _ = _pair("DroneHoverBulletFreeEnvWithGust-v0", 40000, {})
+    n, d = e.num_envs, e.obs_dim
+    e.reset()
+    a = torch.zeros(n, 4, device=gpu)
+    o = torch.empty(n, d, device=gpu)
+    r = torch.empty(n, device=gpu)
+    dn = torch.empty(n, dtype=torch.uint8, device=gpu)
+    v, lp = torch.empty(n, device=gpu), torch.empty(n, device=gpu)
+    with pytest.raises(ValueError):           # wrong shape of the next actions
+        e.collect_step_into(a, o, r, dn, None, None, p, torch.empty(n, 3, device=gpu), v, lp)
+    st = e.lib.cf2_collect_step(e._ctx, a.data_ptr(), o.data_ptr(), r.data_ptr(), dn.data_ptr(), None, None,
+                                p.w.data_ptr(), d, p.prec, 0, 0, 0, a.data_ptr(), v.data_ptr(), lp.data_ptr(), e.stream)
+    assert st != 0, "act_out aliasing act must be rejected"
+    st = e.lib.cf2_collect_step(e._ctx, a.data_ptr(), o.data_ptr(), r.data_ptr(), dn.data_ptr(), None, None,
+                                p.w.data_ptr(), d + 8, p.prec, 0, 0, 0, torch.empty(n, 4, device=gpu).data_ptr(),
+                                v.data_ptr(), lp.data_ptr(), e.stream)
+    assert st != 0 and st != _native.CF2_ERR_UNSUPPORTED, "an obs_dim that is not the env's is an error"
+    e.close()

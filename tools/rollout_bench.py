@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--torch-policy", action="store_true", help="torch layers instead of the fused HIP policy")
     ap.add_argument("--precision", default="fp32", help="fused policy products: fp32 | bf16x3")
     ap.add_argument("--max-episode-steps", type=int, default=500, help="TimeLimit (shorter: more time-outs)")
+    ap.add_argument("--no-fuse", action="store_true", help="two launches per step (cf2_step + cf2_policy_forward)")
     ap.add_argument("--env-warmup", type=int, default=1000, help="random-action env-steps before the collects")
     args = ap.parse_args()
     from cf2sim.rollout import FusedActorCritic, MLPActorCritic, collect
@@ -37,12 +38,12 @@ def main():
     obs = obs.clone()
     # warm-up at the timed length: kernels, GEMM heuristics, and the caching allocator's blocks for
     # the [T, N, ...] rollout storage (a training loop collects the same T every epoch)
-    ro = collect(envs, ac, args.steps, obs=obs, generator=g)
+    ro = collect(envs, ac, args.steps, obs=obs, generator=g, fuse=not args.no_fuse)
     torch.cuda.synchronize()
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        ro = collect(envs, ac, args.steps, obs=ro.last_obs, generator=g)
+        ro = collect(envs, ac, args.steps, obs=ro.last_obs, generator=g, fuse=not args.no_fuse)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
     # split: policy forward alone vs env step alone on the same sizes
@@ -65,7 +66,8 @@ def main():
                       "policy_ms_per_step": pol_ms, "env_ms_per_step": env_ms, "envs": args.envs,
                       "steps": args.steps, "env_id": args.env_id, "max_episode_steps": args.max_episode_steps,
                       "timeouts_per_step": float(ro.trunc.float().mean()) * args.envs,
-                      "policy": "torch" if args.torch_policy else f"fused HIP ({args.precision})"}))
+                      "policy": "torch" if args.torch_policy else f"fused HIP ({args.precision})",
+                      "collect_step": "two launches" if args.no_fuse or args.torch_policy else "cf2_collect_step where built"}))
     envs.close()
 
 
