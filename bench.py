@@ -215,6 +215,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-envs", type=int, default=16384)
     ap.add_argument("--cpu-steps", type=int, default=1000)
     ap.add_argument("--env-kw", default="{}", help="JSON env kwargs (ablations), e.g. '{\"observation_noise\": 0}'")
+    ap.add_argument("--collect-steps", type=int, default=32,
+                    help="steps per collect of the f3 line (rollout.collect, fused env + policy; 0 = skip)")
     ap.add_argument("--rollout-k", type=int, default=32,
                     help="also time the fused K-step rollout (cf2_rollout, random actions) on 1 GPU; 0 = skip")
     return ap.parse_args(argv)
@@ -438,6 +440,31 @@ def main(argv=None):
                  "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[1]}
         del racts
 
+    collect_line = None
+    if world == 1 and args.collect_steps > 0:
+        # the f3 caller: PPO/IWPG data collection (algs/iwpg/iwpg.py:372-410) over the batch with the
+        # reference's default actor-critic (random init), one cf2_collect_step launch per env-step
+        # (env-step + policy forward on its observations), GAE and the time-out values after the loop
+        from cf2sim.rollout import FusedActorCritic, MLPActorCritic, collect
+        cenv = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, device=dev, want_final_obs=True, **env_kw)
+        bind_synthetic_tables(cenv, dev)
+        cac = FusedActorCritic(MLPActorCritic(obs_dim=cenv.obs_dim).to(dev), seed=args.seed, precision="bf16x3")
+        T = args.collect_steps
+        ro = collect(cenv, cac, T)           # warm-up: kernels, the rollout storage's allocator blocks
+        torch.cuda.synchronize()
+        reps = 2
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ro = collect(cenv, cac, T, obs=ro.last_obs)
+        torch.cuda.synchronize()
+        cus = (time.perf_counter() - t0) * 1e6 / (reps * T)
+        collect_line = {"value": n / (cus * 1e-6), "unit": "env-steps/s", "us_per_env_step": cus,
+                        "steps_per_collect": T, "policy": "MLP actor-critic 34-50-50-4 / 34-64-64-1, bf16x3",
+                        "one_launch_per_env_step": bool(cenv.last_collect_fused),
+                        "includes": "env-step, policy forward + sampling, rollout storage, GAE, time-out values"}
+        cenv.close()
+        del ro
+
     streaming = None
     if world == 1 and args.streaming_ring > 0:
         # the same env-step with the actions cycled through a ring larger than the Infinity Cache
@@ -568,6 +595,7 @@ def main(argv=None):
             "no_gather": no_gather,
             "weak_scaling": weak,
             "fused_rollout": fused,
+            "collect": collect_line,
             "streaming_actions": streaming,
         }
         print(json.dumps(line), flush=True)

@@ -29,7 +29,11 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
 # (tests/test_gpu_fullsize.py, contexts of 131 072 / 65 536 / 2 x 32 768 against one of 262 144) at
 # no measured cost (262 144 envs 36.08-36.19 vs 36.06-36.13 us, 32 768 envs within noise).
 SOURCE_FLAGS = {"cf2sim_kernels.hip": ["-fno-slp-vectorize", "-ffp-contract=on"], "cf2sim_api.cpp": ["-fno-slp-vectorize"],
-                "cf2sim_policy.hip": ["-fno-slp-vectorize"]}
+                "cf2sim_policy.hip": ["-fno-slp-vectorize", "-ffp-contract=on"]}
+# The policy TU contracts like the env kernels too: the fused collect kernel (cf2sim_kernels.hip)
+# runs the same policy code (cf2sim_policy.h), and with "fast" the policy kernel alone fused the
+# standardisation's product into the hi/lo split's subtraction (8 v_fma instead of v_sub), so the
+# two paths' actions and values differed in the last bit in ~20 % of rows.
 
 
 def _hipcc() -> str:

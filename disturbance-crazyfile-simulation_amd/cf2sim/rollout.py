@@ -390,6 +390,7 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         for t0 in range(0, steps, per):                      # V(final obs) of the time-outs only
             t1 = min(steps, t0 + per)
             ac.value_masked(fin[t0:t1].view(-1, d), tr8[t0:t1].view(-1), trunc_val[t0:t1].view(-1))
+        envs.last_collect_fused = fuse         # every env-step ran as one cf2_collect_step launch
         o = obs_buf[steps]
         adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True)
         buf_o, buf_d, buf_tr = obs_buf[:steps], d8.view(torch.bool), tr8.view(torch.bool)   # 0/1 bytes

@@ -70,6 +70,7 @@ class BatchedCrazyflieEnv:
         self.cost = torch.zeros(n, dtype=torch.float32, device=d)
         self.level = torch.zeros(n, dtype=torch.float32, device=d)
         self.want_final_obs = want_final_obs
+        self.last_collect_fused = False      # set by rollout.collect: its env-steps ran as cf2_collect_step
         self.final_obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=d) if want_final_obs else None
         # the observations of the latest reset / step: self.obs, or the caller buffer (slab) that
         # step_into / rollout / step_raw wrote them to (what save_checkpoint saves)

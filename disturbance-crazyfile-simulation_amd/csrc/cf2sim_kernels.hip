@@ -1933,14 +1933,26 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 #ifndef CF2_COLLECT_MIN_WAVES
 #define CF2_COLLECT_MIN_WAVES CF2_STEP_MIN_WAVES
 #endif
+#ifndef CF2_COLLECT_RT
+#define CF2_COLLECT_RT 1      // row tiles per forward call; 2 (two chains interleaved, 163 VGPRs): same time
+#endif
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect_kernel(KParams P0, StepIO io,
                                                                                        PolicyIO pio) {
     static_assert(NOISE, "the fused collect kernel is built for the 34-wide observation");
-    static_assert(RT == 1, "one 16-row tile per policy chunk");
     const KParams P = shape_view<SPEC>(P0);
     if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
+#ifdef CF2_COLLECT_STAGGER
+    // A/B: the g-th third of the first round's blocks (one block per CU each) starts g * STAGGER
+    // cycles late, so co-resident blocks reach their policy phases at different times.  Measured
+    // slower at every delay (262 144 envs: 4k / 10k / 20k cycles 62.1 / 64.1 / 67.2 us against
+    // 61.1 us; profiles/r03_collect_ab.txt)
+    if (blockIdx.x < P0.late_block) {
+        const uint32_t g3 = blockIdx.x / (P0.late_block / 3u);
+        for (uint32_t k = 0; k < g3 * (CF2_COLLECT_STAGGER / 512); ++k) __builtin_amdgcn_s_sleep(8);
+    }
+#endif
     constexpr int OD = 34;
     constexpr uint32_t B = CF2_STEP_BLOCK, C = CF2_RESET_CHUNK, W = B / 64u;
     static_assert(B == 256, "one 64-row wave per SIMD quarter of the block");
@@ -1964,44 +1976,76 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, B);
+#if defined(CF2_COLLECT_AB) && CF2_COLLECT_AB == 1
+    return;                  // A/B only: the env phase alone
+#endif
     // ---- policy phase.  Lane l of wave wv holds, for row tile c, row 64 wv + 16 c + (l & 15):
     // inputs 8 g .. 8 g + 7 (k-block 0) and 32 + g (the fp32 k-step; clamped, zero weight past D)
     const uint32_t l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
     const int g = (int)(l >> 4);
-    ObsRegs<OD, CF2_POLICY_BF16X3> X[4];
+    constexpr int CR = CF2_COLLECT_RT, NCH = 4 / CR;          // row tiles per forward call, calls per wave
+    ObsRegs<OD, CF2_POLICY_BF16X3, CR> X[NCH];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const float* row = s_obs + (64u * wv + 16u * (uint32_t)c + r16) * OD;
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float2 v = *reinterpret_cast<const float2*>(row + 8 * g + 2 * q);
-            X[c].x8[0][0][2 * q] = v.x;
-            X[c].x8[0][0][2 * q + 1] = v.y;
+        for (int rt = 0; rt < CR; ++rt) {
+            const float* row = s_obs + (64u * wv + 16u * (uint32_t)(CR * c + rt) + r16) * OD;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float2 v = *reinterpret_cast<const float2*>(row + 8 * g + 2 * q);
+                X[c].x8[rt][0][2 * q] = v.x;
+                X[c].x8[rt][0][2 * q + 1] = v.y;
+            }
+            X[c].x1[rt][0] = row[__builtin_elementwise_min(32 + g, OD - 1)];
         }
-        X[c].x1[0][0] = row[__builtin_elementwise_min(32 + g, OD - 1)];
-    }
     __syncthreads();         // every wave holds its rows: the LDS takes the fragments
+    // fragment loads first; while they are in flight each lane draws the sampling noise of the
+    // wave's row 64 wv + l (one Philox block per row, instead of one per row tile on all 64 lanes)
+    constexpr uint32_t NQ4 = POL_WORDS / 4, NQ = (NQ4 + B - 1) / B;
+    float4 stg[NQ];
     {
         const float4* src = reinterpret_cast<const float4*>(pio.w);
+#pragma unroll
+        for (uint32_t q = 0; q < NQ; ++q) {
+            const uint32_t k = __builtin_elementwise_min(tid + q * B, NQ4 - 1u);
+            stg[q] = src[k < PK::O_L3 / 4 ? k : k + L3N / 4];
+        }
+    }
+    float ep[4];
+    policy_noise(pio.key0, pio.key1, pio.counter, pio.row_offset + base + 64u * wv + l, ep);
+    {
         float4* dst = reinterpret_cast<float4*>(s_mem);
-        for (uint32_t k = tid; k < POL_WORDS / 4; k += B) dst[k] = src[k < PK::O_L3 / 4 ? k : k + L3N / 4];
+#pragma unroll
+        for (uint32_t q = 0; q < NQ; ++q)
+            if (tid + q * B < NQ4) dst[tid + q * B] = stg[q];
     }
     __syncthreads();
+#if defined(CF2_COLLECT_AB) && CF2_COLLECT_AB == 2
+    if (X[0].x1[0][0] == 12345.0f) pio.val[i] = s_mem[tid];      // A/B only: staging, no forward
+    return;
+#endif
     PolicyLane<OD, CF2_POLICY_BF16X3> CL;
     policy_lane_init<OD, CF2_POLICY_BF16X3>(s_mem + PK::O_L3, g, CL);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {            // unrolled: X[c] stays in registers
+    for (int c = 0; c < NCH; ++c) {          // unrolled: X[c] stays in registers
         int off = 0;
         asm volatile("" : "+v"(off));        // keep the fragment reads inside the loop (policy_kernel)
         const float* sw = s_mem + off;
-        ObsRegs<OD, CF2_POLICY_BF16X3> Xc = X[c];
-        policy_standardize<OD, CF2_POLICY_BF16X3>(sw + PK::O_L3, g, CL, Xc);
-        f4v o[1];
-        policy_layers<OD, CF2_POLICY_BF16X3, 0>(sw, sw + PK::O_L3, pio.w + PK::O_L3, (int)l, Xc, o);
-        const uint32_t row = base + 64u * wv + 16u * (uint32_t)c + r16;
-        if (row < P.N)
-            policy_emit<OD, CF2_POLICY_BF16X3, 0>(o[0], row, g, CL, pio.key0, pio.key1, pio.counter, pio.row_offset, 1,
-                                                  pio.act, pio.val, pio.logp, nullptr);
+        ObsRegs<OD, CF2_POLICY_BF16X3, CR> Xc = X[c];
+        policy_standardize<OD, CF2_POLICY_BF16X3, CR>(sw + PK::O_L3, g, CL, Xc);
+        f4v o[CR];
+        policy_layers<OD, CF2_POLICY_BF16X3, 0, CR>(sw, sw + PK::O_L3, pio.w + PK::O_L3, (int)l, Xc, o);
+#pragma unroll
+        for (int rt = 0; rt < CR; ++rt) {
+            const uint32_t wr = 16u * (uint32_t)(CR * c + rt) + r16, row = base + 64u * wv + wr;
+            float e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)      // row wr's noise from lane wr
+                e[k] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(wr << 2), __float_as_int(ep[k])));
+            if (row < P.N)
+                policy_emit_eps<OD, CF2_POLICY_BF16X3, 0>(o[rt], row, g, CL, e, 1, pio.act, pio.val, pio.logp,
+                                                          nullptr);
+        }
     }
 }
 

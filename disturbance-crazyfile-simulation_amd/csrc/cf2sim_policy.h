@@ -237,12 +237,12 @@ constexpr int PB = CF2_POLICY_BLOCK, PW = PB / 64;
 // (indices clamped into the buffer): a row past n is never written out and an input index past
 // D meets a zero weight; branch-free loads keep the waitcnt counting exact, so the prefetch of
 // the next chunk stays in flight under this chunk's MFMAs.
-template <int D, int PREC>
+template <int D, int PREC, int R = RT>
 struct ObsRegs {
     using P = Packed<D, PREC>;
-    float x8[RT][P::KB1 > 0 ? P::KB1 : 1][8];
-    float x1[RT][P::KS1 > 0 ? P::KS1 : 1];
-    float xr[RT][P::SL ? P::R1 : 1];
+    float x8[R][P::KB1 > 0 ? P::KB1 : 1][8];
+    float x1[R][P::KS1 > 0 ? P::KS1 : 1];
+    float xr[R][P::SL ? P::R1 : 1];
 };
 template <int D, int PREC>
 __device__ __forceinline__ void load_obs(const float* __restrict__ obs, uint32_t n, uint32_t r0, int l,
@@ -306,9 +306,9 @@ __device__ __forceinline__ void policy_lane_init(const float* sb, int g, PolicyL
 
 // observation standardisation (obs - mean) * scale, per input index of this lane; the k-block
 // constants are re-read from LDS per chunk (16 fewer live VGPRs than holding them)
-template <int D, int PREC>
+template <int D, int PREC, int R = RT>
 __device__ __forceinline__ void policy_standardize(const float* sb, int g, const PolicyLane<D, PREC>& C,
-                                                   ObsRegs<D, PREC>& Xc) {
+                                                   ObsRegs<D, PREC, R>& Xc) {
     using P = Packed<D, PREC>;
     constexpr int T_MEAN = P::O_MEAN - P::O_BIAS, T_SCALE = P::O_SCALE - P::O_BIAS;
     float mean8[P::KB1 > 0 ? P::KB1 : 1][8], scale8[P::KB1 > 0 ? P::KB1 : 1][8];
@@ -322,7 +322,7 @@ __device__ __forceinline__ void policy_standardize(const float* sb, int g, const
             scale8[kb][4 * q] = sc.x; scale8[kb][4 * q + 1] = sc.y; scale8[kb][4 * q + 2] = sc.z; scale8[kb][4 * q + 3] = sc.w;
         }
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
+    for (int rt = 0; rt < R; ++rt) {
 #pragma unroll
         for (int kb = 0; kb < P::KB1; ++kb)
 #pragma unroll
@@ -337,9 +337,10 @@ __device__ __forceinline__ void policy_standardize(const float* sb, int g, const
 
 // layers 1-3 on standardised inputs.  MODE 0: both networks (o: lanes 0..15 mu[0..3] of row
 // l & 15, lanes 16..31 v in register 0); MODE 1: the v network only.
-template <int D, int PREC, int MODE>
+template <int D, int PREC, int MODE, int R = RT>
 __device__ __forceinline__ void policy_layers(const float* sw, const float* sb, const float* l3, int l,
-                                              const ObsRegs<D, PREC>& Xc, f4v (&o)[RT]) {
+                                              const ObsRegs<D, PREC, R>& Xc, f4v (&o)[R]) {
+    constexpr int RT = R;      // row tiles of this call (each fragment read feeds R MFMAs)
     using P = Packed<D, PREC>;
     constexpr bool PI = MODE == 0, BF = P::BF;
     constexpr int T_BIAS = 0;
@@ -500,23 +501,16 @@ __device__ __forceinline__ void policy_layers(const float* sw, const float* sb, 
 }
 
 // Outputs of one row from the layer-3 tile (lanes 0..15 hold mu[0..3] of row 16 rt + l, lanes
-// 16..31 hold v in register 0): the value, and in MODE 0 the Gaussian sample a = mu + std * eps with
-// eps from Philox(seed, counter, row_offset + row) and its log-probability (core.py:253-291)
+// 16..31 hold v in register 0): the value, and in MODE 0 the Gaussian sample a = mu + std * eps
+// and its log-probability (core.py:253-291), eps given (lanes 0..15)
 template <int D, int PREC, int MODE>
-__device__ __forceinline__ void policy_emit(const f4v& o, uint32_t row, int g, const PolicyLane<D, PREC>& C,
-                                            uint32_t key0, uint32_t key1, uint32_t counter, uint32_t row_offset,
-                                            int sample, float* __restrict__ act, float* __restrict__ val,
-                                            float* __restrict__ logp, const uint8_t* __restrict__ mask) {
+__device__ __forceinline__ void policy_emit_eps(const f4v& o, uint32_t row, int g, const PolicyLane<D, PREC>& C,
+                                                const float (&eps)[4], int sample, float* __restrict__ act,
+                                                float* __restrict__ val, float* __restrict__ logp,
+                                                const uint8_t* __restrict__ mask) {
     constexpr bool PI = MODE == 0;
     if (g == 1 && (MODE == 0 || mask[row])) val[row] = o[0];
     if (PI && g == 0) {
-        float eps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (sample) {
-            const Keys K = make_keys(key0, key1);
-            const U4 u = philox(K, 0u, counter, row_offset + row, TAG_POLICY);
-            box_muller(u.x, u.y, eps[0], eps[1]);
-            box_muller(u.z, u.w, eps[2], eps[3]);
-        }
         float lp = 0.0f;
         float4 a;
         float* ap = &a.x;
@@ -528,6 +522,23 @@ __device__ __forceinline__ void policy_emit(const f4v& o, uint32_t row, int g, c
         reinterpret_cast<float4*>(act)[row] = a;
         if (logp) logp[row] = sample ? lp : 1.0f;
     }
+}
+// the sampling noise of one row: Philox(seed, counter, row_offset + row), two Box-Muller pairs
+__device__ __forceinline__ void policy_noise(uint32_t key0, uint32_t key1, uint32_t counter, uint32_t prow,
+                                             float (&eps)[4]) {
+    const Keys K = make_keys(key0, key1);
+    const U4 u = philox(K, 0u, counter, prow, TAG_POLICY);
+    box_muller(u.x, u.y, eps[0], eps[1]);
+    box_muller(u.z, u.w, eps[2], eps[3]);
+}
+template <int D, int PREC, int MODE>
+__device__ __forceinline__ void policy_emit(const f4v& o, uint32_t row, int g, const PolicyLane<D, PREC>& C,
+                                            uint32_t key0, uint32_t key1, uint32_t counter, uint32_t row_offset,
+                                            int sample, float* __restrict__ act, float* __restrict__ val,
+                                            float* __restrict__ logp, const uint8_t* __restrict__ mask) {
+    float eps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (MODE == 0 && g == 0 && sample) policy_noise(key0, key1, counter, row_offset + row, eps);
+    policy_emit_eps<D, PREC, MODE>(o, row, g, C, eps, sample, act, val, logp, mask);
 }
 
 }  // namespace cf2
