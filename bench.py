@@ -450,9 +450,14 @@ def main(argv=None):
         bind_synthetic_tables(cenv, dev)
         cac = FusedActorCritic(MLPActorCritic(obs_dim=cenv.obs_dim).to(dev), seed=args.seed, precision="bf16x3")
         T = args.collect_steps
-        ro = collect(cenv, cac, T)           # warm-up: kernels, the rollout storage's allocator blocks
+        cenv.reset()
+        wact = torch.rand(8, n, 4, device=dev, generator=g) * 2 - 1
+        for k in range(500):                 # past the synchronised-start transient
+            cenv.step_raw(wact[k % 8].data_ptr())
+        del wact
+        ro = collect(cenv, cac, T, obs=cenv.obs.clone())   # warm-up: kernels, the rollout storage's blocks
         torch.cuda.synchronize()
-        reps = 2
+        reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
             ro = collect(cenv, cac, T, obs=ro.last_obs)
