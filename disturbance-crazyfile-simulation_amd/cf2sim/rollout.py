@@ -74,6 +74,17 @@ class OnlineMeanStd(nn.Module):
         x_new = (x - self.mean) / (self.std + self.eps) if subtract_mean else x / (self.std + self.eps)
         return torch.clamp(x_new, -self.bound, self.bound) if clip else x_new
 
+    def std_host(self) -> float:
+        """std as a host float (shape (1,) statistics), re-read from the device only after the
+        buffer changed (in place or replaced): collect() needs it every epoch for reward scaling,
+        and a device read would drain the GPU's queue at the start of every collect."""
+        t = self.std
+        if getattr(self, "_std_host_key", None) is None or self._std_host_key[0] is not t \
+                or self._std_host_key[1] != t._version:
+            self._std_host = float(t.item())
+            self._std_host_key = (t, t._version)
+        return self._std_host
+
     @torch.no_grad()
     def update(self, x: torch.Tensor) -> None:
         x = torch.as_tensor(x, dtype=torch.float32, device=self.mean.device)
@@ -364,7 +375,7 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
     trunc_val = torch.zeros(steps, n, device=dev)
     fused = isinstance(ac, FusedActorCritic)
     module = ac.ac if fused else ac
-    rew_den = float(module.ret_oms.std.item() + module.ret_oms.eps) if module.ret_oms is not None else None
+    rew_den = module.ret_oms.std_host() + module.ret_oms.eps if module.ret_oms is not None else None
     if fused:
         # zero-copy: the policy and the env write straight into the rollout storage
         obs_buf = torch.empty(steps + 1, n, d, device=dev)

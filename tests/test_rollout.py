@@ -216,3 +216,17 @@ def test_gae_kernel_matches_reference(gpu):
                                trunc_val[:, k].astype(np.float64), float(last_val[k]), 0.99, 0.95)
         np.testing.assert_allclose(adv[:, k], ra, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(ret[:, k], rr, rtol=1e-4, atol=1e-4)
+
+
+def test_return_std_host_mirror_follows_every_change():
+    """collect() reads the return std on the host without a device sync per epoch (OnlineMeanStd.
+    std_host caches it); the mirror must follow update(), in-place edits and a replaced buffer."""
+    from cf2sim.rollout import OnlineMeanStd
+    oms = OnlineMeanStd(shape=(1,))
+    assert oms.std_host() == 1.0
+    oms.update(torch.tensor([1.0, 3.0, 5.0]))
+    assert oms.std_host() == pytest.approx(float(oms.std.item()))
+    oms.std.fill_(2.5)
+    assert oms.std_host() == 2.5
+    oms.std = torch.full((1,), 4.0)
+    assert oms.std_host() == 4.0
