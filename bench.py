@@ -460,13 +460,14 @@ def main(argv=None):
         reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
-            ro = collect(cenv, cac, T, obs=ro.last_obs)
+            ro = collect(cenv, cac, T, obs=ro.last_obs, out=ro)   # storage re-used, as every training epoch
         torch.cuda.synchronize()
         cus = (time.perf_counter() - t0) * 1e6 / (reps * T)
         collect_line = {"value": n / (cus * 1e-6), "unit": "env-steps/s", "us_per_env_step": cus,
                         "steps_per_collect": T, "policy": "MLP actor-critic 34-50-50-4 / 34-64-64-1, bf16x3",
                         "one_launch_per_env_step": bool(cenv.last_collect_fused),
-                        "includes": "env-step, policy forward + sampling, rollout storage, GAE, time-out values"}
+                        "includes": "env-step, policy forward + sampling, rollout storage (re-used across collects), GAE, "
+                                    "time-out values"}
         cenv.close()
         del ro
 

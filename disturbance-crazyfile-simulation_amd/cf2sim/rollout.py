@@ -242,6 +242,7 @@ class FusedActorCritic:
         flat = pack_policy_weights(self.ac).to(dev)
         assert flat.numel() == self.lib.cf2_policy_weights_count(self.obs_dim)
         self.w = torch.empty(self.lib.cf2_policy_packed_count(self.obs_dim, self.prec), device=dev)
+        self.w_ptr = self.w.data_ptr()
         _native.check(self.lib.cf2_policy_pack(flat.data_ptr(), self.obs_dim, self.prec, self.w.data_ptr(),
                                                torch.cuda.current_stream(dev).cuda_stream), "cf2_policy_pack")
 
@@ -318,13 +319,21 @@ def gae(rew, val, done, trunc, last_val, trunc_val, gamma: float = 0.99, lam: fl
 
 
 def gae_device(rew, val, done_u8, trunc_u8, last_val, trunc_val, gamma: float = 0.99, lam: float = 0.95,
-               rew_den: float | None = None, with_discounted: bool = False):
-    """``gae`` as one HIP launch (cf2_gae): one thread per env scans T backward."""
+               rew_den: float | None = None, with_discounted: bool = False, out=None):
+    """``gae`` as one HIP launch (cf2_gae): one thread per env scans T backward.  out: optional
+    (adv, ret, disc) [T, N] float32 buffers to write."""
     from . import _native
     T, n = rew.shape
-    adv = torch.empty_like(rew)
-    ret = torch.empty_like(rew)
-    disc = torch.empty_like(rew) if with_discounted else None
+    if out is not None:
+        adv, ret, disc = out
+        for b in (adv, ret) + ((disc,) if with_discounted else ()):
+            if b.shape != rew.shape or b.dtype != torch.float32 or not b.is_contiguous() or b.device != rew.device:
+                raise ValueError("gae_device out buffers must be contiguous float32 [T, N] on the same device")
+        disc = disc if with_discounted else None
+    else:
+        adv = torch.empty_like(rew)
+        ret = torch.empty_like(rew)
+        disc = torch.empty_like(rew) if with_discounted else None
     lib = _native.load()
     _native.check(lib.cf2_gae(T, n, rew.contiguous().data_ptr(), val.contiguous().data_ptr(),
                               done_u8.contiguous().data_ptr(), trunc_u8.contiguous().data_ptr(),
@@ -350,51 +359,74 @@ class Rollout:
     last_val: torch.Tensor   # [N] V(last_obs)
     trunc_val: torch.Tensor  # [T, N] V(pre-reset obs), used where trunc
     discounted_ret: torch.Tensor  # [T, N] per-episode discounted returns (return statistics)
+    # the fused path's buffers, re-used by collect(..., out=this rollout)
+    storage: dict | None = dataclasses.field(default=None, repr=False, compare=False)
+
+
+def _fused_storage(steps: int, n: int, d: int, dev) -> dict:
+    """The fused collect path's rollout storage: observations [T+1, N, D] (slab 0 = the start
+    observation), final observations [T, N, D] (rows written where an episode ended), actions,
+    values, log-probabilities, rewards, uint8 done / truncation flags, GAE outputs and scratch for
+    the policy call on the last observation."""
+    e = lambda *shape, dt=torch.float32: torch.empty(*shape, device=dev, dtype=dt)
+    return {"key": (steps, n, d, str(dev)), "obs": e(steps + 1, n, d), "fin": e(steps, n, d), "act": e(steps, n, 4),
+            "rew": e(steps, n), "val": e(steps, n), "logp": e(steps, n), "d8": e(steps, n, dt=torch.uint8),
+            "tr8": e(steps, n, dt=torch.uint8), "trunc_val": e(steps, n), "adv": e(steps, n), "ret": e(steps, n),
+            "disc": e(steps, n), "last_val": e(n), "a_last": e(n, 4), "lp_last": e(n)}
 
 
 @torch.no_grad()
 def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float = 0.99,
-            lam: float = 0.95, generator: torch.Generator | None = None, fuse: bool = True) -> Rollout:
+            lam: float = 0.95, generator: torch.Generator | None = None, fuse: bool = True,
+            out: Rollout | None = None) -> Rollout:
     """``roll_out`` for all envs of a BatchedCrazyflieEnv at once; everything stays on the GPU.
     ``ac`` is an MLPActorCritic (torch layers) or a FusedActorCritic (HIP kernels).  With a
     FusedActorCritic and ``fuse`` each env-step and the policy forward on its observations are one
     launch (cf2_collect_step) where the config has a fused instance, else two launches; the
-    results are bit-identical either way.
+    results are bit-identical either way.  ``out``: a Rollout of an earlier fused collect of the
+    same shape whose storage is re-used (its tensors are overwritten; ``obs=out.last_obs`` is
+    allowed), as a training loop collecting every epoch would.
     ``envs`` must have been created with want_final_obs=True (time-out bootstrapping)."""
     if envs.final_obs is None:
         raise ValueError("collect() needs BatchedCrazyflieEnv(..., want_final_obs=True)")
     n, d, dev = envs.num_envs, envs.obs_dim, envs.device
     o = envs.reset() if obs is None else obs
-    buf_o = torch.empty(steps, n, d, device=dev)
-    buf_a = torch.empty(steps, n, 4, device=dev)
-    buf_r = torch.empty(steps, n, device=dev)
-    buf_v = torch.empty(steps, n, device=dev)
-    buf_lp = torch.empty(steps, n, device=dev)
-    buf_d = torch.empty(steps, n, dtype=torch.bool, device=dev)
-    buf_tr = torch.empty(steps, n, dtype=torch.bool, device=dev)
-    trunc_val = torch.zeros(steps, n, device=dev)
     fused = isinstance(ac, FusedActorCritic)
     module = ac.ac if fused else ac
     rew_den = module.ret_oms.std_host() + module.ret_oms.eps if module.ret_oms is not None else None
     if fused:
         # zero-copy: the policy and the env write straight into the rollout storage
-        obs_buf = torch.empty(steps + 1, n, d, device=dev)
-        obs_buf[0] = o
-        d8 = torch.empty(steps, n, dtype=torch.uint8, device=dev)
-        tr8 = torch.empty(steps, n, dtype=torch.uint8, device=dev)
-        # final observations kept per step (rows written only where an episode ended), so that the
-        # time-out values are one masked launch over all T*N rows after the loop
-        fin = torch.empty(steps, n, d, device=dev)
+        S = out.storage if out is not None and out.storage is not None else None
+        if S is None or S["key"] != (steps, n, d, str(dev)):
+            S = _fused_storage(steps, n, d, dev)
+        obs_buf, fin, buf_a, buf_r, buf_v, buf_lp = S["obs"], S["fin"], S["act"], S["rew"], S["val"], S["logp"]
+        d8, tr8, trunc_val, last_val = S["d8"], S["tr8"], S["trunc_val"], S["last_val"]
+        obs_buf[0].copy_(o)
+        trunc_val.zero_()                 # read only where truncated; zero elsewhere, as the torch path
         # the policy of step t + 1 runs right behind the env-step of step t (fused: in its launch);
         # the last one gives V(obs_T), its sampled action and logp are not used
-        last_val = torch.empty(n, device=dev)
-        a_last, lp_last = torch.empty(n, 4, device=dev), torch.empty(n, device=dev)
         ac.step_into(obs_buf[0], buf_a[0], buf_v[0], buf_lp[0])
         for t in range(steps):
-            nxt = (buf_a[t + 1], buf_v[t + 1], buf_lp[t + 1]) if t + 1 < steps else (a_last, last_val, lp_last)
-            if fuse and envs.collect_step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], fin[t], ac, *nxt):
-                continue
-            fuse = False
+            nxt = (buf_a[t + 1], buf_v[t + 1], buf_lp[t + 1]) if t + 1 < steps else (S["a_last"], last_val, S["lp_last"])
+            if fuse and t == 0:
+                # the first step goes through every buffer check; the later slabs have the same
+                # shapes, so the loop then passes raw pointers (slab strides) to keep ahead of the GPU
+                if envs.collect_step_into(buf_a[0], obs_buf[1], buf_r[0], d8[0], tr8[0], fin[0], ac, *nxt):
+                    continue
+                fuse = False
+            elif fuse:
+                sa, so, sf = n * 16, n * d * 4, n * 4            # slab strides in bytes
+                a_p, o_p, r_p, v_p, l_p, f_p = (buf_a.data_ptr(), obs_buf.data_ptr(), buf_r.data_ptr(),
+                                                buf_v.data_ptr(), buf_lp.data_ptr(), fin.data_ptr())
+                dp, tp = d8.data_ptr(), tr8.data_ptr()
+                last = (S["a_last"].data_ptr(), last_val.data_ptr(), S["lp_last"].data_ptr())
+                for u in range(t, steps):
+                    nx = (a_p + (u + 1) * sa, v_p + (u + 1) * sf, l_p + (u + 1) * sf) if u + 1 < steps else last
+                    if not envs.collect_step_raw(a_p + u * sa, o_p + (u + 1) * so, r_p + u * sf, dp + u * n, tp + u * n,
+                                                 f_p + u * so, ac, *nx):
+                        raise RuntimeError("cf2_collect_step stopped being supported inside a collect")
+                envs._obs_latest = obs_buf[steps]    # what save_checkpoint saves after this collect
+                break
             envs.step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], final_obs_out=fin[t])
             ac.step_into(obs_buf[t + 1], *nxt)
         per = max(1, (2**31 - 1) // n)                      # row counts of the C ABI are 32-bit
@@ -403,9 +435,19 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
             ac.value_masked(fin[t0:t1].view(-1, d), tr8[t0:t1].view(-1), trunc_val[t0:t1].view(-1))
         envs.last_collect_fused = fuse         # every env-step ran as one cf2_collect_step launch
         o = obs_buf[steps]
-        adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True)
+        adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True,
+                                    out=(S["adv"], S["ret"], S["disc"]))
         buf_o, buf_d, buf_tr = obs_buf[:steps], d8.view(torch.bool), tr8.view(torch.bool)   # 0/1 bytes
-        return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val, disc)
+        return Rollout(buf_o, buf_a, buf_r, buf_v, buf_lp, buf_d, buf_tr, adv, ret, o, last_val, trunc_val, disc,
+                       storage=S)
+    buf_o = torch.empty(steps, n, d, device=dev)
+    buf_a = torch.empty(steps, n, 4, device=dev)
+    buf_r = torch.empty(steps, n, device=dev)
+    buf_v = torch.empty(steps, n, device=dev)
+    buf_lp = torch.empty(steps, n, device=dev)
+    buf_d = torch.empty(steps, n, dtype=torch.bool, device=dev)
+    buf_tr = torch.empty(steps, n, dtype=torch.bool, device=dev)
+    trunc_val = torch.zeros(steps, n, device=dev)
     for t in range(steps):
         a, v, lp = ac.step(o, generator=generator)
         buf_o[t] = o

@@ -218,6 +218,22 @@ class BatchedCrazyflieEnv:
         self._obs_latest = obs_out
         return True
 
+    def collect_step_raw(self, act: int, obs: int, rew: int, done: int, trunc: int, final_obs: int, policy,
+                         act_out: int, val_out: int, logp_out: int) -> bool:
+        """collect_step_into on raw device pointers (rollout.collect's loop after its first step,
+        whose slabs collect_step_into has checked; the C ABI still rejects null or misaligned
+        pointers): keeps the host's per-step cost well under the kernel's."""
+        st = self.lib.cf2_collect_step(self._ctx, act, obs, rew, done, trunc, final_obs, policy.w_ptr, self.obs_dim,
+                                       policy.prec, policy.seed, policy.counter & 0xFFFFFFFF, 0, act_out, val_out,
+                                       logp_out, self.stream)
+        if st == _native.CF2_ERR_UNSUPPORTED:
+            return False
+        _native.check(st, "cf2_collect_step")
+        policy.counter += 1
+        self._state_version += 1
+        self._obs_latest = None          # rollout.collect points it at the slab afterwards
+        return True
+
     def rollout(self, actions: torch.Tensor, obs_out: torch.Tensor | None = None, rew_out=None, done_out=None,
                 trunc_out=None, cost_out=None, level_out=None, final_obs_out=None):
         """K env-steps in one fused launch (cf2_rollout): actions [K, N, 4]; returns (obs [K, N, D],

@@ -66,6 +66,11 @@ def _run(env_id, n, kw, setup=None, T=24):
     ra2 = collect(ea, pa, 5, obs=ra.last_obs, fuse=True)
     rb2 = collect(eb, pb, 5, obs=rb.last_obs, fuse=False)
     _check_equal(ra2, rb2)
+    # a collect that re-uses an earlier rollout's storage (out=) gives the same results
+    ra3 = collect(ea, pa, 5, obs=ra2.last_obs, fuse=True, out=ra2)
+    rb3 = collect(eb, pb, 5, obs=rb2.last_obs, fuse=False)
+    assert ra3.storage is ra2.storage
+    _check_equal(ra3, rb3)
     ea.close()
     eb.close()
     return launched
@@ -93,7 +98,7 @@ def test_fused_collect_hj_boltzmann(gpu):
 ])
 def test_unfused_configs_fall_back(gpu, env_id, n, kw):
     launched = _run(env_id, n, kw, T=8)
-    assert launched == [False, False], "an unsupported config launches nothing and is probed once per collect"
+    assert launched == [False] * 3, "an unsupported config launches nothing and is probed once per collect"
 
 
 def test_collect_step_rejects_bad_args(gpu):

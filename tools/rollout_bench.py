@@ -43,7 +43,8 @@ def main():
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        ro = collect(envs, ac, args.steps, obs=ro.last_obs, generator=g, fuse=not args.no_fuse)
+        ro = collect(envs, ac, args.steps, obs=ro.last_obs, generator=g, fuse=not args.no_fuse,
+                     out=ro if not args.torch_policy else None)     # storage re-used, as every epoch of a training loop
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
     # split: policy forward alone vs env step alone on the same sizes
