@@ -162,10 +162,11 @@ def load_valu_issue(workload_key: str):
         key = step_kernel_key()
         for e in d.get("entries", []):
             if e.get("workload") == workload_key and e.get("kernel_key") == key:
-                return e["step_kernel"]["valu_issue_frac"], e["rollout_kernel"]["valu_issue_frac"]
+                return (e["step_kernel"]["valu_issue_frac"], e["rollout_kernel"]["valu_issue_frac"],
+                        (e.get("collect_kernel") or {}).get("valu_issue_frac"))
     except (OSError, ValueError, ImportError, KeyError):
         pass
-    return None, None
+    return None, None, None
 
 
 def bytes_per_env_step(env) -> int:
@@ -466,6 +467,8 @@ def main(argv=None):
         collect_line = {"value": n / (cus * 1e-6), "unit": "env-steps/s", "us_per_env_step": cus,
                         "steps_per_collect": T, "policy": "MLP actor-critic 34-50-50-4 / 34-64-64-1, bf16x3",
                         "one_launch_per_env_step": bool(cenv.last_collect_fused),
+                        # fraction of the fused kernel's SIMD cycles issuing VALU (PMC, tools/pmc_valu.sh)
+                        "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[2],
                         "includes": "env-step, policy forward + sampling, rollout storage (re-used across collects), GAE, "
                                     "time-out values"}
         cenv.close()

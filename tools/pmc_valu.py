@@ -21,9 +21,9 @@ SIMDS = 1024
 NAMES = ["SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
 
 
-def per_dispatch(kern):
+def per_dispatch(kern, sub="pmc"):
     per = {}
-    for f in glob.glob(os.path.join(out, "pmc", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(out, sub, "**", "*counter_collection.csv"), recursive=True):
         for i, row in enumerate(csv.DictReader(open(f))):
             if kern in row.get("Kernel_Name", "") and row["Counter_Name"] in NAMES:
                 key = int(row.get("Dispatch_Id") or i)
@@ -32,10 +32,10 @@ def per_dispatch(kern):
     return [per[k] for k in sorted(per)]
 
 
-def durations(kern):
+def durations(kern, sub="pmc"):
     """Profiled dispatch durations (ns) of kern from the kernel trace of the same pass."""
     d = []
-    for f in glob.glob(os.path.join(out, "pmc", "**", "*kernel_trace.csv"), recursive=True):
+    for f in glob.glob(os.path.join(out, sub, "**", "*kernel_trace.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if kern in row.get("Kernel_Name", ""):
                 d.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
@@ -65,6 +65,9 @@ roll = per_dispatch("rollout_kernel")
 res = {"workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}", "kernel_key": key,
        "step_kernel": summarize(step, "step_kernel", 1, durations("step_kernel")[-30:]),
        "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations("rollout_kernel")),
+       "collect_kernel": (summarize(per_dispatch("collect_kernel", "pmc_collect"), "collect_kernel (env-step + policy)",
+                                    1, durations("collect_kernel", "pmc_collect"))
+                          if per_dispatch("collect_kernel", "pmc_collect") else None),
        "note": __doc__.split("\n\n")[1]}
 prof = os.path.join(ROOT, "profiles", "valu_issue.json")
 try:
