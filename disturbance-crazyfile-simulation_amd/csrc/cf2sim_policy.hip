@@ -158,7 +158,17 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
     policy_lane_init<D, PREC>(s_w + P::O_BIAS, g, C);
     ObsRegs<D, PREC> X;
     if (MODE == 0 && wave < nchunks) load_obs<D, PREC>(obs, n, wave * CHUNK, l, X);
-    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+    // sampling noise, one Philox block per row: at every 4th chunk lane group g draws the rows of
+    // the wave's chunk k + g (lane 16 g + r), and chunk k + j takes its rows' normals from lane
+    // group j (ds_bpermute), instead of all 64 lanes drawing every chunk's 16 rows
+    constexpr bool ROWNOISE = MODE == 0 && RT == 1;
+    float ep[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t kk = 0;
+    for (uint32_t c = wave; c < nchunks; c += nwaves, ++kk) {
+        if (ROWNOISE && sample && (kk & 3u) == 0u) {
+            const uint32_t cg = c + (uint32_t)g * nwaves;
+            if (cg < nchunks) policy_noise(key0, key1, counter, row_offset + cg * CHUNK + (uint32_t)r16, ep);
+        }
         const uint32_t r0 = c * CHUNK;
         if (MODE == 1) {
             // marked rows are sparse: a chunk without one is skipped before its observations load
@@ -178,11 +188,21 @@ __global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const floa
         if (MODE == 0 && c + nwaves < nchunks) load_obs<D, PREC>(obs, n, (c + nwaves) * CHUNK, l, X);
         f4v o[RT];
         policy_layers<D, PREC, MODE>(sw, sw + P::O_BIAS, sw + P::O_L3, l, Xc, o);
+        if constexpr (ROWNOISE) {
+            float e[4];
+            const int src = (int)((((kk & 3u) << 4) | (uint32_t)r16) << 2);
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            const uint32_t row = r0 + 16 * rt + r16;
-            if (row >= n) continue;
-            policy_emit<D, PREC, MODE>(o[rt], row, g, C, key0, key1, counter, row_offset, sample, act, val, logp, mask);
+            for (int k = 0; k < 4; ++k) e[k] = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(ep[k])));
+            const uint32_t row = r0 + (uint32_t)r16;
+            if (row < n) policy_emit_eps<D, PREC, MODE>(o[0], row, g, C, e, sample, act, val, logp, mask);
+        } else {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const uint32_t row = r0 + 16 * rt + r16;
+                if (row >= n) continue;
+                policy_emit<D, PREC, MODE>(o[rt], row, g, C, key0, key1, counter, row_offset, sample, act, val, logp,
+                                           mask);
+            }
         }
     }
 }
