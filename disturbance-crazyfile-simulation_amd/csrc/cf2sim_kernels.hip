@@ -2093,29 +2093,37 @@ __device__ __forceinline__ void finish_outputs(const KParams& P, const StepIO& i
 enum { SEED_SMALL = 10 };   // per finished env, wave 0 -> waves 1-3: final body rates, gyro bias, OU state
 enum { C2_WORDS = 9 };      // per env, wave 3 -> wave 2: the second reset sensor call's gyro normals
 
-template <bool NOISE, bool DR, int PHYS, int SPEC>
-__global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO io) {
-    const KParams P = shape_view<SPEC>(P0);
-    constexpr int OL = NOISE ? 13 : 17;
-    constexpr int OD = 2 * (OL + 4);
-    __shared__ __align__(16) float s_obs[64 * OD];         // the block's obs rows, global layout
-    __shared__ float s_seed[SEED_SMALL * 64];              // [word][env]
-    __shared__ float s_c2[C2_WORDS * 64];                  // [word][env]
-    __shared__ __align__(16) float s_rrow[64 * OD];        // speculative reset observation rows
-    __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
-    __shared__ double s_hjgrid[6 * HJ_PTS];
+// The small-N kernel's LDS arrays (step_kernel_small declares them; collect_kernel_small carves
+// them out of a buffer the policy fragments re-use afterwards)
+template <bool NOISE, int SPEC>
+struct SmallLds {
+    static constexpr int OL = NOISE ? 13 : 17, OD = 2 * (OL + 4);
     // reference-default shape with sensor noise: the helpers also draw the env-step's randomness
     // after its first sub-step (HD_* layout), handed over at an LDS barrier before sub-step 1
-    constexpr bool HD = SPEC == 1 && NOISE;
-    __shared__ float s_draw[HD ? HD_WORDS * 64 : 1];
+    static constexpr bool HD = SPEC == 1 && NOISE;
 #ifdef CF2_SMALL_OFFLOAD
-    constexpr bool FIN = HD;         // A/B: reward / cost / outputs finished by helper wave 3
+    static constexpr bool FIN = HD;  // A/B: reward / cost / outputs finished by helper wave 3
 #else
     // measured slower (32 768 envs 10.3 -> 11.0 us): wave 3's post-barrier outputs lengthened
     // the reset tail more than they shortened the env wave's epilogue
-    constexpr bool FIN = false;
+    static constexpr bool FIN = false;
 #endif
-    __shared__ float s_fin[FIN ? FIN_WORDS * 64 : 1];
+    // word offsets in a carved buffer (doubles 8-B aligned, rows 16-B aligned)
+    static constexpr uint32_t O_OBS = 0, O_RROW = 64 * OD, O_SEED = 128 * OD, O_C2 = O_SEED + SEED_SMALL * 64,
+                              O_DRAW = O_C2 + C2_WORDS * 64, O_FIN = O_DRAW + (HD ? HD_WORDS * 64 : 1),
+                              O_MASK = O_FIN + (FIN ? FIN_WORDS * 64 : 1), O_HJ = (O_MASK + 2 + 1) & ~1u,
+                              WORDS = O_HJ + 2 * 6 * HJ_PTS;
+};
+
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& io, float* s_obs, float* s_seed,
+                                               float* s_c2, float* s_rrow, uint32_t* s_mask, double* s_hjgrid,
+                                               float* s_draw, float* s_fin) {
+    const KParams P = shape_view<SPEC>(P0);
+    using SL = SmallLds<NOISE, SPEC>;
+    constexpr int OL = SL::OL;
+    constexpr int OD = SL::OD;
+    constexpr bool HD = SL::HD, FIN = SL::FIN;
 #ifdef CF2_TIMING
     if (uint64_t* r = timing_row()) {
         if ((threadIdx.x & 63) == 0) {
@@ -2321,6 +2329,87 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     if (uint64_t* r = timing_row())
         if ((threadIdx.x & 63) == 0) r[2] = __builtin_amdgcn_s_memrealtime();
 #endif
+    return mask;
+}
+
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO io) {
+    using SL = SmallLds<NOISE, SPEC>;
+    __shared__ __align__(16) float s_obs[64 * SL::OD];     // the block's obs rows, global layout
+    __shared__ float s_seed[SEED_SMALL * 64];              // [word][env]
+    __shared__ float s_c2[C2_WORDS * 64];                  // [word][env]
+    __shared__ __align__(16) float s_rrow[64 * SL::OD];    // speculative reset observation rows
+    __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    __shared__ float s_draw[SL::HD ? HD_WORDS * 64 : 1];
+    __shared__ float s_fin[SL::FIN ? FIN_WORDS * 64 : 1];
+    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw, s_fin);
+}
+
+// The fused collect step at small N (N <= 32 768: the 8-GPU node shard, C2): step_kernel_small's
+// env-step (64 envs per block, helper waves), then the policy forward of the block's 64 new
+// observations, one 16-row tile per wave.  Alone, the policy kernel at these sizes is a fixed
+// cost (weights staging + one tile's dependent chain + a launch: ~15-18 us per step at 4096-32 768
+// rows, more than the env-step); here it follows the env-step inside the block.  The final
+// observation rows are read from LDS (s_obs, or s_rrow where the env reset), then the block's LDS
+// takes the fragments (all but layer 3, as collect_kernel).  Outputs bit-identical to cf2_step +
+// cf2_policy_forward.
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(256, 2) collect_kernel_small(KParams P0, StepIO io, PolicyIO pio) {
+    static_assert(NOISE, "the fused collect kernel is built for the 34-wide observation");
+    using SL = SmallLds<NOISE, SPEC>;
+    constexpr int OD = SL::OD;
+    using PK = Packed<OD, CF2_POLICY_BF16X3>;
+    constexpr uint32_t L3N = PK::O_BIAS - PK::O_L3, POL_WORDS = PK::TOTAL - L3N;
+    constexpr uint32_t LDS_WORDS = POL_WORDS > SL::WORDS ? POL_WORDS : SL::WORDS;
+    __shared__ __align__(16) float s_mem[LDS_WORDS];
+    const uint64_t mask = small_body<NOISE, DR, PHYS, SPEC>(
+        P0, io, s_mem + SL::O_OBS, s_mem + SL::O_SEED, s_mem + SL::O_C2, s_mem + SL::O_RROW,
+        reinterpret_cast<uint32_t*>(s_mem + SL::O_MASK), reinterpret_cast<double*>(s_mem + SL::O_HJ),
+        s_mem + SL::O_DRAW, s_mem + SL::O_FIN);
+    // ---- policy phase: wave w takes rows 16 w .. 16 w + 15 of the block (lane l: row 16 w + (l & 15),
+    // inputs 8 g .. 8 g + 7 and 32 + g)
+    const uint32_t tid = threadIdx.x, l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
+    const int g = (int)(l >> 4);
+    const uint32_t br = 16u * wv + r16, base = blockIdx.x * 64u, row = base + br;
+    ObsRegs<OD, CF2_POLICY_BF16X3> X;
+    {
+        const float* src = (((mask >> br) & 1ull) ? s_mem + SL::O_RROW : s_mem + SL::O_OBS) + br * OD;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float2 v = *reinterpret_cast<const float2*>(src + 8 * g + 2 * q);
+            X.x8[0][0][2 * q] = v.x;
+            X.x8[0][0][2 * q + 1] = v.y;
+        }
+        X.x1[0][0] = src[__builtin_elementwise_min(32 + g, OD - 1)];
+    }
+    __syncthreads();         // every wave holds its rows: the LDS takes the fragments
+    constexpr uint32_t NQ4 = POL_WORDS / 4, NQ = (NQ4 + 255u) / 256u;
+    float4 stg[NQ];
+    {
+        const float4* src = reinterpret_cast<const float4*>(pio.w);
+#pragma unroll
+        for (uint32_t q = 0; q < NQ; ++q) {
+            const uint32_t k = __builtin_elementwise_min(tid + q * 256u, NQ4 - 1u);
+            stg[q] = src[k < PK::O_L3 / 4 ? k : k + L3N / 4];
+        }
+    }
+    float ep[4];             // this lane's row's sampling noise, drawn while the loads are in flight
+    policy_noise(pio.key0, pio.key1, pio.counter, pio.row_offset + row, ep);
+    {
+        float4* dst = reinterpret_cast<float4*>(s_mem);
+#pragma unroll
+        for (uint32_t q = 0; q < NQ; ++q)
+            if (tid + q * 256u < NQ4) dst[tid + q * 256u] = stg[q];
+    }
+    __syncthreads();
+    PolicyLane<OD, CF2_POLICY_BF16X3> CL;
+    policy_lane_init<OD, CF2_POLICY_BF16X3>(s_mem + PK::O_L3, g, CL);
+    policy_standardize<OD, CF2_POLICY_BF16X3>(s_mem + PK::O_L3, g, CL, X);
+    f4v o[1];
+    policy_layers<OD, CF2_POLICY_BF16X3, 0>(s_mem, s_mem + PK::O_L3, pio.w + PK::O_L3, (int)l, X, o);
+    if (row < P0.N)
+        policy_emit_eps<OD, CF2_POLICY_BF16X3, 0>(o[0], row, g, CL, ep, 1, pio.act, pio.val, pio.logp, nullptr);
 }
 
 // One physics sub-step of every env: the physics plugin's step_forward on its own (PyBulletPhysics
@@ -2893,7 +2982,11 @@ static hipError_t launch_collect_t(const KParams& P, const StepIO& io, const Pol
     if constexpr (!NOISE || SPEC != 1 || PHYS != PHYS_BULLET_T) {
         return hipErrorNotSupported;
     } else {
-        if (P.N <= 32768u) return hipErrorNotSupported;     // small N: 64-env blocks (step_kernel_small)
+        if (P.N <= 32768u) {     // small N: 64-env blocks with helper waves (as launch_step_t)
+            hipLaunchKernelGGL((collect_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s,
+                               P, io, pio);
+            return hipGetLastError();
+        }
         static int round_blocks = -1;
         if (round_blocks < 0) {
             int dev = 0, cus = 0, per_cu = 0;

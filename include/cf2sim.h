@@ -299,7 +299,7 @@ int  cf2_value_forward_masked(const float* packed_dev, uint32_t n, uint32_t obs_
  * pair env.step + ac.step of IWPGAlgorithm.roll_out (phoenix_drone_simulation/algs/iwpg/iwpg.py:
  * 377-380; ActorCritic.step algs/core.py:371-395).  Every output is bit-identical to the two
  * calls.  Fused only where built (precision CF2_POLICY_BF16X3, obs_dim 34 = sensor noise on, the
- * default Bullet env-step shape, one drone per formation, N > 32 768); elsewhere it returns
+ * default Bullet env-step shape, one drone per formation; any N); elsewhere it returns
  * CF2_ERR_UNSUPPORTED and launches nothing, and the caller makes the two calls. */
 int  cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
                       uint8_t* trunc_dev, float* final_obs_dev, const float* packed_dev, uint32_t obs_dim,

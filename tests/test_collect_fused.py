@@ -13,6 +13,10 @@ CASES = [
     ("DroneHoverBulletFreeEnvWithGust-v0", 40000, {}),                                    # bench workload, partial block
     ("DroneHoverBulletFreeEnvWithoutAdversary-v0", 33024, dict(max_episode_steps=7, domain_randomization=0)),
     ("DroneHoverBulletFreeEnvWithRandomAdversary-v0", 65536, dict(max_episode_steps=11)),
+    # small N (collect_kernel_small: 64 envs per block with helper waves)
+    ("DroneHoverBulletFreeEnvWithGust-v0", 32768, {}),                                    # the 8-GPU node shard
+    ("DroneHoverBulletFreeEnvWithConstWind-v0", 4096, dict(max_episode_steps=9)),         # C2
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", 5000, dict(domain_randomization=0)),   # partial last block
 ]
 
 
@@ -92,8 +96,8 @@ def test_fused_collect_hj_boltzmann(gpu):
 
 
 @pytest.mark.parametrize("env_id,n,kw", [
-    ("DroneHoverBulletFreeEnvWithGust-v0", 4096, {}),                         # small N: no fused instance
     ("DroneHoverBulletFreeEnvWithGust-v0", 40000, dict(observation_noise=0)),  # 42-wide obs
+    ("DroneHoverBulletFreeEnvWithGust-v0", 4096, dict(observation_noise=0)),   # 42-wide obs, small N
     ("DroneHoverSimpleEnv-v0", 40000, {}),
 ])
 def test_unfused_configs_fall_back(gpu, env_id, n, kw):
