@@ -45,6 +45,22 @@ def _hipcc() -> str:
 
 BUILD_DIR = os.path.join(PKG_DIR, "_build")
 
+# -D defines the native sources know.  CF2_TIMING adds the per-wave phase stamps tools/timeline.py
+# reads (cf2_debug_timing_buffer); it changes no result.  Any other CF2_ define is a typo or a
+# removed A/B knob: it would compile silently into a library that differs from the tested one, so
+# it is rejected.
+KNOWN_DEFINES = frozenset({"CF2_TIMING"})
+
+
+def check_defines(flags) -> None:
+    """ValueError for a -DCF2_* flag that is not in KNOWN_DEFINES."""
+    for f in flags:
+        if not f.startswith("-D"):
+            continue
+        name = f[2:].split("=", 1)[0]
+        if name.startswith("CF2_") and name not in KNOWN_DEFINES:
+            raise ValueError(f"unknown define {name}: the native sources only know {sorted(KNOWN_DEFINES)}")
+
 
 def _digest(*parts: bytes) -> str:
     h = hashlib.sha256()
@@ -63,16 +79,16 @@ def _headers_blob() -> bytes:
     return b"".join(_read(os.path.join(SRC_DIR, h)) for h in HEADERS) + _read(os.path.join(INC_DIR, "cf2sim.h"))
 
 
-def _compile_flags(src: str | None = None):
-    return [f for f in FLAGS if f != "-shared"] + SOURCE_FLAGS.get(src, []) + ["-c"]
+def _compile_flags(src: str | None = None, extra=()):
+    return [f for f in FLAGS if f != "-shared"] + SOURCE_FLAGS.get(src, []) + list(extra) + ["-c"]
 
 
-def _obj_key(src: str) -> str:
-    return _digest(" ".join(_compile_flags(src)).encode(), _read(os.path.join(SRC_DIR, src)), _headers_blob())
+def _obj_key(src: str, extra=()) -> str:
+    return _digest(" ".join(_compile_flags(src, extra)).encode(), _read(os.path.join(SRC_DIR, src)), _headers_blob())
 
 
-def _lib_key() -> str:
-    return _digest(*[_obj_key(s).encode() for s in SOURCES])
+def _lib_key(extra=()) -> str:
+    return _digest(*[_obj_key(s, extra).encode() for s in SOURCES])
 
 
 def _stamp(path: str) -> str | None:
@@ -89,19 +105,28 @@ def up_to_date() -> bool:
     return os.path.exists(LIB) and _stamp(LIB) == _lib_key()
 
 
-def build_native(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return LIB
-    os.makedirs(BUILD_DIR, exist_ok=True)
+def build_native(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
+    """Build libcf2sim.so in-tree (or, with extra_flags, e.g. ['-DCF2_TIMING'], a variant at `out`,
+    from objects in their own build directory, leaving the in-tree library untouched)."""
+    extra = list(extra_flags)
+    check_defines(extra)
+    if extra and out is None:
+        raise ValueError("a build with extra flags needs an output path (out=): the in-tree library is the tested one")
+    lib = os.path.abspath(out) if out else LIB
+    bdir = BUILD_DIR if not extra else BUILD_DIR + "_" + _digest(" ".join(extra).encode())[:12]
+    if not force and os.path.exists(lib) and _stamp(lib) == _lib_key(extra):
+        return lib
+    os.makedirs(bdir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     procs = []
     objs = []
     for src in SOURCES:      # one object per source, compiled in parallel, skipped when unchanged
-        obj = os.path.join(BUILD_DIR, os.path.splitext(src)[0] + ".o")
+        obj = os.path.join(bdir, os.path.splitext(src)[0] + ".o")
         objs.append(obj)
-        key = _obj_key(src)
+        key = _obj_key(src, extra)
         if not force and os.path.exists(obj) and _stamp(obj) == key:
             continue
-        cmd = [_hipcc(), *_compile_flags(src), "-I", INC_DIR, "-o", obj + ".tmp", os.path.join(SRC_DIR, src)]
+        cmd = [_hipcc(), *_compile_flags(src, extra), "-I", INC_DIR, "-o", obj + ".tmp", os.path.join(SRC_DIR, src)]
         if verbose:
             print(" ".join(cmd))
         procs.append((subprocess.Popen(cmd), obj, key))
@@ -115,11 +140,11 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
             f.write(key)
     if failed:
         raise subprocess.CalledProcessError(1, "hipcc")
-    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    with open(LIB + ".stamp", "w") as f:
-        f.write(_lib_key())
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    with open(lib + ".stamp", "w") as f:
+        f.write(_lib_key(extra))
+    return lib

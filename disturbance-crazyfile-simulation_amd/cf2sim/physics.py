@@ -80,22 +80,22 @@ class BatchedDrone:
 
     def _fields(self):
         sf, _ = self.env.snapshot()          # one conversion per state change, shared by the properties
-        return sf, self.env.layout
+        return sf, self.env.layout           # (each property returns its own copy: .clone())
 
     @property
     def xyz(self):
         sf, L = self._fields()
-        return sf[L.f_pos:L.f_pos + 3].T.contiguous()
+        return sf[L.f_pos:L.f_pos + 3].T.clone(memory_format=torch.contiguous_format)
 
     @property
     def quaternion(self):
         sf, L = self._fields()
-        return sf[L.f_quat:L.f_quat + 4].T.contiguous()
+        return sf[L.f_quat:L.f_quat + 4].T.clone(memory_format=torch.contiguous_format)
 
     @property
     def xyz_dot(self):
         sf, L = self._fields()
-        return sf[L.f_vel:L.f_vel + 3].T.contiguous()
+        return sf[L.f_vel:L.f_vel + 3].T.clone(memory_format=torch.contiguous_format)
 
     @property
     def x(self):
@@ -109,7 +109,7 @@ class BatchedDrone:
         sf, L = self._fields()
         w = sf[L.f_omega:L.f_omega + 3].T
         if self.physics_type == PHYS_SIMPLE:
-            return w.contiguous()
+            return w.clone(memory_format=torch.contiguous_format)
         return torch.einsum("nji,nj->ni", _rotmat(sf[L.f_quat:L.f_quat + 4].T), w)
 
     @property
@@ -118,7 +118,7 @@ class BatchedDrone:
         SimplePhysics agents)."""
         sf, L = self._fields()
         if self.physics_type == PHYS_SIMPLE:
-            return sf[L.f_rpy:L.f_rpy + 3].T.contiguous()
+            return sf[L.f_rpy:L.f_rpy + 3].T.clone(memory_format=torch.contiguous_format)
         return _euler_from_quat(sf[L.f_quat:L.f_quat + 4].T)
 
     def close(self):

@@ -7,8 +7,13 @@ obs, r, done, info = env.step(a)`` (tests/test_envs.py:96-123, algs/iwpg/iwpg.py
 
 * ``reset() -> np.ndarray[obs_dim]`` float64 (the reference builds obs with numpy float64 ops)
 * ``step(a) -> (obs, float r, bool done, dict info)``, ``info`` = compute_info() keys
-  (``cost``, ``disturbance_level``) plus ``TimeLimit.truncated`` when gym's TimeLimit(500) ends
-  the episode (gym 0.19 TimeLimit semantics: done = terminal or truncated; no auto-reset)
+  (``cost``, ``disturbance_level``, and ``xyz_limit`` / ``rpy`` / ``xzy_dot`` / ``rpy_dot`` for the
+  constraints the step violates, envs/hover_free.py:138-166) plus ``TimeLimit.truncated`` when gym's
+  TimeLimit(500) ends the episode (gym 0.19 TimeLimit semantics: done = terminal or truncated; no
+  auto-reset)
+* HJ-adversary ids read value tables: ``make(id, value_tables=dir)`` loads the reference's
+  ``fastrack_{level}_15x15.npy`` files (distur_gener.py:155; a directory, a dict by level or an
+  array, see vec_env.load_value_tables); ``env.bind_hj_tables(...)`` rebinds them
 * ``observation_space`` Box(-1000, 1000, (34,), float32) / (42,) without noise, ``action_space``
   Box(-1, 1, (4,), float32) (envs/base.py:139-148); ``metadata`` as envs/base.py:24
 * ``seed(s)`` re-seeds the Philox stream (the reference re-seeds numpy's global RNG)
@@ -53,9 +58,11 @@ class CrazyflieEnv:
     metadata = {"render.modes": ["human", "rgb_array"]}   # envs/base.py:24
     reward_range = (-float("inf"), float("inf"))
 
-    def __init__(self, env_id: str, seed: int = 0, device=None, physics: str | None = None, **env_kwargs):
+    def __init__(self, env_id: str, seed: int = 0, device=None, physics: str | None = None, value_tables=None,
+                 **env_kwargs):
         from .vec_env import BatchedCrazyflieEnv
         self.spec = spec_for_id(env_id)
+        self._value_tables = value_tables
         self.env_id = env_id
         self._kwargs = dict(env_kwargs)
         self._device = device
@@ -73,6 +80,8 @@ class CrazyflieEnv:
                               auto_reset=False, max_episode_steps=0, _spec=spec, **self._kwargs)
         self.observation_space = self._env.observation_space
         self.action_space = self._env.action_space
+        if self._value_tables is not None:
+            self._env.bind_value_tables(self._value_tables)
         self._t = 0
         self._needs_reset = True
         self._last_action = np.zeros(4, np.float32)
@@ -82,6 +91,20 @@ class CrazyflieEnv:
         self.penalty_log = self.penalty_rpy_log = self.penalty_crash_log = 0.0
         self.penalty_z_log = self.penalty_rpy_dot_log = self.penalty_velocity_log = 0.0
 
+    def bind_hj_tables(self, value_tables, table_of_level=None):
+        """Bind the HJ value tables of an adversary env: a directory with the reference's
+        ``fastrack_{level}_15x15.npy`` files (or the reference's repository root), a dict
+        {level: table}, or an array of tables (``table_of_level`` maps each level to a row).  Kept
+        across ``seed()``."""
+        import torch
+        if table_of_level is not None:
+            self._env.bind_hj_tables(torch.as_tensor(value_tables), table_of_level)
+        else:
+            self._env.bind_value_tables(value_tables)
+        self._value_tables = value_tables if table_of_level is None else None
+        if table_of_level is not None:
+            self._tables_explicit = (value_tables, table_of_level)
+
     @property
     def disturbance_level(self) -> float:        # read by iwpg.py:408
         return float(self._env.level[0].item())
@@ -90,6 +113,9 @@ class CrazyflieEnv:
         self._seed = int(seed) if seed is not None else 0
         self._env.close()
         self._make()
+        if getattr(self, "_tables_explicit", None) is not None and self._value_tables is None:
+            import torch
+            self._env.bind_hj_tables(torch.as_tensor(self._tables_explicit[0]), self._tables_explicit[1])
         return [self._seed]
 
     def _state_fields(self):
@@ -131,8 +157,9 @@ class CrazyflieEnv:
         od = self._env.obs_dim
         r, terminal, cost, level = float(h[od]), bool(h[od + 1] != 0), float(h[od + 2]), float(h[od + 3])
         self._t += 1
-        self._log_penalties(act, terminal, h[od + 4:])
-        info_out = {"cost": cost, "disturbance_level": level}
+        rpy, rpy_dot = self._log_penalties(act, terminal, h[od + 4:])
+        info_out = self._constraint_info(h[od + 4:], rpy, act)
+        info_out.update({"cost": cost, "disturbance_level": level})
         truncated = self._t >= self.max_episode_steps > 0
         if truncated and not terminal:
             info_out["TimeLimit.truncated"] = True
@@ -170,6 +197,38 @@ class CrazyflieEnv:
                             + pen_action + self.penalty_crash_log)
         self.penalty_z_log = c.penalty_z * abs(p[2] - tgt_pos[2])
         self._last_action = action
+        return rpy, rpy_dot
+
+    def _constraint_info(self, st, rpy, action) -> dict:
+        """The conditional keys of compute_info (envs/hover_free.py:138-166, envs/hover.py:116-144)
+        from the state after the step.  state = get_state() = [xyz, quat, xyz_dot, rpy_dot (body),
+        last_action] (agents.py:339-348), and the reference indexes state[10:13] (the body rates)
+        as 'xzy_dot' and state[13:16] (the first three last-action entries) as 'rpy_dot': reproduced
+        as written.  last_action is the action just applied (apply_action, agents.py:263).  The
+        kernel's cost flag (info['cost']) uses the same conditions."""
+        c = self._env.cfg
+        p, q, v, w = st[0:3], st[3:7], st[7:10], st[10:13]
+        la = np.asarray(action, dtype=np.float64)
+        if int(c.physics) == PHYS_SIMPLE:
+            wb = w
+        else:
+            x, y, z, qw = q
+            s2 = 2.0 / float(q @ q)
+            R = np.array([[1 - s2 * (y * y + z * z), s2 * (x * y - qw * z), s2 * (x * z + qw * y)],
+                          [s2 * (x * y + qw * z), 1 - s2 * (x * x + z * z), s2 * (y * z - qw * x)],
+                          [s2 * (x * z - qw * y), s2 * (y * z + qw * x), 1 - s2 * (x * x + y * y)]])
+            wb = R.T @ w
+        state = np.concatenate([p, q, v, wb, la])
+        info = {}
+        if abs(p[0]) > c.cost_xy_lim or abs(p[1]) > c.cost_xy_lim or p[2] > c.cost_z_lim:
+            info["xyz_limit"] = state[:3]
+        if (np.abs(np.asarray(rpy)[:2]) > c.cost_rp_lim).any():
+            info["rpy"] = np.asarray(rpy)
+        if (np.abs(state[10:13]) > c.cost_vel_lim).any():
+            info["xzy_dot"] = state[10:13]
+        if (np.abs(state[13:16]) > c.cost_rate_lim).any():
+            info["rpy_dot"] = state[13:16] * 180 / np.pi
+        return info
 
     def render(self, mode="human"):
         raise NotImplementedError("rendering is outside the accelerated path (DESIGN.md 'Out of scope')")

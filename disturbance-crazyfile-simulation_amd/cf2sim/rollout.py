@@ -262,11 +262,15 @@ class FusedActorCritic:
         return act, val, logp
 
     @torch.no_grad()
-    def step_into(self, obs: torch.Tensor, act: torch.Tensor, val: torch.Tensor, logp: torch.Tensor):
+    def step_into(self, obs: torch.Tensor, act: torch.Tensor, val: torch.Tensor, logp: torch.Tensor,
+                  row_offset: int = 0):
+        """step() into caller buffers.  row_offset: global index of row 0 (the sampling noise of row
+        r is keyed by row_offset + r; collect() passes the env shard's env_id_offset, so a rank's
+        envs draw the noise they would draw in one process holding every env)."""
         from . import _native
         _native.check(self.lib.cf2_policy_forward(
             self.w.data_ptr(), obs.shape[0], self.obs_dim, self.prec, obs.data_ptr(), self.seed,
-            self.counter & 0xFFFFFFFF, 0, 1,
+            self.counter & 0xFFFFFFFF, int(row_offset), 1,
             act.data_ptr(), val.data_ptr(), logp.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream),
             "cf2_policy_forward")
         self.counter += 1
@@ -405,7 +409,8 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         trunc_val.zero_()                 # read only where truncated; zero elsewhere, as the torch path
         # the policy of step t + 1 runs right behind the env-step of step t (fused: in its launch);
         # the last one gives V(obs_T), its sampled action and logp are not used
-        ac.step_into(obs_buf[0], buf_a[0], buf_v[0], buf_lp[0])
+        roff = int(envs.cfg.env_id_offset)    # sampling noise keyed by the global env id
+        ac.step_into(obs_buf[0], buf_a[0], buf_v[0], buf_lp[0], row_offset=roff)
         for t in range(steps):
             nxt = (buf_a[t + 1], buf_v[t + 1], buf_lp[t + 1]) if t + 1 < steps else (S["a_last"], last_val, S["lp_last"])
             if fuse and t == 0:
@@ -428,7 +433,7 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
                 envs._obs_latest = obs_buf[steps]    # what save_checkpoint saves after this collect
                 break
             envs.step_into(buf_a[t], obs_buf[t + 1], buf_r[t], d8[t], tr8[t], final_obs_out=fin[t])
-            ac.step_into(obs_buf[t + 1], *nxt)
+            ac.step_into(obs_buf[t + 1], *nxt, row_offset=roff)
         per = max(1, (2**31 - 1) // n)                      # row counts of the C ABI are 32-bit
         for t0 in range(0, steps, per):                      # V(final obs) of the time-outs only
             t1 = min(steps, t0 + per)

@@ -22,6 +22,64 @@ from .config import CF2Config, DSTB_EXTERNAL, DSTB_HJ, build_config, obs_dim, sp
 from .spaces import make_box
 
 
+# where the reference keeps its HJ value tables, relative to its repository root (distur_gener.py:155)
+REFERENCE_TABLE_DIR = "phoenix_drone_simulation/adversarial_generation/FasTrack_data"
+
+
+def value_table_name(level: float) -> str:
+    """The reference's file name of the value table for a disturbance level: distur_gener.py:155
+    formats the level as Python prints it (0.0, 0.1, ..., 1.5, ...; Boltzmann() rounds to 1 decimal)."""
+    return f"fastrack_{round(float(level), 1)}_15x15.npy"
+
+
+def load_value_tables(source, cfg):
+    """The HJ value tables an env of configuration ``cfg`` reads, as (V [T, 15**6] float32 numpy,
+    table_of_level).  ``source``:
+      * a directory holding ``fastrack_{level}_15x15.npy`` (the reference's FasTrack_data folder), or
+        the reference's repository root (the files under ``REFERENCE_TABLE_DIR``);
+      * a dict {level: array of 15**6 values};
+      * an array [T, 15**6] / [15]*6 / [T, 15, ..., 15] (bound as given; one table = every level).
+    Files are read with ``np.load(allow_pickle=False)`` (they are plain arrays; nothing in them is
+    executed).  A fixed-level env needs the table of its level only; a Boltzmann-level env one per
+    level of ``cfg.level_values`` (distur_gener loads ``fastrack_{level}`` per call)."""
+    import os
+    nl = int(cfg.num_levels)
+    boltz = int(cfg.level_mode) == 1
+    levels = [float(cfg.level_values[k]) for k in range(nl)] if boltz else [float(cfg.dstb_level)]
+    if isinstance(source, (str, os.PathLike)):
+        root = os.fspath(source)
+        cand = [root, os.path.join(root, REFERENCE_TABLE_DIR)]
+        tabs = {}
+        for lv in levels:
+            name = value_table_name(lv)
+            path = next((os.path.join(d, name) for d in cand if os.path.isfile(os.path.join(d, name))), None)
+            if path is None:
+                raise FileNotFoundError(f"{name} not found in {root} or {os.path.join(root, REFERENCE_TABLE_DIR)}")
+            tabs[round(lv, 1)] = np.load(path, allow_pickle=False)
+        source = tabs
+    if isinstance(source, dict):
+        keys = {round(float(k), 1): v for k, v in source.items()}
+        uniq, rows, tol = [], {}, []
+        for lv in levels:
+            k = round(lv, 1)
+            if k not in keys:
+                raise KeyError(f"no value table for level {k}")
+            obj = id(keys[k])                 # levels given the same array share one row
+            if obj not in rows:
+                rows[obj] = len(uniq)
+                uniq.append(np.asarray(keys[k], dtype=np.float32).reshape(-1))
+            tol.append(rows[obj])
+        V = np.stack(uniq)
+        table_of_level = tol if boltz else [0] * nl
+    else:
+        V = np.asarray(source.cpu() if isinstance(source, torch.Tensor) else source, dtype=np.float32)
+        V = V.reshape(-1, 15 ** 6) if V.size % 15 ** 6 == 0 else V
+        table_of_level = None
+    if V.ndim != 2 or V.shape[1] != 15 ** 6:
+        raise ValueError("HJ value tables must be 15^6 grids")
+    return np.ascontiguousarray(V), table_of_level
+
+
 def _check_buf(t, name, shape, dtype, device, align=4):
     """Raise ValueError unless t is a contiguous `dtype` tensor of `shape` on `device` whose data
     pointer is `align`-byte aligned (the kernel reads and writes these buffers with no bounds
@@ -45,7 +103,7 @@ def _check_buf(t, name, shape, dtype, device, align=4):
 class BatchedCrazyflieEnv:
     def __init__(self, env_id: str, num_envs: int, seed: int = 0, device=None, env_id_offset: int = 0,
                  auto_reset: bool = True, want_final_obs: bool = False, config: CF2Config | None = None,
-                 _spec=None, **env_kwargs):
+                 _spec=None, value_tables=None, copy_outputs: bool = False, **env_kwargs):
         if not torch.cuda.is_available():
             raise _native.CF2Error("BatchedCrazyflieEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -78,9 +136,14 @@ class BatchedCrazyflieEnv:
         self._state_version = 0          # bumped by every call that changes the env state
         self._snap = None                # (version, state_f, state_i) of the last snapshot()
         self._tables = None
+        # step() returns its output buffers themselves (overwritten by the next step) unless
+        # copy_outputs, or step(copy=True)
+        self.copy_outputs = bool(copy_outputs)
         # spaces (envs/base.py:139-148)
         self.observation_space = make_box(-1000.0, 1000.0, shape=(self.obs_dim,), dtype=np.float32)
         self.action_space = make_box(-1.0, 1.0, shape=(4,), dtype=np.float32)
+        if value_tables is not None:
+            self.bind_value_tables(value_tables)
 
     # ---- lifecycle ----
     def close(self):
@@ -123,12 +186,23 @@ class BatchedCrazyflieEnv:
         _native.check(self.lib.cf2_bind_hj_tables(self._ctx, V.data_ptr(), V.shape[0], t), "cf2_bind_hj_tables")
         self._tables = V   # keep alive
 
+    def bind_value_tables(self, source):
+        """Load and bind the HJ value tables this env reads (``load_value_tables``: the reference's
+        ``fastrack_{level}_15x15.npy`` files from a directory, a dict by level, or an array)."""
+        V, table_of_level = load_value_tables(source, self.cfg)
+        self.bind_hj_tables(torch.from_numpy(V), table_of_level)
+
     # ---- gym-like API ----
     def reset(self, mask: torch.Tensor | None = None) -> torch.Tensor:
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
-        if mask is not None and self._obs_latest is not None and self._obs_latest is not self.obs:
+            if self._obs_latest is None:
+                # the rows of the envs that do not reset would keep stale values: the latest
+                # observations went to a raw pointer (step_raw(obs_ptr=) or a raw collect step)
+                raise ValueError("masked reset after a step into a raw obs pointer: the other envs' observations "
+                                 "are not in env.obs; copy them into env.obs (or reset all envs) first")
+        if mask is not None and self._obs_latest is not self.obs:
             # a masked reset writes only the reset envs' rows: the others must already be in self.obs
             self.obs.copy_(self._obs_latest)
         _native.check(self.lib.cf2_reset(self._ctx, _native.ptr(m), self.obs.data_ptr(), self.stream), "cf2_reset")
@@ -136,7 +210,12 @@ class BatchedCrazyflieEnv:
         self._obs_latest = self.obs
         return self.obs
 
-    def step(self, actions: torch.Tensor, dstb: torch.Tensor | None = None):
+    def step(self, actions: torch.Tensor, dstb: torch.Tensor | None = None, copy: bool | None = None):
+        """One env-step of every env: (obs [N, D], rew [N], done [N] uint8, info).
+
+        The returned tensors are this env's output buffers (self.obs, self.rew, ...), written
+        again by the next step(): a caller that keeps a step's results across steps must clone
+        them, or pass copy=True (or construct with copy_outputs=True) to get fresh tensors."""
         a = torch.as_tensor(actions)
         if a.device != self.device or a.dtype != torch.float32 or not a.is_contiguous() or a.data_ptr() % 16:
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
@@ -162,6 +241,9 @@ class BatchedCrazyflieEnv:
         info = {"cost": self.cost, "truncated": self.trunc, "disturbance_level": self.level}
         if self.final_obs is not None:
             info["final_obs"] = self.final_obs
+        if self.copy_outputs if copy is None else copy:
+            info = {k: v.clone() for k, v in info.items()}
+            return self.obs.clone(), self.rew.clone(), self.done.clone(), info
         return self.obs, self.rew, self.done, info
 
     def step_into(self, actions: torch.Tensor, obs_out: torch.Tensor, rew_out: torch.Tensor, done_out: torch.Tensor,
@@ -209,7 +291,8 @@ class BatchedCrazyflieEnv:
         st = self.lib.cf2_collect_step(
             self._ctx, actions.data_ptr(), obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
             _native.ptr(trunc_out), _native.ptr(final_obs_out), policy.w.data_ptr(), od, policy.prec, policy.seed,
-            policy.counter & 0xFFFFFFFF, 0, act_out.data_ptr(), val_out.data_ptr(), logp_out.data_ptr(), self.stream)
+            policy.counter & 0xFFFFFFFF, int(self.cfg.env_id_offset), act_out.data_ptr(), val_out.data_ptr(),
+            logp_out.data_ptr(), self.stream)
         if st == _native.CF2_ERR_UNSUPPORTED:
             return False
         _native.check(st, "cf2_collect_step")
@@ -224,8 +307,8 @@ class BatchedCrazyflieEnv:
         whose slabs collect_step_into has checked; the C ABI still rejects null or misaligned
         pointers): keeps the host's per-step cost well under the kernel's."""
         st = self.lib.cf2_collect_step(self._ctx, act, obs, rew, done, trunc, final_obs, policy.w_ptr, self.obs_dim,
-                                       policy.prec, policy.seed, policy.counter & 0xFFFFFFFF, 0, act_out, val_out,
-                                       logp_out, self.stream)
+                                       policy.prec, policy.seed, policy.counter & 0xFFFFFFFF, int(self.cfg.env_id_offset),
+                                       act_out, val_out, logp_out, self.stream)
         if st == _native.CF2_ERR_UNSUPPORTED:
             return False
         _native.check(st, "cf2_collect_step")
@@ -299,10 +382,17 @@ class BatchedCrazyflieEnv:
         _native.check(self.lib.cf2_set_state(self._ctx, sf.data_ptr(), si.data_ptr(), self.stream), "cf2_set_state")
         self._state_version += 1
 
+    def invalidate(self):
+        """Mark the cached snapshot (and the observations' owner) stale.  Needed after anything
+        that changes the state without going through this object: replaying a hipGraph that
+        captured step_raw / step_into, or calling the C ABI on self._ctx directly."""
+        self._state_version += 1
+
     def snapshot(self):
         """get_state(), cached until the next call that changes the state (step, reset, rollout,
         set_state, a physics-plugin step): repeated reads of agent attributes between two steps
-        cost one conversion kernel, not one each.  The tensors are shared: do not modify them."""
+        cost one conversion kernel, not one each.  The tensors are shared: do not modify them.
+        A graph replay or a direct C-ABI call does not update the cache: call invalidate()."""
         if self._snap is None or self._snap[0] != self._state_version:
             sf, si = self.get_state()
             self._snap = (self._state_version, sf, si)

@@ -26,7 +26,7 @@ struct cf2_ctx {
 
 static thread_local int g_last_hip_error = 0;
 
-static int hip_fail(hipError_t e) {
+int cf2::hip_fail(hipError_t e) {
     g_last_hip_error = (int)e;
     return e == hipErrorOutOfMemory ? CF2_ERR_OUT_OF_MEMORY : CF2_ERR_HIP;
 }
@@ -50,6 +50,33 @@ static int validate(const cf2_config* c) {
     if (M > 1 && c->physics != CF2_PHYS_BULLET) return CF2_ERR_UNSUPPORTED;
     return CF2_OK;
 }
+
+// Bytes one env-step of this configuration moves (state read + written once, the action, every
+// step() output); per-episode writes excluded.  The same count as bench.py's
+// algorithmic_bytes_per_env_step over the whole step() boundary (762 B for the bench workload).
+static uint64_t step_bytes_per_env(const cf2_config* c) {
+    const bool noise = c->observation_noise_on, dr = c->domain_randomization_on;
+    const int ol = noise ? 13 : 17, B = c->buf_size;
+    const bool held = (c->aggregate_phy_steps % c->obs_rate) != 0;
+    const bool gust_or_const = c->disturbance == CF2_DSTB_CONST || c->disturbance == CF2_DSTB_GUST;
+    const bool level = c->disturbance == CF2_DSTB_CONST || c->disturbance == CF2_DSTB_HJ ||
+                       c->level_mode == CF2_LEVEL_BOLTZMANN;
+    int persist = 13 + 8 + 4 * B + (noise ? 6 : 0) + (noise && held ? 10 : 0) + ol + 8;
+    if (c->physics == CF2_PHYS_SIMPLE) persist += 3;
+    if (c->use_motor_dynamics) persist += 4;
+    const int rd_f = persist + (dr ? 15 : 0) + (gust_or_const ? 3 : 0) + (level ? 1 : 0);
+    const int wr_f = persist + (c->disturbance == CF2_DSTB_GUST ? 3 : 0);
+    const int rd_i = 3 + (level ? 1 : 0) + (c->disturbance == CF2_DSTB_GUST ? 1 : 0);
+    const int wr_i = 3 + (c->disturbance == CF2_DSTB_GUST ? 1 : 0);
+    uint64_t b = 4u * (uint64_t)(rd_f + wr_f + rd_i + wr_i) + 16u;
+    if (c->disturbance == CF2_DSTB_EXTERNAL) b += 12u;
+    const int od = 2 * (ol + 4);
+    return b + 4u * (uint64_t)od + 4u + 1u + 1u + 4u + 4u;
+}
+// Working-set bytes above which the step kernel's state stores are non-temporal: the Infinity
+// Cache is 256 MB; measured on the bench workload, 327 680 envs (250 MB) run faster with plain
+// stores and 393 216 envs (300 MB) with nt stores (profiles/r03_ab_nt_threshold.txt)
+static const uint64_t NT_STATE_BYTES = 240ull << 20;
 
 static void fill_tables(const cf2_config* c, KTables& T) {
     memset(&T, 0, sizeof(T));
@@ -159,6 +186,7 @@ static void fill_params(const cf2_config* c, KParams& P) {
     P.tab = nullptr;
     P.V = nullptr;
     P.hj_bits = nullptr;
+    P.nt_state = (uint64_t)c->num_envs * step_bytes_per_env(c) > NT_STATE_BYTES ? 1u : 0u;
 }
 
 extern "C" {
@@ -200,6 +228,7 @@ int cf2_create(const cf2_config* cfg, cf2_ctx** out_ctx) {
         for (int k = 0; k < 9; ++k) { T.dr_lo[k] = P.dr_lo[k]; T.dr_hi[k] = P.dr_hi[k]; }
     }
     hipError_t e = hipGetDevice(&ctx->device);
+    if (e == hipSuccess) e = query_occupancy(ctx->P);      // this device, this config's kernel instances
     if (e != hipSuccess) { delete ctx; return hip_fail(e); }
     const size_t N = cfg->num_envs;
     e = hipMalloc((void**)&ctx->tab_dev, sizeof(KTables));

@@ -70,6 +70,9 @@ enum : int {
 __host__ __device__ constexpr uint32_t tiles_of(uint32_t n) { return (n + 63u) / 64u; }
 __host__ __device__ constexpr size_t state_bytes(uint32_t n) { return (size_t)tiles_of(n) * NG * 1024u; }
 enum { HJ_PTS = 15, HJ_TABLE = 11390625 };
+// up to this many envs per context the env kernels run 64 envs per 256-thread block with helper
+// waves (step_kernel_small, rollout_kernel_small, collect_kernel_small)
+constexpr uint32_t SMALL_N_MAX = 32768;
 enum { PHYS_BULLET_T = 0, PHYS_SIMPLE_T = 1 };
 enum { DSTB_NONE_T = 0, DSTB_EXTERNAL_T = 1, DSTB_UNIFORM_T = 2, DSTB_CONST_T = 3, DSTB_GUST_T = 4, DSTB_HJ_T = 5 };
 enum { LEVEL_FIXED_T = 0, LEVEL_BOLTZMANN_T = 1 };
@@ -80,7 +83,11 @@ struct KParams {
     uint32_t N, gid_off, key0, key1;
     uint32_t late_block;          // step kernel: first block index past one residency round (set per launch)
     uint32_t out_stride;          // rollout kernel: rows per per-step output slab (set per launch)
-    uint32_t epb;                 // step kernel: envs per block, 64 or CF2_STEP_BLOCK (set per launch)
+    // host-side, set once at cf2_create for the context's device and configuration: blocks
+    // resident at once of the large-N step / fused rollout / fused collect kernels
+    // (query_occupancy), and whether the step's working set exceeds the Infinity Cache
+    // (nt state stores)
+    uint32_t rb_step, rb_roll, rb_collect, nt_state;
     int32_t agg, obs_rate, buf_size, use_latency, use_motor_dyn, max_steps, auto_reset, reset_dist;
     int32_t dstb_mode, level_mode, num_levels, gust_dur, noise, dr, phys, held_persistent, need_level;
     float time_step, mass, ixx, iyy, izz, ft0, ft1, K, A, B, hover_x, hover_action, ou_sigma;
@@ -130,6 +137,10 @@ struct StepIO {
     float* final_obs;
 };
 
+// records e as the thread's last HIP error (cf2_last_hip_error) and maps it to a cf2_status
+int hip_fail(hipError_t e);
+// fills P.rb_* for the kernel instances P dispatches to, on the current device
+hipError_t query_occupancy(KParams& P);
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
 // The collect loop's policy half, fused behind the env-step (collect_kernel): the actor-critic
 // forward on the new observations (packed bf16x3 fragments of cf2_policy_pack, obs_dim 34)

@@ -456,16 +456,11 @@ __device__ __forceinline__ F4 f4(float x, float y, float z, float w) { return F4
 __device__ __forceinline__ float ib(int v) { return __int_as_float(v); }       // int field -> slot bits
 __device__ __forceinline__ int bi(float v) { return __float_as_int(v); }
 
-#ifndef CF2_STATE_LD_AUX
-#define CF2_STATE_LD_AUX 0     // cache-policy bits of the state loads (A/B: 2 = nt)
-#endif
-#ifndef CF2_STATE_ST_AUX
-#define CF2_STATE_ST_AUX 0     // ... and stores
-#endif
 // ST_AUX: cache-policy bits of the state stores.  2 = nt: the step kernel's stores when the
 // working set exceeds the Infinity Cache (launch_step_t) -- at 1 Mi envs 185 -> 144 us, while at
-// 262 144 envs (cache-resident) nt stores cost +3 us, as nt loads do at both sizes.
-template <int ST_AUX = CF2_STATE_ST_AUX>
+// 262 144 envs (cache-resident) nt stores cost +3 us, as nt loads do at both sizes (the loads
+// always use the default policy).
+template <int ST_AUX = 0>
 struct TileT {
     __amdgpu_buffer_rsrc_t r;
     uint32_t voff;
@@ -473,7 +468,7 @@ struct TileT {
         : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(uint32_t)state_bytes(N), 0x00020000)),
           voff((i >> 6) * (uint32_t)(NG * 1024) + (i & 63u) * 16u) {}
     __device__ __forceinline__ F4 ld(int g) const {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + (uint32_t)g * 1024u), 0, CF2_STATE_LD_AUX);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(voff + (uint32_t)g * 1024u), 0, 0);
         return F4{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
     }
     __device__ __forceinline__ void st(int g, F4 f) const {
@@ -589,7 +584,7 @@ __device__ __forceinline__ void load_env(const KParams& P, const float* __restri
 
 // state the physics sub-steps update (stored as soon as the last sub-step is done; group 3,
 // which carries the counters, is stored with the history at the end of the step)
-template <bool NOISE, bool DR, int PHYS, int ST_AUX = CF2_STATE_ST_AUX>
+template <bool NOISE, bool DR, int PHYS, int ST_AUX = 0>
 __device__ __forceinline__ void store_core(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
     const TileT<ST_AUX> T(sf, P.N, i);
     T.st(0, f4(E.p[0], E.p[1], E.p[2], E.q[0]));
@@ -627,7 +622,7 @@ __device__ __forceinline__ void store_obs_prev(const TT& T, const Env& E) {
 }
 
 // end of the step: history, counters (group 3 with the last angular-rate component)
-template <bool NOISE, int ST_AUX = CF2_STATE_ST_AUX>
+template <bool NOISE, int ST_AUX = 0>
 __device__ __forceinline__ void store_tail(const KParams& P, float* __restrict__ sf, uint32_t i, const Env& E) {
     const TileT<ST_AUX> T(sf, P.N, i);
     T.st(G_HACT, f4(E.hact[0][0], E.hact[0][1], E.hact[0][2], E.hact[0][3]));
@@ -1342,14 +1337,10 @@ enum { SEED_WORDS = 13 };
 // HD (small-N kernel, reference-default shape with sensor noise): the draws after the first
 // sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
 // env wave joins the helpers' LDS barrier before its second sub-step.
-// fin (small-N kernel, HD): this env's column of the [word][env] LDS table the outputs are
-// finished from (FIN_* layout), or null to finish them here.
-enum { FIN_P = 0, FIN_V = 3, FIN_RPY = 6, FIN_WB = 9, FIN_FLAGS = 12, FIN_LEVEL = 13, FIN_WORDS = 14 };
-template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, class KT = Keys,
-          int ST_AUX = CF2_STATE_ST_AUX>
+template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0>
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
                                               float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
-                                              const float* hd = nullptr, float* fin = nullptr) {
+                                              const float* hd = nullptr) {
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     const uint32_t gid = P.gid_off + i;
@@ -1357,8 +1348,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     TREADY("v"(E.p[0]), "v"(E.obs_prev[OL - 1]), "v"(E.hact[1][3]), "v"(E.K[3]), "v"(a4.w), "v"(E.rng));
     TSTAMP(1);   // every state load has landed
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-    const KT K = make_keys_as((const KT*)nullptr, P.key0, P.key1);
-    const RngT<KT> g{K, E.rng, gid, TAG_STEP};
+    const Keys K = make_keys(P.key0, P.key1);
+    const Rng g{K, E.rng, gid, TAG_STEP};
     // reference-default shape: the final (full) sensor call's blocks are drawn up front (RowRng)
     const bool pre_final = !HD && NOISE && P.agg == 2 && P.obs_rate == 2;
     const uint32_t* hdw = reinterpret_cast<const uint32_t*>(hd);
@@ -1501,16 +1492,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     // resets follow __syncthreads, whose workgroup-scope release/acquire orders these stores before
     // the reset waves' stores to the same groups (skipping them cost 0.6 us there)
     if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS, ST_AUX>(P, io.sf, i, E);
-    if (HD && fin != nullptr) {
-        // small-N kernel: reward, cost and the per-env outputs are finished by a helper wave after
-        // the block barrier (finish_outputs), off this wave's chain; it gets what they read
-        fin[FIN_P * 64] = E.p[0]; fin[(FIN_P + 1) * 64] = E.p[1]; fin[(FIN_P + 2) * 64] = E.p[2];
-        fin[FIN_V * 64] = E.v[0]; fin[(FIN_V + 1) * 64] = E.v[1]; fin[(FIN_V + 2) * 64] = E.v[2];
-        fin[FIN_RPY * 64] = E.rpy[0]; fin[(FIN_RPY + 1) * 64] = E.rpy[1]; fin[(FIN_RPY + 2) * 64] = E.rpy[2];
-        fin[FIN_WB * 64] = E.wb[0]; fin[(FIN_WB + 1) * 64] = E.wb[1]; fin[(FIN_WB + 2) * 64] = E.wb[2];
-        fin[FIN_FLAGS * 64] = __uint_as_float((term ? 1u : 0u) | (trunc ? 2u : 0u));
-        fin[FIN_LEVEL * 64] = level_used;
-    } else {
+    {
         const float r = compute_reward(P, E, a, term);
         const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
         io.rew[i] = r;
@@ -1544,17 +1526,15 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     return do_reset;
 }
 
-template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = CF2_STATE_ST_AUX>
+template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0>
 __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
-                                         ResetSeed& rs, const double* hj_grid, const float* hd = nullptr,
-                                         float* fin = nullptr) {
+                                         ResetSeed& rs, const double* hj_grid, const float* hd = nullptr) {
     Env E;
     // every state load is issued before the first state store: on gfx9 vmcnt also counts stores,
     // so a load issued after the state stores would wait for the whole store burst to drain (the
     // history is loaded after the physics sub-steps, still ahead of store_core, in step_env_body)
     load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
-    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD, Keys, ST_AUX>(P, io, i, E, obs_row, rs, hj_grid, hd,
-                                                                                 fin);
+    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD, ST_AUX>(P, io, i, E, obs_row, rs, hj_grid, hd);
 }
 
 // Reset one env in place: reads only what a reset consumes from the finished episode (the
@@ -1590,31 +1570,6 @@ __device__ __forceinline__ void reset_one(const KParams& P, float* __restrict__ 
     E.rng = rng_ctr + 1;
     if (obs) write_obs<NOISE>(obs, i, o);
     store_env<NOISE, DR, PHYS>(P, sf, i, E, true);
-}
-
-// Auto-reset of env i from a seed handed over in LDS; the reset observation goes to obs_row (LDS).
-template <bool NOISE, bool DR, int PHYS>
-__device__ __forceinline__ void reset_seeded(const KParams& P, float* __restrict__ sf, uint32_t i, const ResetSeed& rs,
-                                             const TableRng& g, float* __restrict__ obs_row) {
-    constexpr int OD = NOISE ? 34 : 42;
-    Env E;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { E.wb[k] = rs.wb[k]; E.bias[k] = rs.bias[k]; }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) E.ou[k] = rs.ou[k];
-    E.level = rs.level;
-    E.level_idx = rs.level_idx;
-    E.rng = rs.ctr;
-    float o[OD];
-    TSTAMP(6);
-    reset_env<NOISE, DR, PHYS>(P, E, g, P.gid_off + i, o);
-    TREADY("v"(o[OD - 1]), "v"(E.p[0]), "v"(E.K[3]));
-    TSTAMP(7);   // reset state + observation computed
-    E.rng = rs.ctr + 1;
-#pragma unroll
-    for (int k = 0; k < OD; k += 2) *reinterpret_cast<float2*>(obs_row + k) = make_float2(o[k], o[k + 1]);
-    store_env<NOISE, DR, PHYS>(P, sf, i, E, true);
-    TSTAMP(8);   // reset stores issued
 }
 
 // The state groups an auto-reset writes, in three sets (their union is store_env(params_dirty)):
@@ -1720,7 +1675,7 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
 template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C>
 __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& io, uint32_t base, uint32_t tid,
                                                bool do_reset, const ResetSeed& rs, float* s_obs, uint32_t* s_list,
-                                               uint32_t* s_rand, uint32_t* s_wcnt, uint32_t EPB = B) {
+                                               uint32_t* s_rand, uint32_t* s_wcnt) {
     constexpr int OD = NOISE ? 34 : 42;
     constexpr uint32_t W = B / 64u;
     if (P.auto_reset) {
@@ -1747,9 +1702,6 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
         uint32_t wc[W], cnt = 0;
 #pragma unroll
         for (uint32_t w = 0; w < W; ++w) { wc[w] = s_wcnt[w]; cnt += wc[w]; }
-#ifdef CF2_AB_NO_RESET
-        cnt = 0;     // A/B only: measures the auto-reset tail's share
-#endif
         // global reset position -> block-local env index
         auto env_at = [&](uint32_t p) -> uint32_t {
             uint32_t w = 0;
@@ -1761,18 +1713,15 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
         // Resets run in chunks of C envs.  Their ~26 Philox blocks per env are drawn by every
         // thread of the block in parallel into LDS; then the reset math runs on the table, split
         // by role over the four waves.  (On one lane each, the draws made the reset tail, which
-        // every wave of the block waits for, about as long as the env-step itself.)
+        // every wave of the block waits for, about as long as the env-step itself; one wave running
+        // whole resets instead of the role split: 41.2 vs 40.1 us at 262 144 envs.)
+        static_assert(B == 256u, "four waves, one reset role each");
         for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
             const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
-#ifndef CF2_RESET_ONE_WAVE
-            const bool roles = B == 256u;
-#else
-            const bool roles = false;
-#endif
             // role lanes take their seed now: this chunk's rows are only overwritten after the
             // barrier below (and other chunks' roles never touch them), so no extra barrier
             const uint32_t rl = tid & 63u, role = ((tid >> 6) + blockIdx.x) & 3u;
-            const bool act = roles && rl < nc;
+            const bool act = rl < nc;
             ResetSeed q;
             uint32_t t = 0;
             if (act) {
@@ -1808,31 +1757,11 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
                 }
             }
             __syncthreads();
-            if (roles) {
-                // the four waves split each reset by role (reset_role); the role of a wave rotates
-                // with the block index so the co-resident blocks' roles spread over the SIMDs
-                if (act) {
-                    const TableRng tg{s_rand + rl, C};
-                    reset_role<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD, role);
-                }
-            } else {
-                // one wave runs whole resets; it rotates with the block index, so the resets of
-                // the blocks sharing a CU do not all queue on one SIMD
-                const uint32_t r1 = tid - 64u * (blockIdx.x % W);
-                if (r1 < nc) {
-                    const uint32_t t1 = env_at(c0 + r1);
-                    const uint32_t* row = reinterpret_cast<const uint32_t*>(s_obs + t1 * OD);
-                    ResetSeed q1;
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) { q1.wb[c] = __uint_as_float(row[c]); q1.bias[c] = __uint_as_float(row[3 + c]); }
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) q1.ou[c] = __uint_as_float(row[6 + c]);
-                    q1.level = __uint_as_float(row[10]);
-                    q1.level_idx = (int)row[11];
-                    q1.ctr = row[12];
-                    const TableRng tg{s_rand + r1, C};
-                    reset_seeded<NOISE, DR, PHYS>(P, io.sf, base + t1, q1, tg, s_obs + t1 * OD);
-                }
+            // the four waves split each reset by role (reset_role); the role of a wave rotates
+            // with the block index so the co-resident blocks' roles spread over the SIMDs
+            if (act) {
+                const TableRng tg{s_rand + rl, C};
+                reset_role<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD, role);
             }
             __syncthreads();     // the next chunk reuses s_rand
         }
@@ -1840,36 +1769,28 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
     } else {
         __syncthreads();         // every obs row of the block is in LDS
     }
-    write_obs_rows(io.obs + (size_t)base * OD, s_obs, P.N - base < EPB ? P.N - base : EPB, EPB, OD, tid, B);
+    write_obs_rows(io.obs + (size_t)base * OD, s_obs, P.N - base < B ? P.N - base : B, B, OD, tid, B);
 }
 
-#ifndef CF2_STEP_MIN_WAVES
-#define CF2_STEP_MIN_WAVES 3   // waves per SIMD: <= 168 VGPRs (and <= 53 KB LDS per block)
-#endif
+// Launch shape of the large-N env kernels: 256-thread blocks of 256 envs (= the auto-reset
+// compaction group), 3 waves per SIMD (<= 168 VGPRs, <= 53 KB LDS per block); resets drawn and run
+// in chunks of 32
+constexpr uint32_t STEP_BLOCK = 256, STEP_MIN_WAVES = 3, RESET_CHUNK = 32;
 // Step kernel: one lane per env.  Auto-reset is compacted per block: with random actions a few
 // % of envs finish per step, so nearly every wave would hold one and run the whole reset path
 // divergently.  Finished envs are listed in LDS and reset by the fewest waves after a block
 // barrier; their state rows were just written by this block and are still in L2, so the reset's
 // scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
 // 4-byte field access for them).
-template <bool NOISE, bool DR, int PHYS, int SPEC, int ST_AUX = CF2_STATE_ST_AUX>
-#ifndef CF2_STEP_BLOCK
-#define CF2_STEP_BLOCK 256     // envs per block = auto-reset compaction group
-#endif
-__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
+template <bool NOISE, bool DR, int PHYS, int SPEC, int ST_AUX = 0>
+__global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
     const KParams P = shape_view<SPEC>(P0);
     // Issue priority: the blocks that start only after the first residency round (the partial
     // last round at 262 144 envs) run mostly alone on their SIMDs and end the kernel; their waves
-    // get the issue slots first, so they overlap the tail of the first round (-1 us measured).
+    // get the issue slots first, so they overlap the tail of the first round (-1 us measured;
+    // starting the first round's co-resident blocks 2k-8k cycles apart instead: equal or slower).
     if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
-#ifdef CF2_STAGGER
-    // experiment: the g-th block of each CU in the first round starts g * CF2_STAGGER cycles late
-    if (blockIdx.x < P0.late_block) {
-        const uint32_t g = blockIdx.x / (P0.late_block / 3u);
-        for (uint32_t k = 0; k < g * (CF2_STAGGER / 512); ++k) __builtin_amdgcn_s_sleep(8);   // ~512 cycles each
-    }
-#endif
 #ifdef CF2_TIMING
     if (uint64_t* r = timing_row()) {
         if ((threadIdx.x & 63) == 0) {
@@ -1882,27 +1803,18 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
     }
 #endif
     constexpr int OD = NOISE ? 34 : 42;
-    constexpr uint32_t B = CF2_STEP_BLOCK;
+    constexpr uint32_t B = STEP_BLOCK, C = RESET_CHUNK;
     __shared__ __align__(16) float s_obs[B * OD];          // the block's obs rows, global layout
     __shared__ uint32_t s_list[B];                         // queue: block-local env index
-#ifndef CF2_RESET_CHUNK
-#define CF2_RESET_CHUNK 32
-#endif
-    constexpr uint32_t C = CF2_RESET_CHUNK;                // auto-resets per chunk
-    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // their Philox blocks, [slot][word][env]
+    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];       // the chunk's Philox blocks, [slot][word][env]
     __shared__ uint32_t s_wcnt[B / 64];                    // finished envs per wave
-    // envs per block: B, or 64 at small N (set per launch): the block's other three waves then
-    // only help with its auto-resets (table draws and reset roles), which at small N are the
-    // launch's critical path, and four times as many CUs take part
-    const uint32_t EPB = P0.epb;
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * EPB, i = base + tid;
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
     bool do_reset = false;
     ResetSeed rs;
     __shared__ double s_hjgrid[6 * HJ_PTS];
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    if (tid < EPB && i < P.N)
-        do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
-    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, EPB);
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
+    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
     if (uint64_t* r = timing_row())
@@ -1930,31 +1842,18 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_STEP_MIN_WAVES) step_kerne
 // Built for the bench workload's shape (noise on: 34-wide observations; bf16x3 products) at
 // N > 32 768 (256 envs per block); other configs return hipErrorNotSupported and the caller runs
 // the two launches.
-#ifndef CF2_COLLECT_MIN_WAVES
-#define CF2_COLLECT_MIN_WAVES CF2_STEP_MIN_WAVES
-#endif
-#ifndef CF2_COLLECT_RT
-#define CF2_COLLECT_RT 1      // row tiles per forward call; 2 (two chains interleaved, 163 VGPRs): same time
-#endif
+// Delaying a third of the first round's blocks by 4k / 10k / 20k cycles, so that co-resident
+// blocks reach their policy phases at different times, was slower at every delay (62.1 / 64.1 /
+// 67.2 vs 61.1 us at 262 144 envs, profiles/r03_collect_ab.txt); two row tiles per forward call
+// (two chains interleaved, 163 VGPRs) took the same time as one.
 template <bool NOISE, bool DR, int PHYS, int SPEC>
-__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect_kernel(KParams P0, StepIO io,
-                                                                                       PolicyIO pio) {
+__global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) collect_kernel(KParams P0, StepIO io, PolicyIO pio) {
     static_assert(NOISE, "the fused collect kernel is built for the 34-wide observation");
     const KParams P = shape_view<SPEC>(P0);
     if (blockIdx.x >= P0.late_block) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
-#ifdef CF2_COLLECT_STAGGER
-    // A/B: the g-th third of the first round's blocks (one block per CU each) starts g * STAGGER
-    // cycles late, so co-resident blocks reach their policy phases at different times.  Measured
-    // slower at every delay (262 144 envs: 4k / 10k / 20k cycles 62.1 / 64.1 / 67.2 us against
-    // 61.1 us; profiles/r03_collect_ab.txt)
-    if (blockIdx.x < P0.late_block) {
-        const uint32_t g3 = blockIdx.x / (P0.late_block / 3u);
-        for (uint32_t k = 0; k < g3 * (CF2_COLLECT_STAGGER / 512); ++k) __builtin_amdgcn_s_sleep(8);
-    }
-#endif
     constexpr int OD = 34;
-    constexpr uint32_t B = CF2_STEP_BLOCK, C = CF2_RESET_CHUNK, W = B / 64u;
+    constexpr uint32_t B = STEP_BLOCK, C = RESET_CHUNK, W = B / 64u;
     static_assert(B == 256, "one 64-row wave per SIMD quarter of the block");
     using PK = Packed<OD, CF2_POLICY_BF16X3>;
     // LDS: the env phase's arrays, then the fragments but layer 3 (the tail from O_BIAS on moves
@@ -1975,15 +1874,12 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect
     ResetSeed rs;
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
-    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt, B);
-#if defined(CF2_COLLECT_AB) && CF2_COLLECT_AB == 1
-    return;                  // A/B only: the env phase alone
-#endif
+    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
     // ---- policy phase.  Lane l of wave wv holds, for row tile c, row 64 wv + 16 c + (l & 15):
     // inputs 8 g .. 8 g + 7 (k-block 0) and 32 + g (the fp32 k-step; clamped, zero weight past D)
     const uint32_t l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
     const int g = (int)(l >> 4);
-    constexpr int CR = CF2_COLLECT_RT, NCH = 4 / CR;          // row tiles per forward call, calls per wave
+    constexpr int CR = 1, NCH = 4 / CR;                       // row tiles per forward call, calls per wave
     ObsRegs<OD, CF2_POLICY_BF16X3, CR> X[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
@@ -2020,10 +1916,6 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect
             if (tid + q * B < NQ4) dst[tid + q * B] = stg[q];
     }
     __syncthreads();
-#if defined(CF2_COLLECT_AB) && CF2_COLLECT_AB == 2
-    if (X[0].x1[0][0] == 12345.0f) pio.val[i] = s_mem[tid];      // A/B only: staging, no forward
-    return;
-#endif
     PolicyLane<OD, CF2_POLICY_BF16X3> CL;
     policy_lane_init<OD, CF2_POLICY_BF16X3>(s_mem + PK::O_L3, g, CL);
 #pragma unroll
@@ -2060,36 +1952,14 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_COLLECT_MIN_WAVES) collect
 //   wave 2 (B): the pose again, the first reset sensor call's held measurement and gyro normals;
 //               stages the reset observation row but for its two gyro-LPF triples
 //   wave 3 (C): the pose again and the second sensor call's held part (into the staged row) and
-//               gyro normals (handed to B in LDS); after the barrier it finishes every env's reward,
-//               cost and outputs (finish_outputs), off the env wave's chain
+//               gyro normals (handed to B in LDS)
 // After one LDS barrier only the finished envs' work remains, on their lanes of waves 1-3: the two
 // gyro updates, which need the finished episode's body rates (the gyro LPF seed) and gyro bias,
 // the reset observation row, and the reset's state stores (store_reset_*).  The env wave does not
 // store the state of envs that reset (step_env_body), so no group is stored twice.
-// reward, cost and the per-env outputs of step_env_body, from the FIN_* table (the small-N
-// kernel's helper wave 3, after the block barrier)
-__device__ __forceinline__ void finish_outputs(const KParams& P, const StepIO& io, uint32_t i, const float* fin,
-                                               const float4 a4) {
-    Env F;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        F.p[k] = fin[(FIN_P + k) * 64]; F.v[k] = fin[(FIN_V + k) * 64];
-        F.rpy[k] = fin[(FIN_RPY + k) * 64]; F.wb[k] = fin[(FIN_WB + k) * 64];
-    }
-    const uint32_t fl = __float_as_uint(fin[FIN_FLAGS * 64]);
-    const bool term = fl & 1u, trunc = (fl & 2u) != 0u;
-    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) F.la[k] = a[k];      // apply_action's drone.last_action
-    const float r = compute_reward(P, F, a, term);
-    const float cost = io.cost ? compute_cost(P, F) : 0.0f;
-    io.rew[i] = r;
-    io.done[i] = (uint8_t)(term || trunc);
-    if (io.trunc) io.trunc[i] = (uint8_t)trunc;
-    if (io.cost) io.cost[i] = cost;
-    if (io.level) io.level[i] = fin[FIN_LEVEL * 64];
-}
-
+// Measured and not kept: reward, cost and the per-env outputs finished by helper wave 3 from an
+// LDS table after the barrier (32 768 envs 10.3 -> 11.0 us: the reset tail grew more than the env
+// wave's epilogue shrank); the DR draws before the draw barrier (10.6 -> 11.2 us).
 enum { SEED_SMALL = 10 };   // per finished env, wave 0 -> waves 1-3: final body rates, gyro bias, OU state
 enum { C2_WORDS = 9 };      // per env, wave 3 -> wave 2: the second reset sensor call's gyro normals
 
@@ -2101,29 +1971,21 @@ struct SmallLds {
     // reference-default shape with sensor noise: the helpers also draw the env-step's randomness
     // after its first sub-step (HD_* layout), handed over at an LDS barrier before sub-step 1
     static constexpr bool HD = SPEC == 1 && NOISE;
-#ifdef CF2_SMALL_OFFLOAD
-    static constexpr bool FIN = HD;  // A/B: reward / cost / outputs finished by helper wave 3
-#else
-    // measured slower (32 768 envs 10.3 -> 11.0 us): wave 3's post-barrier outputs lengthened
-    // the reset tail more than they shortened the env wave's epilogue
-    static constexpr bool FIN = false;
-#endif
     // word offsets in a carved buffer (doubles 8-B aligned, rows 16-B aligned)
     static constexpr uint32_t O_OBS = 0, O_RROW = 64 * OD, O_SEED = 128 * OD, O_C2 = O_SEED + SEED_SMALL * 64,
-                              O_DRAW = O_C2 + C2_WORDS * 64, O_FIN = O_DRAW + (HD ? HD_WORDS * 64 : 1),
-                              O_MASK = O_FIN + (FIN ? FIN_WORDS * 64 : 1), O_HJ = (O_MASK + 2 + 1) & ~1u,
-                              WORDS = O_HJ + 2 * 6 * HJ_PTS;
+                              O_DRAW = O_C2 + C2_WORDS * 64, O_MASK = O_DRAW + (HD ? HD_WORDS * 64 : 1),
+                              O_HJ = (O_MASK + 2 + 1) & ~1u, WORDS = O_HJ + 2 * 6 * HJ_PTS;
 };
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& io, float* s_obs, float* s_seed,
                                                float* s_c2, float* s_rrow, uint32_t* s_mask, double* s_hjgrid,
-                                               float* s_draw, float* s_fin) {
+                                               float* s_draw) {
     const KParams P = shape_view<SPEC>(P0);
     using SL = SmallLds<NOISE, SPEC>;
     constexpr int OL = SL::OL;
     constexpr int OD = SL::OD;
-    constexpr bool HD = SL::HD, FIN = SL::FIN;
+    constexpr bool HD = SL::HD;
 #ifdef CF2_TIMING
     if (uint64_t* r = timing_row()) {
         if ((threadIdx.x & 63) == 0) {
@@ -2140,21 +2002,9 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     const bool live = i < P.N;
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     const Tile T(io.sf, P.N, i);
-    // wave 3: this env's action, loaded at entry for finish_outputs after the barrier
-    float4 act_fin = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (FIN && wave == 3 && live) act_fin = reinterpret_cast<const float4*>(io.act)[i];
-    // domain randomisation / disturbance / level draws of the reset: on wave 1 with wave 3 busy
-    // finishing the outputs, else on wave 3
-#ifndef CF2_SMALL_PARAMS_WAVE
+    // the domain randomisation / disturbance / level draws of the reset: wave 1 in the
+    // reference-default shape (whose step draws waves 2 and 3 share), else wave 3
     constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
-#else
-    constexpr uint32_t PARAMS_WAVE = CF2_SMALL_PARAMS_WAVE;
-#endif
-#ifdef CF2_SMALL_PARAMS_EARLY
-    constexpr bool PARAMS_EARLY = HD;    // A/B: the DR draws before the draw barrier
-#else
-    constexpr bool PARAMS_EARLY = false;
-#endif
     Env H;                         // waves 1-3: the speculative reset (kept across the barrier)
     float held1[10], ng1[9];       // wave 2: first reset sensor call
     HeldNoise hn;                  // waves 2 / 3: the noise of the first / second reset sensor call
@@ -2164,17 +2014,16 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     const Keys K = make_keys(P.key0, P.key1);
     const Rng gr{K, ctr, gid, TAG_RESET};
     // the speculative reset's work that needs no reset pose: DR / disturbance / level draws (wave
-    // PARAMS_WAVE) and the two reset sensor calls' noise (waves 2, 3).  Measured: all of it before
-    // the draw barrier (in the time the helpers wait there) made the env wave wait at that barrier
-    // (32 768 envs 10.6 -> 11.2 us); CF2_SMALL_PARAMS_EARLY moves only the DR draws there
-    auto reset_prework = [&](bool before_draw_barrier) {
-        if (wave == PARAMS_WAVE && before_draw_barrier == PARAMS_EARLY) {
+    // PARAMS_WAVE) and the two reset sensor calls' noise (waves 2, 3), after the draw barrier (all
+    // of it before that barrier, in the time the helpers wait there, made the env wave wait at it)
+    auto reset_prework = [&]() {
+        if (wave == PARAMS_WAVE) {
             const bool need_level = P.need_level || io.level != nullptr;
             H.level = need_level ? T.ld(G_LEVEL).w : P.level_fixed;
             H.level_idx = need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
             reset_params<DR>(P, H, gr);
         }
-        if (NOISE && wave >= 2 && !before_draw_barrier) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
+        if (NOISE && wave >= 2) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
     };
     if (HD && wave != 0) {
         // the env-step's draws after sub-step 0 (step tag, the env's counter), split over the
@@ -2211,7 +2060,6 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
                 d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
                 d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
             }
-            if (P.auto_reset && PARAMS_EARLY) reset_prework(true);
         }
         TSTAMP(10);      // helper: step draws in LDS
         lds_barrier();   // joined by the env wave before its second sub-step (step_env_body)
@@ -2222,8 +2070,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
         bool do_reset = false;
         ResetSeed rs;
         if (live)
-            do_reset = step_env<NOISE, DR, PHYS, true, HD>(P, io, i, s_obs + lane * OD, rs, s_hjgrid, s_draw + lane,
-                                                          FIN ? s_fin + lane : nullptr);
+            do_reset = step_env<NOISE, DR, PHYS, true, HD>(P, io, i, s_obs + lane * OD, rs, s_hjgrid, s_draw + lane);
         const uint64_t m = __ballot(do_reset);
         if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
         if (do_reset) {
@@ -2234,7 +2081,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
         }
     } else if (P.auto_reset && live) {
         __builtin_amdgcn_s_setprio(0);
-        reset_prework(false);
+        reset_prework();
         if (wave == 1) {
             reset_kinematics<PHYS>(P, H, gr, gid);
         } else if (wave == 2) {
@@ -2273,11 +2120,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     lds_barrier();
     TSTAMP(4);   // block barrier passed
     const uint64_t mask = ((uint64_t)s_mask[1] << 32) | (uint64_t)s_mask[0];
-#ifdef CF2_AB_NO_RESET
-    const bool mine = false;       // A/B only: measures the reset tail's share
-#else
     const bool mine = wave != 0 && ((mask >> lane) & 1ull);
-#endif
     if (mine) {
         TSTAMP(6);
         if (wave == 1) {
@@ -2319,7 +2162,6 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
         }
         if (wave == PARAMS_WAVE) store_reset_params<DR>(P, T, H);
     }
-    if (FIN && wave == 3 && live) finish_outputs(P, io, i, s_fin + lane, act_fin);
     lds_barrier();
     TSTAMP(12);  // reset rows in LDS
     write_obs_rows_merged<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, P.N - base < 64u ? P.N - base : 64u,
@@ -2342,8 +2184,7 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
     __shared__ double s_hjgrid[6 * HJ_PTS];
     __shared__ float s_draw[SL::HD ? HD_WORDS * 64 : 1];
-    __shared__ float s_fin[SL::FIN ? FIN_WORDS * 64 : 1];
-    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw, s_fin);
+    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw);
 }
 
 // The fused collect step at small N (N <= 32 768: the 8-GPU node shard, C2): step_kernel_small's
@@ -2366,7 +2207,7 @@ __global__ void __launch_bounds__(256, 2) collect_kernel_small(KParams P0, StepI
     const uint64_t mask = small_body<NOISE, DR, PHYS, SPEC>(
         P0, io, s_mem + SL::O_OBS, s_mem + SL::O_SEED, s_mem + SL::O_C2, s_mem + SL::O_RROW,
         reinterpret_cast<uint32_t*>(s_mem + SL::O_MASK), reinterpret_cast<double*>(s_mem + SL::O_HJ),
-        s_mem + SL::O_DRAW, s_mem + SL::O_FIN);
+        s_mem + SL::O_DRAW);
     // ---- policy phase: wave w takes rows 16 w .. 16 w + 15 of the block (lane l: row 16 w + (l & 15),
     // inputs 8 g .. 8 g + 7 and 32 + g)
     const uint32_t tid = threadIdx.x, l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
@@ -2462,33 +2303,25 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
 // finished envs and draws their reset tables block-parallel as step_kernel does, but each env is
 // then reset in place by its own lane (its state is in that lane's registers); per env-step HBM
 // traffic is the actions and the outputs only (~170 B instead of ~765 B).
-#ifndef CF2_ROLL_MIN_WAVES
-#define CF2_ROLL_MIN_WAVES 2   // the whole state stays live across the loop (~270 registers at peak)
-#endif
-// Round keys of the fused rollout.  With all 20 in SGPRs (Keys) the kernel spills 28 B/lane of
-// VGPRs (7 registers); re-deriving them per Philox call (KeysBase, -DCF2_ROLL_BASE_KEYS) removes
-// every VGPR spill but was slower on MI355X (K = 32 per env-step: 27.9 -> 30.0 us at 262 144 envs,
-// 8.5 -> 10.1 us at 4096): the SALU adds sit in each Philox chain, the spills do not.
-#ifdef CF2_ROLL_BASE_KEYS
-typedef KeysBase RollKeys;
-#else
-typedef Keys RollKeys;
-#endif
-template <bool NOISE, bool DR, int PHYS, int SPEC, uint32_t EPB>
-__global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_kernel(KParams P0, StepIO io0, uint32_t K,
-                                                                                  uint32_t act_stride) {
+// 2 waves per SIMD: the whole state stays live across the loop (~270 registers at peak).  The 20
+// Philox round keys in SGPRs make it spill 28 B/lane of VGPRs (7 registers); re-deriving them per
+// Philox call removes every VGPR spill but was slower on MI355X (K = 32 per env-step: 27.9 -> 30.0
+// us at 262 144 envs, 8.5 -> 10.1 us at 4096): the SALU adds sit in each Philox chain, the spills
+// do not.
+constexpr uint32_t ROLL_MIN_WAVES = 2;
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(STEP_BLOCK, ROLL_MIN_WAVES) rollout_kernel(KParams P0, StepIO io0, uint32_t K,
+                                                                          uint32_t act_stride) {
     const KParams P = shape_view<SPEC>(P0);
     constexpr int OD = NOISE ? 34 : 42;
-    constexpr uint32_t B = CF2_STEP_BLOCK;
-    constexpr uint32_t C = CF2_RESET_CHUNK;
+    constexpr uint32_t B = STEP_BLOCK, EPB = STEP_BLOCK;
+    constexpr uint32_t C = RESET_CHUNK;
     __shared__ __align__(16) float s_obs[B * OD];
     __shared__ uint32_t s_list[B];
     __shared__ uint32_t s_ctr[B];                       // rng counter of each listed env's reset
     __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];
     __shared__ uint32_t s_cnt;
     __shared__ double s_hjgrid[6 * HJ_PTS];
-    // EPB: envs per block (64 at small N, as step_kernel; a template parameter here: a runtime
-    // count cost the large-N rollout 2.5 %)
     const uint32_t tid = threadIdx.x, base = blockIdx.x * EPB, i = base + tid;
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     const bool live = tid < EPB && i < P.N;
@@ -2509,7 +2342,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
         if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
         bool do_reset = false;
         ResetSeed rs;
-        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false, RollKeys>(P, io, i, E, obs_row, rs, s_hjgrid);
+        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false>(P, io, i, E, obs_row, rs, s_hjgrid);
         __syncthreads();             // s_cnt initialised
         uint32_t pos = 0;
         const uint64_t m = __ballot(do_reset);
@@ -2525,7 +2358,7 @@ __global__ void __launch_bounds__(CF2_STEP_BLOCK, CF2_ROLL_MIN_WAVES) rollout_ke
         for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
             const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
             {
-                const RollKeys Kk = make_keys_as((const RollKeys*)nullptr, P.key0, P.key1);
+                const Keys Kk = make_keys(P.key0, P.key1);
                 for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
                     const uint32_t sl = w / nc, e = w - sl * nc, p2 = c0 + e;
                     U4 u = philox(Kk, reset_block_of_slot((int)sl), s_ctr[p2], P.gid_off + base + s_list[p2], TAG_RESET);
@@ -2620,7 +2453,7 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
             bool do_reset = false;
             ResetSeed rs;
             if (live)
-                do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD, RollKeys>(P, io, i, E, obs_row, rs, s_hjgrid,
+                do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD>(P, io, i, E, obs_row, rs, s_hjgrid,
                                                                                      s_draw + lane);
             const uint64_t m = __ballot(do_reset);
             if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
@@ -2935,45 +2768,49 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 // ------------------------------------------------------------------------------------
 // host-side launch table
 // ------------------------------------------------------------------------------------
-#ifndef CF2_NT_STATE_BYTES
-#define CF2_NT_STATE_BYTES (240u << 20)   // working-set bytes (762 B per env-step) above which state stores are nt
-#endif
+// Blocks resident at once (CUs x blocks per CU at the kernel's VGPR / LDS use) of the large-N
+// kernels of this configuration, queried once per context at cf2_create for the context's device
+// (KParams::rb_*): the first block index past one residency round (step_kernel's issue priority)
+// and the slice size of the fused rollout.
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+static hipError_t occupancy_t(KParams& P) {
+    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_step, step_kernel<NOISE, DR, PHYS, SPEC>, STEP_BLOCK, 0);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_roll, rollout_kernel<NOISE, DR, PHYS, SPEC>, STEP_BLOCK, 0);
+    if constexpr (NOISE && SPEC == 1 && PHYS == PHYS_BULLET_T)
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_collect, collect_kernel<NOISE, DR, PHYS, SPEC>,
+                                                             STEP_BLOCK, 0);
+    if (e != hipSuccess) return e;
+    P.rb_step = (uint32_t)(cus * (per_step > 0 ? per_step : 1));
+    P.rb_roll = (uint32_t)(cus * (per_roll > 0 ? per_roll : 1));
+    P.rb_collect = (uint32_t)(cus * (per_collect > 0 ? per_collect : 1));
+    return hipSuccess;
+}
+
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
     // small N (<= 32768 envs: at most one 64-env wave per two SIMDs with the helpers) runs 64 envs
     // per block, the other three waves computing the envs' potential resets meanwhile
     // (step_kernel_small); above that the helper waves would cost residency (65 536 envs: 15.5 ->
     // 24.7 us with 64-env blocks)
-#ifndef CF2_SMALL_OLD
-    if (P.N <= 32768u) {
+    if (P.N <= SMALL_N_MAX) {
         hipLaunchKernelGGL((step_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s, P, io);
         return hipGetLastError();
     }
-#endif
-    const uint32_t epb = P.N <= 32768u ? 64u : (uint32_t)CF2_STEP_BLOCK;
-    const dim3 grid((P.N + epb - 1) / epb), block(CF2_STEP_BLOCK);
-    // blocks resident at once = CUs x blocks per CU at this kernel's VGPR/LDS use (queried once)
-    static int round_blocks = -1;
-    if (round_blocks < 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<NOISE, DR, PHYS, SPEC>, CF2_STEP_BLOCK, 0);
-        if (e != hipSuccess) return e;
-        round_blocks = cus * per_cu;
-    }
+    const dim3 grid((P.N + STEP_BLOCK - 1) / STEP_BLOCK), block(STEP_BLOCK);
     KParams Pl = P;
-    Pl.late_block = (uint32_t)round_blocks;
-    Pl.epb = epb;
-#ifndef CF2_NO_NT_STATE
-    // the env state (480 B per env) plus the step's I/O no longer fit the 256 MB Infinity Cache
-    // between env-steps: stream the state stores past it (nt), HBM-bound regime
-    if ((uint64_t)P.N * 762u > (uint64_t)CF2_NT_STATE_BYTES) {
+    Pl.late_block = P.rb_step;
+    // the env state plus the step's I/O no longer fit the 256 MB Infinity Cache between env-steps
+    // (P.nt_state, cf2_create): stream the state stores past it (nt), HBM-bound regime
+    if (P.nt_state) {
         hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC, 2>), grid, block, 0, s, Pl, io);
         return hipGetLastError();
     }
-#endif
     hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, Pl, io);
     return hipGetLastError();
 }
@@ -2982,50 +2819,28 @@ static hipError_t launch_collect_t(const KParams& P, const StepIO& io, const Pol
     if constexpr (!NOISE || SPEC != 1 || PHYS != PHYS_BULLET_T) {
         return hipErrorNotSupported;
     } else {
-        if (P.N <= 32768u) {     // small N: 64-env blocks with helper waves (as launch_step_t)
+        if (P.N <= SMALL_N_MAX) {     // small N: 64-env blocks with helper waves (as launch_step_t)
             hipLaunchKernelGGL((collect_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s,
                                P, io, pio);
             return hipGetLastError();
         }
-        static int round_blocks = -1;
-        if (round_blocks < 0) {
-            int dev = 0, cus = 0, per_cu = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e == hipSuccess)
-                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, collect_kernel<NOISE, DR, PHYS, SPEC>,
-                                                                 CF2_STEP_BLOCK, 0);
-            if (e != hipSuccess) return e;
-            round_blocks = cus * (per_cu > 0 ? per_cu : 1);
-        }
         KParams Pl = P;
-        Pl.late_block = (uint32_t)round_blocks;
-        Pl.epb = CF2_STEP_BLOCK;
-        hipLaunchKernelGGL((collect_kernel<NOISE, DR, PHYS, SPEC>), dim3((P.N + CF2_STEP_BLOCK - 1) / CF2_STEP_BLOCK),
-                           dim3(CF2_STEP_BLOCK), 0, s, Pl, io, pio);
+        Pl.late_block = P.rb_collect;
+        hipLaunchKernelGGL((collect_kernel<NOISE, DR, PHYS, SPEC>), dim3((P.N + STEP_BLOCK - 1) / STEP_BLOCK),
+                           dim3(STEP_BLOCK), 0, s, Pl, io, pio);
         return hipGetLastError();
     }
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
-    // envs are processed in slices that fit one residency round (blocks resident at once =
-    // CUs x blocks per CU): a slice's blocks run all K steps together, so no block waits K steps
-    // for a free slot.  Slices run one after the other on the stream.
-    static int round_blocks = -1;
-    if (round_blocks < 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_kernel<NOISE, DR, PHYS, SPEC, CF2_STEP_BLOCK>,
-                                                             CF2_STEP_BLOCK, 0);
-        if (e != hipSuccess) return e;
-        round_blocks = cus * (per_cu > 0 ? per_cu : 1);
-    }
-    // small N: 64 envs per block, the other waves help with the resets (as launch_step_t)
-    const uint32_t epb = P.N <= 32768u ? 64u : (uint32_t)CF2_STEP_BLOCK;
+    // envs are processed in slices that fit one residency round (P.rb_roll blocks resident at
+    // once): a slice's blocks run all K steps together, so no block waits K steps for a free slot.
+    // Slices run one after the other on the stream.  Small N: 64 envs per block, the other waves
+    // help with the resets (as launch_step_t).
+    const uint32_t epb = P.N <= SMALL_N_MAX ? 64u : STEP_BLOCK;
     const uint32_t blocks = (P.N + epb - 1) / epb;
-    const uint32_t nslices = (blocks + (uint32_t)round_blocks - 1) / (uint32_t)round_blocks;
+    const uint32_t round_blocks = P.rb_roll > 0 ? P.rb_roll : 1u;
+    const uint32_t nslices = (blocks + round_blocks - 1) / round_blocks;
     const uint32_t per = (blocks + nslices - 1) / nslices;           // blocks per slice (balanced)
     constexpr int OD = NOISE ? 34 : 42;
     for (uint32_t b0 = 0; b0 < blocks; b0 += per) {
@@ -3049,18 +2864,12 @@ static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t 
         if (io.level) ios.level = io.level + e0;
         if (io.final_obs) ios.final_obs = io.final_obs + (size_t)e0 * OD;
         Ps.out_stride = P.N;
-#ifndef CF2_ROLL_SMALL_OLD
         if (epb == 64u)
             hipLaunchKernelGGL((rollout_kernel_small<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(256), 0, s, Ps, ios, K,
                                act_stride);
-#else
-        if (epb == 64u)
-            hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC, 64u>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s, Ps, ios,
-                               K, act_stride);
-#endif
         else
-            hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC, CF2_STEP_BLOCK>), dim3(nb), dim3(CF2_STEP_BLOCK), 0, s,
-                               Ps, ios, K, act_stride);
+            hipLaunchKernelGGL((rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(STEP_BLOCK), 0, s, Ps, ios, K,
+                               act_stride);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -3080,11 +2889,6 @@ static inline bool spec_default_shape(const KParams& P) {
            P.use_motor_dyn;
 }
 
-#ifdef CF2_BENCH_ONLY
-// A/B builds (tools/build_variant.sh): only the bench workload's instance, so a variant compiles
-// in seconds.  Never the shipped library.
-#define CF2_DISPATCH(FN, ...) return FN<true, true, PHYS_BULLET_T, 1>(__VA_ARGS__)
-#else
 #define CF2_DISPATCH(FN, ...)                                                                          \
     do {                                                                                               \
         const int key = (P.noise ? 4 : 0) | (P.dr ? 2 : 0) | (P.phys == PHYS_SIMPLE_T ? 1 : 0);           \
@@ -3115,13 +2919,13 @@ static inline bool spec_default_shape(const KParams& P) {
         default: return FN<true, true, PHYS_SIMPLE_T, 0>(__VA_ARGS__);                                 \
         }                                                                                              \
     } while (0)
-#endif
 
 #ifdef CF2_TIMING
 extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_cf2_timing), &dev, sizeof(dev));
 }
 #endif
+hipError_t query_occupancy(KParams& P) { CF2_DISPATCH(occupancy_t, P); }
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
 hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
     CF2_DISPATCH(launch_rollout_t, P, io, K, act_stride, s);

@@ -68,12 +68,6 @@ __device__ float w_l3(const float* __restrict__ W, int n, int in) {
     return n == 4 ? W[L::V_W3 + in - 64] : 0.0f;
 }
 
-#ifndef CF2_POLICY_L3F32
-#define CF2_POLICY_L3F32 0
-#endif
-#ifndef CF2_POLICY_SLOT1
-#define CF2_POLICY_SLOT1 0     // measured 35.0 vs 34.2 us at 262 144 rows: the kernel is VALU-, not MFMA-bound
-#endif
 // Packed block layout (floats).  fp32 fragments: 64 floats (lane l: A[16nt + (l&15)][k slot l>>4]).
 // bf16 fragments: 512 floats = hi[64 lanes][8 bf16] then lo[64 lanes][8 bf16] (lane l: k slots
 // 8(l>>4) .. 8(l>>4)+7).  Layer 1 in bf16x3 mode: D/32 bf16 blocks + fp32 k-steps for the rest.
@@ -83,21 +77,20 @@ struct Packed {
     static constexpr int KB1 = BF ? D / 32 : 0;                          // bf16 k-blocks of layer 1
     static constexpr int K1R = 32 * KB1;                                 // first input past them
     static constexpr int R1 = D - K1R;                                   // layer-1 inputs left over
-    // bf16x3 with <= 2 left-over inputs (D = 34): their three split products hi*hi, lo_x*hi_w,
-    // hi_x*lo_w share ONE bf16 MFMA per n-tile (k slots 0..3 R1-1 of lane group 0; a hi-only
-    // fragment, FS floats) instead of fp32 k-steps (16 against 32 cycles per n-tile)
-    static constexpr bool SL = BF && R1 > 0 && 3 * R1 <= 8 && CF2_POLICY_SLOT1;
-    static constexpr int KS1 = SL ? 0 : (BF ? (R1 + 3) / 4 : (D + 3) / 4);   // fp32 k-steps of layer 1
+    // the left-over inputs (D = 34: 2) run as fp32 k-steps.  Measured against one slot-packed bf16
+    // MFMA per n-tile for their three split products: 34.2 vs 35.0 us at 262 144 rows (the kernel
+    // is bound by vector issue, not by the matrix pipe)
+    static constexpr int KS1 = BF ? (R1 + 3) / 4 : (D + 3) / 4;             // fp32 k-steps of layer 1
     static constexpr int KSP = ksteps(50), KSV = ksteps(64);
-    static constexpr int FB = 512, FF = 64, FS = 256;
-    static constexpr int O_L1B = 0, O_L1F = O_L1B + KB1 * 8 * FB, O_L2P = O_L1F + KS1 * 8 * FF + (SL ? 8 * FS : 0);
+    static constexpr int FB = 512, FF = 64;
+    static constexpr int O_L1B = 0, O_L1F = O_L1B + KB1 * 8 * FB, O_L2P = O_L1F + KS1 * 8 * FF;
     static constexpr int N_L2 = BF ? 2 * 4 * FB : 0;
     static constexpr int O_L2V = O_L2P + (BF ? N_L2 : KSP * 4 * FF);
     static constexpr int O_L3 = O_L2V + (BF ? N_L2 : KSV * 4 * FF);
-    // layer 3 (5 outputs) on fp32 k-steps also in bf16x3 mode (CF2_POLICY_L3F32): its inputs need
-    // no hi/lo split then (-97 VALU per chunk), for 30 fp32 MFMAs instead of 12 bf16 ones; measured
+    // layer 3 (5 outputs) on bf16 k-blocks in bf16x3 mode.  On fp32 k-steps its inputs would need
+    // no hi/lo split (-97 VALU per chunk), for 30 fp32 MFMAs instead of 12 bf16 ones: measured
     // 38.7 vs 34.1 us, so the matrix pipe is as close to the limit as the VALU
-    static constexpr bool L3F = !BF || CF2_POLICY_L3F32;
+    static constexpr bool L3F = !BF;
     static constexpr int O_BIAS = O_L3 + (L3F ? (KSP + KSV) * FF : 4 * FB);
     static constexpr int B_L1 = 0, B_L2P = 128, B_L2V = 192, B_L3 = 256, NB = 272;   // neuron-ordered biases
     static constexpr int O_LOGSTD = O_BIAS + NB, O_MEAN = O_LOGSTD + 4, O_SCALE = O_MEAN + (D + 3) / 4 * 4;
@@ -106,13 +99,10 @@ struct Packed {
 
 // bf16x3 mode packs the v network's layer-1 and layer-2 weights and biases multiplied by
 // TANH_PRESCALE = -2 log2(e), so that its tanh needs no scaling (tanh_prescaled below)
-#ifndef CF2_POLICY_TANH_PRESCALE
-#define CF2_POLICY_TANH_PRESCALE 1
-#endif
 constexpr float TANH_PRESCALE = -2.8853900817779268f;
 template <int PREC>
 __device__ __forceinline__ float v_prescale(bool v_pre_tanh) {
-    return (PREC == CF2_POLICY_BF16X3 && CF2_POLICY_TANH_PRESCALE && v_pre_tanh) ? TANH_PRESCALE : 1.0f;
+    return (PREC == CF2_POLICY_BF16X3 && v_pre_tanh) ? TANH_PRESCALE : 1.0f;
 }
 
 template <int D>
@@ -151,14 +141,10 @@ __device__ __forceinline__ f4v mfma3(const bf8v& ah, const bf8v& al, const bf8v&
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
 }
 // x -> (hi, lo) bf16 operands
-#ifndef CF2_POLICY_PAIRCVT
-#define CF2_POLICY_PAIRCVT 1
-#endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void split8(const float (&x)[8], bf8v& hi, bf8v& lo) {
-#if CF2_POLICY_PAIRCVT
     // two values per v_cvt_pk_bf16_f32: hi pair, its two fp32 values by shift / mask, the two
     // remainders, lo pair (6 VALU per pair; per-value conversions cost ~8)
     u4v h, o;
@@ -172,13 +158,6 @@ __device__ __forceinline__ void split8(const float (&x)[8], bf8v& hi, bf8v& lo) 
     }
     hi = __builtin_bit_cast(bf8v, h);
     lo = __builtin_bit_cast(bf8v, o);
-#else
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        hi[j] = (__bf16)x[j];
-        lo[j] = (__bf16)(x[j] - (float)hi[j]);
-    }
-#endif
 }
 // B operand of k-block (t0, t0 + 1) from two C-layout tiles
 __device__ __forceinline__ void split_tiles(const f4v& a, const f4v& b, bf8v& hi, bf8v& lo) {
@@ -210,7 +189,7 @@ __device__ __forceinline__ float relu(float x) {
 }
 template <int PREC>
 __device__ __forceinline__ float tanh_act(float x) {
-    if constexpr (PREC == CF2_POLICY_BF16X3 && CF2_POLICY_TANH_PRESCALE) return tanh_prescaled(x);
+    if constexpr (PREC == CF2_POLICY_BF16X3) return tanh_prescaled(x);
     else return tanh_fast(x);
 }
 
@@ -219,18 +198,10 @@ enum : uint32_t { TAG_POLICY = 3 };
 // 81.4 -> 76.5 us at 262 144 rows against 2 row tiles per chunk in 4-wave blocks at 2 waves per
 // SIMD (each fragment read then feeds one MFMA instead of two, but twice as many waves hide the
 // LDS and MFMA latencies; 3 waves/SIMD in 6-wave blocks: 50.1 us; 16-wave blocks: 40.2 us)
-#ifndef CF2_POLICY_RT
-#define CF2_POLICY_RT 1          // row tiles (16 rows each) per wave chunk: each fragment read feeds RT MFMAs
-#endif
-#ifndef CF2_POLICY_BLOCK
-#define CF2_POLICY_BLOCK 512     // threads per block (one staged copy of the fragments per block)
-#endif
-#ifndef CF2_POLICY_WAVES
-#define CF2_POLICY_WAVES 4       // waves per SIMD the register budget is sized for
-#endif
-constexpr int RT = CF2_POLICY_RT;
+constexpr int RT = 1;             // row tiles (16 rows each) per wave chunk: each fragment read feeds RT MFMAs
 constexpr int CHUNK = 16 * RT;
-constexpr int PB = CF2_POLICY_BLOCK, PW = PB / 64;
+constexpr int PB = 512, PW = PB / 64;   // threads per block (one staged copy of the fragments per block)
+constexpr int POLICY_WAVES = 4;   // waves per SIMD the register budget is sized for
 
 // The observations of one chunk, raw fp32: per row tile the bf16 k-blocks' 8 consecutive inputs
 // of this lane's group (x8) and the fp32 k-steps' single inputs (x1).  Loads are unconditional
@@ -242,7 +213,6 @@ struct ObsRegs {
     using P = Packed<D, PREC>;
     float x8[R][P::KB1 > 0 ? P::KB1 : 1][8];
     float x1[R][P::KS1 > 0 ? P::KS1 : 1];
-    float xr[R][P::SL ? P::R1 : 1];
 };
 template <int D, int PREC>
 __device__ __forceinline__ void load_obs(const float* __restrict__ obs, uint32_t n, uint32_t r0, int l,
@@ -263,9 +233,6 @@ __device__ __forceinline__ void load_obs(const float* __restrict__ obs, uint32_t
 #pragma unroll
         for (int ks = 0; ks < P::KS1; ++ks)
             X.x1[rt][ks] = src[__builtin_elementwise_min(P::K1R + 4 * ks + (l >> 4), D - 1)];
-        if constexpr (P::SL)
-#pragma unroll
-            for (int r = 0; r < P::R1; ++r) X.xr[rt][r] = src[P::K1R + r];
     }
 }
 
@@ -279,7 +246,6 @@ struct PolicyLane {     // per-lane constants, hoisted out of the chunk loop
     using P = Packed<D, PREC>;
     float ls[4], sd[4];
     float mean1[P::KS1 > 0 ? P::KS1 : 1], scale1[P::KS1 > 0 ? P::KS1 : 1];
-    float meanr[P::SL ? P::R1 : 1], scaler[P::SL ? P::R1 : 1];
 };
 template <int D, int PREC>
 __device__ __forceinline__ void policy_lane_init(const float* sb, int g, PolicyLane<D, PREC>& C) {
@@ -290,12 +256,6 @@ __device__ __forceinline__ void policy_lane_init(const float* sb, int g, PolicyL
         C.ls[k] = sb[T_LOGSTD + k];
         C.sd[k] = __builtin_amdgcn_exp2f(1.4426950408889634f * C.ls[k]);
     }
-    if constexpr (P::SL)
-#pragma unroll
-        for (int r = 0; r < P::R1; ++r) {
-            C.meanr[r] = sb[T_MEAN + P::K1R + r];
-            C.scaler[r] = sb[T_SCALE + P::K1R + r];
-        }
 #pragma unroll
     for (int ks = 0; ks < P::KS1; ++ks) {
         const int k = __builtin_elementwise_min(P::K1R + 4 * ks + g, D - 1);
@@ -329,9 +289,6 @@ __device__ __forceinline__ void policy_standardize(const float* sb, int g, const
             for (int j = 0; j < 8; ++j) Xc.x8[rt][kb][j] = (Xc.x8[rt][kb][j] - mean8[kb][j]) * scale8[kb][j];
 #pragma unroll
         for (int ks = 0; ks < P::KS1; ++ks) Xc.x1[rt][ks] = (Xc.x1[rt][ks] - C.mean1[ks]) * C.scale1[ks];
-        if constexpr (P::SL)
-#pragma unroll
-            for (int r = 0; r < P::R1; ++r) Xc.xr[rt][r] = (Xc.xr[rt][r] - C.meanr[r]) * C.scaler[r];
     }
 }
 
@@ -345,8 +302,6 @@ __device__ __forceinline__ void policy_layers(const float* sw, const float* sb, 
     constexpr bool PI = MODE == 0, BF = P::BF;
     constexpr int T_BIAS = 0;
     const int g = l >> 4;
-    const uint32_t g0 = g == 0 ? 0xffffffffu : 0u;      // slot-mode B operand lives in lane group 0
-    (void)g0;
     // ---- layer 1: [pi | v] 128 neurons (8 n-tiles); MODE 1 runs only the v half
     constexpr int NT0 = PI ? 0 : 4;
     f4v h1[8][RT];
@@ -377,39 +332,6 @@ __device__ __forceinline__ void policy_layers(const float* sw, const float* sb, 
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = mfma4(a, Xc.x1[rt][ks], h1[nt][rt]);
         }
-    if constexpr (P::SL) {
-        bf8v bs[RT];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            uint16_t hb[P::R1], lb[P::R1];
-#pragma unroll
-            for (int r = 0; r < P::R1; ++r) {
-                const __bf16 h = (__bf16)Xc.xr[rt][r];
-                hb[r] = __builtin_bit_cast(uint16_t, h);
-                lb[r] = __builtin_bit_cast(uint16_t, (__bf16)(Xc.xr[rt][r] - (float)h));
-            }
-            u4v wds;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t wq = 0;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int sl = 2 * q + e;
-                    const uint32_t v = sl < P::R1 ? hb[sl] : sl < 2 * P::R1 ? lb[sl - P::R1]
-                                     : sl < 3 * P::R1 ? hb[sl - 2 * P::R1] : 0u;
-                    wq |= v << (16 * e);
-                }
-                wds[q] = wq & g0;
-            }
-            bs[rt] = __builtin_bit_cast(bf8v, wds);
-        }
-#pragma unroll
-        for (int nt = NT0; nt < 8; ++nt) {
-            const bf8v a = __builtin_bit_cast(bf8v, *reinterpret_cast<const float4*>(sw + P::O_L1F + nt * P::FS + 4 * l));
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) h1[nt][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bs[rt], h1[nt][rt], 0, 0, 0);
-        }
-    }
 #pragma unroll
     for (int nt = NT0; nt < 8; ++nt)
 #pragma unroll

@@ -26,7 +26,7 @@
 // registers, with no LDS round trip and no cross-lane move.  Biases initialise the accumulators.
 //
 // Work split: persistent blocks of 8 waves, 2 per CU (4 waves per SIMD); each wave runs chunks of
-// CF2_POLICY_RT row tiles of 16 rows and prefetches the next chunk's observations while the
+// RT row tiles of 16 rows and prefetches the next chunk's observations while the
 // current one runs.  The packed block (A-operand fragments, lane-ordered:
 // conflict-free ds_read_b32 / ds_read_b128) is staged into LDS once per block.
 //
@@ -61,18 +61,6 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, 
     };
     if (k < P::O_L1F) {
         v = bfword(1, k - P::O_L1B, 8);
-    } else if (k < P::O_L2P && P::SL) {
-        // slot s of lane group 0: s < R1 hi(w), s < 2 R1 hi(w) (times lo(x)), s < 3 R1 lo(w)
-        const int r = k - P::O_L1F, nt = r / P::FS, w = r % P::FS, l = w / 4, pr = w % 4;
-        uint32_t bits = 0;
-        for (int e = 0; e < 2; ++e) {
-            const int sl = 2 * pr + e;
-            if ((l >> 4) != 0 || sl >= 3 * P::R1) continue;
-            const float x = w_l1<D>(W, 16 * nt + (l & 15), P::K1R + sl % P::R1) * v_prescale<PREC>(nt >= 4);
-            const float hi = (float)(__bf16)x;
-            bits |= (sl < 2 * P::R1 ? bf16_bits(x) : bf16_bits(x - hi)) << (16 * e);
-        }
-        v = __uint_as_float(bits);
     } else if (k < P::O_L2P) {
         const int r = k - P::O_L1F, f = r / 64, l = r % 64, ks = f / 8, nt = f % 8;
         v = w_l1<D>(W, 16 * nt + (l & 15), P::K1R + 4 * ks + (l >> 4)) * v_prescale<PREC>(nt >= 4);
@@ -116,7 +104,7 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ W, 
 
 // mode: 0 = policy (mu, sample, logp) + value of every row; 1 = value only, rows with mask[r] != 0
 template <int D, int PREC, int MODE>
-__global__ void __launch_bounds__(PB, CF2_POLICY_WAVES) policy_kernel(const float* __restrict__ Wp, uint32_t n,
+__global__ void __launch_bounds__(PB, POLICY_WAVES) policy_kernel(const float* __restrict__ Wp, uint32_t n,
                                                                       const float* __restrict__ obs, uint32_t key0,
                                                                       uint32_t key1, uint32_t counter,
                                                                       uint32_t row_offset, int sample,
@@ -212,11 +200,8 @@ static int policy_grid(uint32_t n) {
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t want = (n + PW * CHUNK - 1) / (PW * CHUNK);
     // resident blocks per CU: LDS (~58-62 KB of fragments per block) and the wave budget
-    const uint32_t by_waves = (uint32_t)(4 * CF2_POLICY_WAVES / PW);
-#ifndef CF2_POLICY_PER_CU
-#define CF2_POLICY_PER_CU 2u     // resident blocks per CU the persistent grid is sized for
-#endif
-    const uint32_t cap_cu = CF2_POLICY_PER_CU;
+    const uint32_t by_waves = (uint32_t)(4 * POLICY_WAVES / PW);
+    const uint32_t cap_cu = 2u;      // resident blocks per CU the persistent grid is sized for (1: slower)
     const uint32_t per_cu = by_waves < cap_cu ? (by_waves ? by_waves : 1u) : cap_cu;
     const uint32_t cap = per_cu * (uint32_t)cus;
     return (int)(want < cap ? want : cap);

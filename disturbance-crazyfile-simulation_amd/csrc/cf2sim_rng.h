@@ -8,42 +8,22 @@ namespace cf2 {
 
 struct U4 { uint32_t x, y, z, w; };
 
-// Round keys k + r * (W0, W1).  Wave-uniform, so they live in SGPRs (an SGPR operand of v_xor
-// costs nothing).  Two forms, chosen per kernel:
-//   Keys      all 20 round keys built once per kernel (the env-step kernels).  When the kernel's
-//             SGPR budget is exhausted some are spilled to VGPR lanes (a v_readlane per use);
-//             -DCF2_VGPR_KEYS holds them in VGPRs instead.
-//   KeysBase  only the two base words; each philox() call re-derives its round keys from an
-//             opaque copy (2 SALU per round).  Removes the key spills (SGPR spill sites 72 -> 32
-//             in the step kernel), but the SALU adds sit in the dependent Philox chain: measured
-//             +0.9 us at 262 144 envs and +2k cycles on a lone env wave's physics at 4096 envs;
-//             in the register-bound fused rollout it removes the VGPR spills and is still slower
-//             (rollout_kernel, CF2_ROLL_BASE_KEYS).  Kept for A/B builds.
+// Round keys k + r * (W0, W1), all 20 built once per kernel.  Wave-uniform, so they live in SGPRs
+// (an SGPR operand of v_xor costs nothing); when a kernel's SGPR budget is exhausted some are
+// spilled to VGPR lanes (a v_readlane per use).  Re-deriving them per call instead (2 SALU per
+// round) removed those spills but was slower everywhere it was measured (+0.9 us at 262 144 envs,
+// +2 us per env-step in the fused rollout): the SALU adds sit in the dependent Philox chain.
 struct Keys { uint32_t k0[10], k1[10]; };
 __device__ __forceinline__ Keys make_keys(uint32_t k0, uint32_t k1) {
     Keys K;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t a = k0 + (uint32_t)r * 0x9E3779B9u, b = k1 + (uint32_t)r * 0xBB67AE85u;
-#ifdef CF2_VGPR_KEYS
-        asm volatile("v_mov_b32 %0, %1" : "=v"(K.k0[r]) : "s"(a));
-        asm volatile("v_mov_b32 %0, %1" : "=v"(K.k1[r]) : "s"(b));
-#else
-        K.k0[r] = a; K.k1[r] = b;
-#endif
+        K.k0[r] = k0 + (uint32_t)r * 0x9E3779B9u;
+        K.k1[r] = k1 + (uint32_t)r * 0xBB67AE85u;
     }
     return K;
 }
-struct KeysBase { uint32_t k0, k1; };
-__device__ __forceinline__ KeysBase make_keys_base(uint32_t k0, uint32_t k1) { return KeysBase{k0, k1}; }
-__device__ __forceinline__ Keys make_keys_as(const Keys*, uint32_t k0, uint32_t k1) { return make_keys(k0, k1); }
-__device__ __forceinline__ KeysBase make_keys_as(const KeysBase*, uint32_t k0, uint32_t k1) {
-    return make_keys_base(k0, k1);
-}
 
-#ifndef CF2_PHILOX_ROUNDS
-#define CF2_PHILOX_ROUNDS 10   // diagnostic knob only: the stream (and parity) is defined for 10
-#endif
 __device__ __forceinline__ void philox_round(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t ka,
                                              uint32_t kb) {
     // one v_mad_u64_u32 per product yields both halves
@@ -56,16 +36,7 @@ __device__ __forceinline__ void philox_round(uint32_t& c0, uint32_t& c1, uint32_
 }
 __device__ __forceinline__ U4 philox(const Keys& K, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
 #pragma unroll
-    for (int r = 0; r < CF2_PHILOX_ROUNDS; ++r) philox_round(c0, c1, c2, c3, K.k0[r], K.k1[r]);
-    return U4{c0, c1, c2, c3};
-}
-__device__ __forceinline__ U4 philox(const KeysBase& K, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    // opaque per call: the round keys are not common subexpressions of different philox() calls
-    uint32_t b0 = K.k0, b1 = K.k1;
-    asm volatile("" : "+s"(b0), "+s"(b1));
-#pragma unroll
-    for (int r = 0; r < CF2_PHILOX_ROUNDS; ++r)
-        philox_round(c0, c1, c2, c3, b0 + (uint32_t)r * 0x9E3779B9u, b1 + (uint32_t)r * 0xBB67AE85u);
+    for (int r = 0; r < 10; ++r) philox_round(c0, c1, c2, c3, K.k0[r], K.k1[r]);
     return U4{c0, c1, c2, c3};
 }
 

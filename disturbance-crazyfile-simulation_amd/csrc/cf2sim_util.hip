@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/cf2sim.h"
+#include "cf2sim_internal.h"
 
 namespace cf2 {
 
@@ -57,5 +58,6 @@ extern "C" int cf2_hbm_probe(void* dst_dev, const void* src_dev, size_t bytes, i
     auto* d = static_cast<cf2::u32x4v*>(dst_dev);
     if (mode == 0) hipLaunchKernelGGL(cf2::hbm_copy_kernel, grid, block, 0, (hipStream_t)stream, s, d, bytes / 16u);
     else hipLaunchKernelGGL(cf2::hbm_read_kernel, grid, block, 0, (hipStream_t)stream, s, d, bytes / 16u);
-    return hipGetLastError() == hipSuccess ? CF2_OK : CF2_ERR_HIP;
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CF2_OK : cf2::hip_fail(e);
 }

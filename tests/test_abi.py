@@ -88,3 +88,30 @@ def test_registry_covers_reference_hover_ids():
     for i in OUT_OF_SCOPE_IDS:
         with pytest.raises(NotImplementedError):
             spec_for_id(i)
+
+
+def test_build_rejects_unknown_defines():
+    """cf2sim.build refuses -DCF2_* defines the sources do not know (a removed A/B knob or a typo
+    would otherwise compile silently into a library that differs from the tested one)."""
+    import pytest
+    from cf2sim.build import check_defines, build_native
+    check_defines(["-DCF2_TIMING", "-O2", "-DNDEBUG"])
+    for bad in (["-DCF2_AB_NO_RESET"], ["-DCF2_SMALL_OLD=1"], ["-DCF2_TIMNG"]):
+        with pytest.raises(ValueError):
+            check_defines(bad)
+        with pytest.raises(ValueError):
+            build_native(extra_flags=bad, out="/tmp/never_built.so")
+    with pytest.raises(ValueError):           # extra flags never overwrite the in-tree library
+        build_native(extra_flags=["-DCF2_TIMING"])
+
+
+def test_kernel_sources_hold_no_ab_branches():
+    """The only preprocessor conditional in the native sources is CF2_TIMING."""
+    import glob
+    import re
+    src = os.path.join(ROOT, "disturbance-crazyfile-simulation_amd", "csrc")
+    for f in glob.glob(os.path.join(src, "*")):
+        for line in open(f):
+            m = re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b(.*)", line)
+            if m:
+                assert "CF2_TIMING" in m.group(2), f"{os.path.basename(f)}: {line.strip()}"

@@ -125,3 +125,34 @@ def test_collect_step_rejects_bad_args(gpu):
                                 v.data_ptr(), lp.data_ptr(), e.stream)
     assert st != 0 and st != _native.CF2_ERR_UNSUPPORTED, "an obs_dim that is not the env's is an error"
     e.close()
+
+
+@pytest.mark.parametrize("env_id,n,kw", [
+    ("DroneHoverBulletFreeEnvWithGust-v0", 65536, {}),                                    # halves at small N
+    ("DroneHoverBulletFreeEnvWithoutAdversary-v0", 8192, dict(max_episode_steps=9)),
+])
+def test_collect_is_split_invariant(gpu, env_id, n, kw):
+    """A collect over two contexts holding global env ids [0, n/2) and [n/2, n) equals one collect
+    over all n envs, env for env (physics keyed by the global env id through env_id_offset, the
+    policy's sampling noise through row_offset = env_id_offset): rank-count invariance of f3."""
+    from cf2sim.rollout import FusedActorCritic, MLPActorCritic, collect
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    torch.manual_seed(5)
+    ac = MLPActorCritic(obs_dim=34).cuda()
+    with torch.no_grad():
+        ac.obs_oms.mean.uniform_(-0.2, 0.2)
+        ac.obs_oms.std.uniform_(0.5, 2.0)
+    h = n // 2
+    whole = BatchedCrazyflieEnv(env_id, n, seed=3, want_final_obs=True, **kw)
+    parts = [BatchedCrazyflieEnv(env_id, h, seed=3, env_id_offset=k * h, want_final_obs=True, **kw) for k in range(2)]
+    rw = collect(whole, FusedActorCritic(ac, seed=9), 16)
+    rp = [collect(e, FusedActorCritic(ac, seed=9), 16) for e in parts]
+    torch.cuda.synchronize()
+    assert rw.done.any()
+    assert whole.last_collect_fused and all(e.last_collect_fused for e in parts)
+    for f in ("obs", "act", "rew", "val", "logp", "done", "trunc", "adv", "ret", "last_obs", "last_val", "trunc_val"):
+        a = getattr(rw, f)
+        b = torch.cat([getattr(r, f) for r in rp], dim=1 if a.dim() >= 2 and a.shape[0] == 16 else 0)
+        assert torch.equal(a, b), f"{f}: max |diff| {(a.float() - b.float()).abs().max().item()}"
+    for e in [whole] + parts:
+        e.close()

@@ -145,3 +145,47 @@ def test_hbm_probe(gpu):
     assert lib.cf2_hbm_probe(dst.data_ptr() + 4, src.data_ptr(), 16, 0, s) != 0        # misaligned
     assert lib.cf2_hbm_probe(None, src.data_ptr(), 16, 0, s) != 0
     assert lib.cf2_hbm_probe(dst.data_ptr(), src.data_ptr(), 16, 2, s) != 0            # no such mode
+
+
+def test_step_output_buffers_and_copy(gpu):
+    """step() returns the env's own output buffers (documented: the next step overwrites them);
+    step(copy=True) / copy_outputs=True return fresh tensors that later steps leave alone."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    n = 256
+    env = BatchedCrazyflieEnv(ENV, n, seed=2)
+    env.reset()
+    a = torch.rand(n, 4, device=gpu) * 0.6 - 0.1
+    o1, r1, d1, i1 = env.step(a)
+    o2, r2, d2, i2 = env.step(a)
+    assert o1 is o2 and r1 is r2 and d1 is d2 and i1["cost"] is i2["cost"]      # persistent buffers
+    c1 = env.step(a, copy=True)
+    keep = c1[0].clone()
+    c2 = env.step(a, copy=True)
+    assert c1[0] is not c2[0] and c1[0] is not env.obs
+    assert torch.equal(c1[0], keep), "a copied result must not change with the next step"
+    assert not torch.equal(c1[0], c2[0]), "two consecutive steps give different observations"
+    env2 = BatchedCrazyflieEnv(ENV, n, seed=2, copy_outputs=True)
+    env2.reset()
+    x1, x2 = env2.step(a), env2.step(a)
+    assert x1[0] is not x2[0] and x1[3]["cost"] is not x2[3]["cost"]
+    env.close()
+    env2.close()
+
+
+def test_masked_reset_after_raw_obs_pointer_is_refused(gpu):
+    """after a step into a raw obs pointer, a masked reset cannot produce the other envs'
+    observations; it raises instead of returning stale rows."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    n = 128
+    env = BatchedCrazyflieEnv(ENV, n)
+    env.reset()
+    a = torch.zeros(n, 4, device=gpu)
+    raw = torch.empty(n, env.obs_dim, device=gpu)
+    env.step_raw(a.data_ptr(), obs_ptr=raw.data_ptr())
+    m = torch.zeros(n, dtype=torch.uint8, device=gpu)
+    m[:3] = 1
+    with pytest.raises(ValueError):
+        env.reset(m)
+    env.reset()              # a full reset is fine
+    env.reset(m)             # and masked resets after it
+    env.close()

@@ -1,5 +1,5 @@
 # Same-box A/B of two full library builds on the rollout caller (bf16x3 and fp32 policy) and the
-# step() bench at action rings 8 and 64.  usage: bash tools/ab_rollout_nt.sh LIB_A LIB_B (full builds: CF2_FULL=1 tools/build_variant.sh)
+# step() bench at action rings 8 and 64.  usage: bash tools/ab_rollout_nt.sh LIB_A LIB_B (builds: tools/build_variant.sh)
 set -o pipefail
 for rep in 1 2; do for lib in "$@"; do
   for p in bf16x3 fp32; do
