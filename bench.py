@@ -21,8 +21,12 @@ workload is BASELINE's metric config: 262 144 envs over the whole job (--global-
 rank stepping its contiguous global-id shard (32 768 envs per GPU at N = 8; "scaling":
 "strong").  Envs are independent, so the physics needs no collective; at N > 1 the reported line
 is the north-star variant with the per-step RCCL all-gather of the observation slab over xGMI
-(--gather-obs, default on at N > 1), pipelined with the next env-step.  The same shards without
-the gather ("no_gather") and 262 144 envs per GPU ("weak_scaling") are extra keys of the line.
+(--gather-obs, default on at N > 1), pipelined with the next env-step.  By default the exchange
+moves deltas (--gather-mode delta, cf2sim.dist: o_k of every env, a reset bitmap and the reset
+rows' first halves; every rank rebuilds the full [262144, 34] slab bit-identically from the
+previous one and the actions, which every rank holds), 2.36x fewer xGMI bytes than the full rows
+(--gather-mode full).  The same shards without the gather ("no_gather") and 262 144 envs per GPU
+("weak_scaling") are extra keys of the line.
 """
 from __future__ import annotations
 
@@ -197,6 +201,8 @@ def parse_args(argv=None):
     ap.add_argument("--gather-obs", dest="gather_obs", action="store_true", default=None,
                     help="per-step RCCL all-gather of the obs slab (default: on at N > 1)")
     ap.add_argument("--no-gather-obs", dest="gather_obs", action="store_false")
+    ap.add_argument("--gather-mode", choices=("delta", "full"), default="delta",
+                    help="delta: o_k + reset side slab, every rank rebuilds the rows (default); full: the rows")
     ap.add_argument("--weak-envs", type=int, default=262144,
                     help="N > 1: the weak_scaling key times this many envs per rank; 0 = skip")
     ap.add_argument("--weak-steps", type=int, default=1000)
@@ -218,6 +224,9 @@ def parse_args(argv=None):
     ap.add_argument("--env-kw", default="{}", help="JSON env kwargs (ablations), e.g. '{\"observation_noise\": 0}'")
     ap.add_argument("--collect-steps", type=int, default=32,
                     help="steps per collect of the f3 line (rollout.collect, fused env + policy; 0 = skip)")
+    ap.add_argument("--exchange-probe", type=int, default=1,
+                    help="N = 1: time the delta obs exchange's pack (one rank of the 8-GPU shape) and unpack "
+                         "(all 262 144 rows) kernels on this GPU; 0 = skip")
     ap.add_argument("--rollout-k", type=int, default=32,
                     help="also time the fused K-step rollout (cf2_rollout, random actions) on 1 GPU; 0 = skip")
     return ap.parse_args(argv)
@@ -312,26 +321,48 @@ def main(argv=None):
     env.reset()
     ring = args.action_ring
     g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    acts = torch.rand(ring, n, 4, device=dev, generator=g) * 2 - 1
+    g.manual_seed(1234)
+    # the job's actions, identical on every rank (the delta exchange rebuilds every env's history
+    # rows from them, as a policy that computed them would); a rank steps its rows [off, off + n)
+    acts_g = torch.rand(ring, global_envs, 4, device=dev, generator=g) * 2 - 1
+    acts = acts_g[:, off:off + n]
     stream = torch.cuda.current_stream()
 
+    from cf2sim.dist import delta_supported
     pipe = None
     gather_mode = None
+    delta = gather and args.gather_mode == "delta"
+    if gather and args.graph:
+        raise SystemExit("bench.py: --graph is for the env-step alone (no --gather-obs)")
+    if delta and (len(set(shards)) != 1 or not delta_supported(env.cfg) or args.envs_per_gpu):
+        delta = False
     if gather:
         if len(set(shards)) == 1:
-            pipe = PipelinedObsGather(n, env.obs_dim, dev)
-            gather_mode = "pipelined all_gather_into_tensor (2 obs buffers, side stream)"
+            pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta)
+            if delta:
+                pipe.start(env.obs)
+                gather_mode = (f"pipelined delta all_gather_into_tensor (o_k + reset bitmap + side slab of "
+                               f"{pipe.cap} resets per rank, rows rebuilt on every rank; side stream)")
+            else:
+                gather_mode = "pipelined all_gather_into_tensor of the rows (2 obs buffers, side stream)"
         else:
             gather_mode = "ragged shards: synchronous padded all_gather"
+    kk = [0]                               # env-steps taken (the delta exchange needs a_{k-1})
 
     def one_step(k, with_gather):
+        j = kk[0]
+        kk[0] += 1
+        a = acts[j % ring]
         if with_gather and pipe is not None:
             buf = pipe.buffer()
-            env.step_raw(acts[k % ring].data_ptr(), obs_ptr=buf.data_ptr())
-            pipe.publish()
+            if delta:
+                env.step_raw(a.data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=pipe.done_buffer().data_ptr())
+                pipe.publish(acts_g[j % ring], acts_g[(j - 1) % ring])
+            else:
+                env.step_raw(a.data_ptr(), obs_ptr=buf.data_ptr())
+                pipe.publish()
         else:
-            env.step_raw(acts[k % ring].data_ptr())
+            env.step_raw(a.data_ptr())
             if with_gather:
                 env.gather_observations()
 
@@ -496,6 +527,47 @@ def main(argv=None):
                      "hbm_frac": bytes_per_env_step(env) * n / (sus * 1e-6) / 1e9 / HBM_PEAK_GBS}
         del sacts
 
+    exchange = None
+    if world == 1 and args.exchange_probe and n == METRIC_GLOBAL_ENVS and delta_supported(env.cfg):
+        # the delta obs exchange of the 8-GPU shape on one GPU: 8 shards of this step's real rows
+        # and done flags packed as the ranks would (cf2_obs_pack, 32 768 rows each), then every
+        # rank's rebuild of all 262 144 rows (cf2_obs_unpack), timed with HIP events on this stream
+        from cf2sim.dist import default_cap, pack_obs, packed_words, unpack_obs
+        W8, n8, ol = 8, n // 8, env.obs_dim // 2 - 4
+        cap = default_cap(n8)
+        words = packed_words(n8, ol, cap)
+        send = torch.zeros(W8 * words, dtype=torch.int32, device=dev)
+        rows, dn = env.obs.clone(), env.done.clone()
+        prev = rows.clone()
+        cur = torch.empty_like(rows)
+        age = torch.full((n,), 3, dtype=torch.uint8, device=dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        reps = 20
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        for _ in range(reps):
+            for r in range(W8):
+                send[r * words:r * words + 1].zero_()
+                pack_obs(rows[r * n8:(r + 1) * n8], dn[r * n8:(r + 1) * n8], cap, out=send[r * words:(r + 1) * words])
+        ev[1].record(stream)
+        for _ in range(reps):
+            unpack_obs(send, W8, n8, ol, cap, acts_g[1], acts_g[0], age, prev, cur)
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        pack_us = ev[0].elapsed_time(ev[1]) * 1e3 / (reps * W8)
+        unpack_us = ev[1].elapsed_time(ev[2]) * 1e3 / reps
+        full_b, delta_b = n8 * env.obs_dim * 4, words * 4
+        exchange = {"shape": f"8 ranks x {n8} envs", "cap_per_rank": cap, "bytes_per_rank_per_step": delta_b,
+                    "full_rows_bytes_per_rank_per_step": full_b, "reduction": full_b / delta_b,
+                    "link_bound_us_8gpu": delta_b / 153e9 * 1e6, "link_bound_us_8gpu_full_rows": full_b / 153e9 * 1e6,
+                    "pack_us_per_rank": pack_us, "unpack_us_all_rows": unpack_us,
+                    "unpack_algorithmic_bytes": n * (4 * env.obs_dim + 4 * (ol + 4) + 4 * ol + 32 + 2),
+                    "note": "link bound: each GPU receives one packed buffer from each of 7 peers over its 7 xGMI links "
+                            "(~153 GB/s each) in parallel; the unpack (every rank rebuilds all rows from the previous "
+                            "slab) runs on the exchange's side stream, beside the next env-step"}
+        exchange["unpack_GBs"] = exchange["unpack_algorithmic_bytes"] / (unpack_us * 1e-6) / 1e9
+        del send, rows, prev, cur
+
     bytes_per = bytes_per_env_step(env)
     out_of_cache = None
     if world == 1 and args.oc_envs > 0:
@@ -558,8 +630,11 @@ def main(argv=None):
     wset = working_set_bytes(env, ring)
     gather_info = None
     if gather:
-        rx = (global_envs - n) * env.obs_dim * 4          # bytes this rank receives per step
-        gather_info = {"mode": gather_mode, "bytes_in_per_rank_per_step": rx, "total_bytes_per_step": global_envs * env.obs_dim * 4,
+        per_rank = pipe.bytes_per_rank_per_step if pipe is not None else n * env.obs_dim * 4
+        rx = (world - 1) * per_rank                       # bytes this rank receives per step
+        gather_info = {"mode": gather_mode, "bytes_in_per_rank_per_step": rx, "total_bytes_per_step": world * per_rank,
+                       "full_rows_bytes_in_per_rank_per_step": (global_envs - n) * env.obs_dim * 4,
+                       "overflows": pipe.overflows() if pipe is not None else 0,
                        "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
                        "rx_frac_of_xgmi": rx / (elapsed / args.steps) / 1e9 / XGMI_PEAK_GBS}
 
@@ -606,6 +681,7 @@ def main(argv=None):
             "fused_rollout": fused,
             "collect": collect_line,
             "streaming_actions": streaming,
+            "delta_exchange": exchange,
         }
         print(json.dumps(line), flush=True)
     env.close()

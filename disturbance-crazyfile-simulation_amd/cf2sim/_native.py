@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = (
     "cf2_set_ground_effect",
     "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
     "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
-    "cf2_hbm_probe",
+    "cf2_hbm_probe", "cf2_obs_packed_words", "cf2_obs_pack", "cf2_obs_unpack",
 )
 
 
@@ -90,9 +90,13 @@ def load() -> ctypes.CDLL:
     lib.cf2_gae.argtypes = [u32, u32, vp, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp,
                             vp, vp]
     lib.cf2_hbm_probe.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    lib.cf2_obs_packed_words.restype = ctypes.c_size_t
+    lib.cf2_obs_packed_words.argtypes = [u32, u32, u32]
+    lib.cf2_obs_pack.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
+    lib.cf2_obs_unpack.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
-                        "cf2_policy_weights_count", "cf2_policy_packed_count"):
+                        "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_obs_packed_words"):
             getattr(lib, name).restype = ctypes.c_int
     if lib.cf2_config_sizeof() != ctypes.sizeof(CF2Config):
         raise CF2Error(f"cf2_config size mismatch: C {lib.cf2_config_sizeof()} vs Python {ctypes.sizeof(CF2Config)}")

@@ -69,62 +69,290 @@ def run_ranks(plan, timeout: float | None = None) -> int:
     return rc
 
 
+# ---- delta observation exchange (csrc/cf2sim_exchange.hip has the protocol; cf2_obs_pack /
+# cf2_obs_unpack run it on GPU tensors, the torch-op versions below on CPU tensors for the gloo
+# rehearsal of the multi-rank path; both produce the same rows bit for bit) ----
+
+def packed_words(n: int, ol: int, cap: int) -> int:
+    """32-bit words of one rank's packed buffer (cf2_obs_packed_words)."""
+    side = 4 + n * ol + (n + 31) // 32
+    return (side + cap * (ol + 5) + 3) & ~3
+
+
+def default_cap(n: int) -> int:
+    """Side-slab capacity: 7.5 % of the shard.  The bench workload ends 4.1 % of its episodes per
+    env-step in steady state and 5.7 % at the synchronised-start peak (profiles/r02_reset_rate.json);
+    a step that exceeds it marks the rows it could not send (NaN) and counts an overflow."""
+    return min(int(n), max(64, (3 * n + 39) // 40))
+
+
+def delta_supported(cfg) -> bool:
+    """The delta rows rely on the action buffer holding only the step's action after an env-step
+    (aggregate_phy_steps a multiple of buf_size, latency on: the reference's default) and on
+    auto-reset (a finished env's next row is its reset row)."""
+    return bool(cfg.auto_reset) and bool(cfg.use_latency) and int(cfg.aggregate_phy_steps) % int(cfg.buf_size) == 0
+
+
+def _bits_to_mask(words, n):
+    import numpy as np
+    import torch
+    b = words.contiguous().cpu().numpy().view(np.uint8)
+    return torch.from_numpy(np.unpackbits(b, bitorder="little")[:n].astype(bool))
+
+
+def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
+    """One rank's packed buffer (int32 [packed_words]) from its step's obs rows [n, OD] and
+    auto-reset flags [n] (uint8 or bool)."""
+    import numpy as np
+    import torch
+    n, od = obs.shape
+    ol = od // 2 - 4
+    words = packed_words(n, ol, cap)
+    if out is None:
+        out = torch.zeros(words, dtype=torch.int32, device=obs.device)
+    if obs.is_cuda:
+        from . import _native
+        lib = _native.load()
+        r8 = reset if reset.dtype == torch.uint8 else reset.to(torch.uint8)
+        _native.check(lib.cf2_obs_pack(obs.data_ptr(), r8.contiguous().data_ptr(), n, ol, cap, out.data_ptr(),
+                                       _native.ptr(clear_next), torch.cuda.current_stream(obs.device).cuda_stream),
+                      "cf2_obs_pack")
+        return out
+    r = reset.bool().cpu()
+    out.zero_()
+    f = out.view(torch.float32)
+    f[4:4 + n * ol] = obs[:, ol + 4:2 * ol + 4].reshape(-1)
+    nb = (n + 31) // 32
+    bits = np.zeros(4 * nb, np.uint8)
+    pb = np.packbits(r.numpy(), bitorder="little")
+    bits[:pb.size] = pb
+    out[4 + n * ol:4 + n * ol + nb] = torch.from_numpy(bits.view(np.int32))
+    idx = torch.nonzero(r).flatten()
+    out[0], out[1], out[2], out[3] = int(idx.numel()), n, ol, cap
+    side = 4 + n * ol + nb
+    for s, i in enumerate(idx[:cap].tolist()):
+        e = side + s * (ol + 5)
+        out[e] = i
+        f[e + 1:e + 1 + ol + 4] = obs[i, :ol + 4]
+    if clear_next is not None:
+        clear_next.zero_()
+    return out
+
+
+def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, slab_prev, slab, overflow=None):
+    """Rebuild every rank's rows [world n, OD] into `slab` from the gathered packed buffers
+    (int32 [world, words]), the previous slab, the step's actions and the previous step's
+    (act, act_prev: [world n, 4]); age (uint8 [world n]) is updated in place."""
+    import torch
+    if recv.is_cuda:
+        from . import _native
+        lib = _native.load()
+        _native.check(lib.cf2_obs_unpack(recv.data_ptr(), world, n, ol, cap, act.data_ptr(), act_prev.data_ptr(),
+                                         age.data_ptr(), slab_prev.data_ptr(), slab.data_ptr(), _native.ptr(overflow),
+                                         torch.cuda.current_stream(recv.device).cuda_stream), "cf2_obs_unpack")
+        return slab
+    words = packed_words(n, ol, cap)
+    rv = recv.reshape(world, words)
+    nan = float("nan")
+    for r in range(world):
+        pk = rv[r]
+        f = pk.view(torch.float32)
+        ok = f[4:4 + n * ol].view(n, ol)
+        rs = _bits_to_mask(pk[4 + n * ol:4 + n * ol + (n + 31) // 32], n)
+        sl = slice(r * n, (r + 1) * n)
+        prev, out = slab_prev[sl], slab[sl]
+        a = torch.clamp(age[sl].to(torch.int32) + 1, max=3)
+        out[:, :ol] = prev[:, ol + 4:2 * ol + 4]
+        out[:, ol:ol + 4] = torch.where((a >= 3)[:, None], prev[:, 2 * ol + 4:], act[sl])
+        out[:, ol + 4:2 * ol + 4] = ok
+        out[:, 2 * ol + 4:] = torch.where((a == 1)[:, None], act[sl], act_prev[sl])
+        cnt = int(pk[0])
+        if cnt > cap:
+            out[rs, :ol + 4] = nan
+            out[rs, 2 * ol + 4:] = nan
+            if overflow is not None:
+                overflow += 1
+        else:
+            side = 4 + n * ol + (n + 31) // 32
+            for s in range(cnt):
+                e = side + s * (ol + 5)
+                i = int(pk[e])
+                out[i, :ol + 4] = f[e + 1:e + 1 + ol + 4]
+                out[i, 2 * ol + 4:] = f[e + 1 + ol:e + 1 + ol + 4]
+        age[sl] = torch.where(rs, torch.zeros_like(a), a).to(torch.uint8)
+    return slab
+
+
 class PipelinedObsGather:
     """Per-step all-gather of the observation slab ("RCCL all-gather over
     xGMI only for the returned observation tensor"), overlapped with the next env-step.
 
-    ``depth`` observation buffers rotate: env-step k writes ``buffer()`` on the compute stream and
-    ``publish()`` starts the all-gather of that buffer on a side stream, so the gather of step k
-    runs while step k+1 computes.  Before step k+depth overwrites a buffer, the compute stream (not
-    the host) waits for the gather that read it.  ``publish()`` returns the [world * n, D] tensor
-    the gather fills; it is complete once ``wait(k)`` or ``drain()`` returned and stays valid until
-    the gather of step k + depth reuses it.  On gloo (CPU rehearsal of the multi-rank path) the
-    gather stages through the host and completes inside ``publish()``."""
+    Env-step k writes ``buffer()`` (and, with ``delta``, ``done_buffer()``) on the compute stream;
+    ``publish()`` starts the exchange of that step on a side stream, so it runs while step k+1
+    computes.  Before step k + depth overwrites a buffer, the compute stream (not the host) waits for
+    the exchange step that read it.  ``publish()`` returns the [world * n, D] slab of step k; it is
+    complete once ``drain()`` returned (or after ``ready()`` on any stream) and stays valid until
+    the publish of step k + 2.  On gloo (the CPU rehearsal of the multi-rank path) the exchange
+    stages through the host and completes inside ``publish()``.
 
-    def __init__(self, n: int, obs_dim: int, device, group=None, depth: int = 2):
+    delta=False: every step all-gathers the whole [n, D] slab of every rank.
+    delta=True: every step all-gathers only what a receiver cannot rebuild (cf2_obs_pack: o_k of
+    every env, a reset bitmap, the reset rows' o_0 and action part for up to ``cap`` resets) and
+    every rank rebuilds the full slab from its previous one and the actions (cf2_obs_unpack): the
+    actions of step k and k - 1 for every env ([world * n, 4], the policy's own outputs) are
+    arguments of ``publish``.  ``start(obs)`` gathers the observations of a reset of every env in
+    full first.  Shards must be equal (ValueError otherwise)."""
+
+    def __init__(self, n: int, obs_dim: int, device, group=None, depth: int = 2, delta: bool = False,
+                 cap: int | None = None):
         import torch
         import torch.distributed as dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.nccl = dist.get_backend(group) == "nccl"
+        sizes = exchange_sizes(n, group)
+        if len(set(sizes)) != 1:
+            raise ValueError(f"PipelinedObsGather needs equal shards, got {sizes}")
+        self.n, self.od, self.ol = int(n), int(obs_dim), int(obs_dim) // 2 - 4
         self.depth = int(depth)
+        self.delta = bool(delta)
+        self.device = torch.device(device)
+        cuda = self.device.type == "cuda"
         self.obs = [torch.empty(n, obs_dim, device=device) for _ in range(self.depth)]
-        self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
-        self.sizes = [n] * self.world
-        self.comm = torch.cuda.Stream(device=device) if self.nccl else None
-        self.work = [None] * self.depth
+        self.comm = torch.cuda.Stream(device=self.device) if (self.nccl and cuda) else None
+        self.free = [None] * self.depth      # events: the exchange of the step that used buffer j read it
         self.k = 0
+        self.started = not self.delta
+        if self.delta:
+            self.cap = default_cap(n) if cap is None else int(cap)
+            self.words = packed_words(n, self.ol, self.cap)
+            self.done = [torch.zeros(n, dtype=torch.uint8, device=device) for _ in range(self.depth)]
+            self.send = [torch.zeros(self.words, dtype=torch.int32, device=device) for _ in range(self.depth)]
+            self.recv = [torch.empty(self.world * self.words, dtype=torch.int32, device=device)
+                         for _ in range(self.depth)]
+            self.slab = [torch.zeros(self.world * n, obs_dim, device=device) for _ in range(2)]
+            self.age = torch.zeros(self.world * n, dtype=torch.uint8, device=device)
+            self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+        else:
+            self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
+
+    @property
+    def bytes_per_rank_per_step(self) -> int:
+        """Bytes one rank contributes to the all-gather of one env-step."""
+        return 4 * self.words if self.delta else 4 * self.n * self.od
+
+    def _wait_free(self, j):
+        import torch
+        if self.free[j] is not None:
+            if isinstance(self.free[j], torch.cuda.Event):
+                torch.cuda.current_stream(self.device).wait_event(self.free[j])
+            self.free[j] = None
 
     def buffer(self):
-        """The obs buffer env-step k writes; the current stream first waits (on the device) for
-        the gather of step k - depth, which read it."""
+        """The obs buffer env-step k writes (the current stream first waits, on the device, for the
+        exchange of step k - depth, which read it)."""
         j = self.k % self.depth
-        w = self.work[j]
-        if w is not None:
-            w.wait()
-            self.work[j] = None
+        self._wait_free(j)
         return self.obs[j]
 
-    def publish(self):
-        """Start the all-gather of the buffer the current env-step wrote; returns its output."""
-        import torch
+    def done_buffer(self):
+        """delta: the uint8 done (auto-reset) buffer env-step k writes; call after buffer()."""
+        return self.done[self.k % self.depth]
+
+    def _gather(self, out, x):
         import torch.distributed as dist
-        j = self.k % self.depth
         if self.nccl:
-            self.comm.wait_stream(torch.cuda.current_stream(self.obs[j].device))
-            with torch.cuda.stream(self.comm):
-                self.work[j] = dist.all_gather_into_tensor(self.out[j], self.obs[j], group=self.group, async_op=True)
+            dist.all_gather_into_tensor(out, x, group=self.group, async_op=True).wait()
         else:
-            gather_rows(self.obs[j], self.group, sizes=self.sizes, out=self.out[j])
+            gather_rows(x.reshape(1, -1), self.group, sizes=[1] * self.world, out=out.view(self.world, -1))
+
+    def start(self, obs):
+        """delta: gather the observations of a reset of every env ([n, D]) in full; every env's
+        step count since its reset is 0 on every rank."""
+        import torch
+        self._run_on_comm(lambda: (self._gather(self.slab[1], obs.contiguous()), self.age.zero_(),
+                                   [s[:1].zero_() for s in self.send]))
+        self.started = True
+        self.k = 0
+        return self.slab[1]
+
+    def _run_on_comm(self, fn):
+        import torch
+        if self.comm is not None:
+            self.comm.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.comm):
+                return fn()
+        return fn()
+
+    def publish(self, act=None, act_prev=None):
+        """Start the exchange of the buffer(s) the current env-step wrote; returns the slab it fills.
+        delta: act / act_prev = the actions of this env-step and of the previous one for all
+        world * n envs (unchanged until the slab is complete)."""
+        import torch
+        j = self.k % self.depth
+        if not self.delta:
+            def run():
+                if self.nccl:
+                    w = torch.distributed.all_gather_into_tensor(self.out[j], self.obs[j], group=self.group,
+                                                                 async_op=True)
+                    w.wait()
+                else:
+                    gather_rows(self.obs[j], self.group, sizes=[self.n] * self.world, out=self.out[j])
+                if self.comm is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(self.comm)
+                    self.free[j] = ev
+                return self.out[j]
+            out = self._run_on_comm(run)
+            self.k += 1
+            return out
+        if not self.started:
+            raise RuntimeError("delta exchange: call start(reset observations) first")
+        if act is None or act_prev is None:
+            raise ValueError("delta exchange: publish needs the actions of this step and of the previous one")
+        prev, cur = self.slab[(self.k + 1) % 2], self.slab[self.k % 2]
+
+        def run():
+            pack_obs(self.obs[j], self.done[j], self.cap, out=self.send[j],
+                     clear_next=self.send[(j + 1) % self.depth][:1])
+            if self.comm is not None:
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+                self.free[j] = ev
+            if self.recv[j].is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
+                host = gather_rows(self.send[j].cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
+                self.recv[j].copy_(host.reshape(-1))
+            else:
+                self._gather(self.recv[j], self.send[j])
+            unpack_obs(self.recv[j], self.world, self.n, self.ol, self.cap, act, act_prev, self.age, prev, cur,
+                       self.overflow)
+            if self.comm is not None:
+                ev2 = torch.cuda.Event()
+                ev2.record(self.comm)
+                self._ready = ev2
+            return cur
+        out = self._run_on_comm(run)
         self.k += 1
-        return self.out[j]
+        return out
+
+    def ready(self):
+        """Make the current stream wait for the latest published slab."""
+        import torch
+        ev = getattr(self, "_ready", None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def overflows(self) -> int:
+        """delta: steps x ranks whose resets exceeded the side-slab capacity so far (host read)."""
+        return int(self.overflow.item()) if self.delta else 0
 
     def drain(self):
-        """Make the current stream wait for every gather in flight."""
-        for j, w in enumerate(self.work):
-            if w is not None:
-                w.wait()
-                self.work[j] = None
+        """Make the current stream wait for every exchange in flight."""
+        import torch
+        if self.comm is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.comm)
+        for j in range(self.depth):
+            self.free[j] = None
 
 
 def shard_range(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:

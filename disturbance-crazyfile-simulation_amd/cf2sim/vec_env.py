@@ -354,16 +354,17 @@ class BatchedCrazyflieEnv:
             info["final_obs"] = final_obs_out
         return obs_out, rew_out, done_out, info
 
-    def step_raw(self, act_ptr: int, obs_ptr: int | None = None, full_info: bool = True):
+    def step_raw(self, act_ptr: int, obs_ptr: int | None = None, full_info: bool = True, done_ptr: int | None = None):
         """Launch one env-step with a raw device pointer to [N, 4] float32 actions (benchmark /
         graph-capture helper; the pointer is not checked).  full_info: also write the truncation,
         cost and level outputs step() returns in info (the reference's compute_info runs every step,
         envs/hover_free.py:138-166).  With obs_ptr the observations go to that raw buffer, which
-        save_checkpoint cannot see: pass it the observations explicitly."""
+        save_checkpoint cannot see: pass it the observations explicitly.  done_ptr: the uint8 done
+        flags go to that buffer instead of self.done (the delta obs exchange packs them later)."""
         self._obs_latest = self.obs if obs_ptr is None else None
         self._state_version += 1
         _native.check(self.lib.cf2_step(
-            self._ctx, act_ptr, None, obs_ptr or self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
+            self._ctx, act_ptr, None, obs_ptr or self.obs.data_ptr(), self.rew.data_ptr(), done_ptr or self.done.data_ptr(),
             self.trunc.data_ptr() if full_info else None, self.cost.data_ptr() if full_info else None,
             self.level.data_ptr() if full_info else None, None, self.stream), "cf2_step")
 

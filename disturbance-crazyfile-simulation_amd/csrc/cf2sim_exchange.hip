@@ -1,0 +1,245 @@
+// cf2sim_exchange.hip -- the multi-GPU observation exchange as deltas.
+//
+// The north star gathers every rank's observation slab to every rank each env-step (RCCL
+// all-gather over xGMI).  A row is [o_{k-1}, A0, o_k, A1] (compute_history, envs/base.py:305-321):
+// of its 34 floats only o_k (13) is new each step -- o_{k-1} was o_k of the previous step's row,
+// and the action slots are actions the receiver issued -- except around auto-resets.  So each
+// rank sends, per env-step:
+//   * o_k of every env                                   (OL words per env)
+//   * a bitmap of the envs that auto-reset this step     (1 bit per env)
+//   * for those envs (up to `cap`): the reset row's o_0 and its action part A (the reset's
+//     action-buffer entry, A_0 = A_1)                    (1 + OL + 4 words each)
+// and every receiver rebuilds the full [N_total, OD] slab from its previous one.  The action slots
+// follow the reference's history aliasing (compute_history with the action deque holding the
+// action buffer's last entry right after a reset, envs/base.py:455-462; the kernel's halias flags):
+// with `age` = env-steps since the env's last reset (0 = reset this step, capped at 3),
+//   age 1:  A0 = A1 = a_k           (both history slots alias the action buffer, which after the
+//                                     step holds a_k in every row: aggregate_phy_steps is a
+//                                     multiple of buf_size, as in the reference's default env)
+//   age 2:  A0 = a_k, A1 = a_{k-1}
+//   age 3+: A0 = the previous row's A1, A1 = a_{k-1}
+// where a_k is the action of the env-step that produced the row.  The receiver tracks age from the
+// bitmaps (exact: reset or not is always known).  More resets than `cap` on a rank in one step
+// (an overflow) leaves those rows' o_0 / A parts unknown: the receiver writes NaN there and counts
+// the overflow; the rows of the following steps are exact again.
+//
+// Packed buffer of one rank (32-bit words, 16-B multiple; cf2_obs_packed_words):
+//   [0] reset count (may exceed cap)   [1] n   [2] OL   [3] cap
+//   [4, 4 + n OL)                       o_k rows
+//   [.., + ceil(n / 32))                reset bitmap, env i = bit i % 32 of word i / 32
+//   [.., + cap (OL + 5))                side entries: local env index, o_0[OL], A[4]
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include "../../include/cf2sim.h"
+#include "cf2sim_internal.h"
+
+namespace cf2 {
+
+struct PackLayout {
+    uint32_t n, ol, cap;
+    __host__ __device__ uint32_t od() const { return 2u * (ol + 4u); }
+    __host__ __device__ uint32_t o_slab() const { return 4u; }
+    __host__ __device__ uint32_t bits() const { return 4u + n * ol; }
+    __host__ __device__ uint32_t side() const { return bits() + (n + 31u) / 32u; }
+    __host__ __device__ uint32_t entry() const { return ol + 5u; }
+    __host__ __device__ uint32_t words() const { return (side() + cap * entry() + 3u) & ~3u; }
+};
+
+constexpr uint32_t XB = 256;        // rows per block
+constexpr uint32_t XMAX_OD = 42;    // 34 with sensor noise, 42 without
+
+// Coalesced copy of `rows` rows of `od` floats (contiguous, 16-B aligned when `al`) between global
+// memory and LDS, all threads of the block
+__device__ __forceinline__ void rows_to_lds(float* s, const float* g, uint32_t count, bool al) {
+    if (al && (count & 3u) == 0) {
+        const float4* g4 = reinterpret_cast<const float4*>(g);
+        float4* s4 = reinterpret_cast<float4*>(s);
+        for (uint32_t k = threadIdx.x; k < count / 4u; k += XB) s4[k] = g4[k];
+    } else {
+        for (uint32_t k = threadIdx.x; k < count; k += XB) s[k] = g[k];
+    }
+}
+__device__ __forceinline__ void lds_to_rows(float* g, const float* s, uint32_t count, bool al) {
+    if (al && (count & 3u) == 0) {
+        float4* g4 = reinterpret_cast<float4*>(g);
+        const float4* s4 = reinterpret_cast<const float4*>(s);
+        for (uint32_t k = threadIdx.x; k < count / 4u; k += XB) g4[k] = s4[k];
+    } else {
+        for (uint32_t k = threadIdx.x; k < count; k += XB) g[k] = s[k];
+    }
+}
+
+// Sender: one thread per env of this rank.  The block's obs rows are read coalesced into LDS, o_k
+// extracted into an LDS stage and written as one contiguous run of the o_k slab; the reset bitmap
+// comes from wave ballots; a reset env takes a side slot by a wave-aggregated atomic (the slot
+// order is immaterial: each entry carries its env index).  clear_next: the count word of the
+// buffer the next pack on this stream writes (its previous contents were gathered already), so the
+// counts need no separate memset.
+__global__ void __launch_bounds__(XB) obs_pack_kernel(const float* __restrict__ obs, const uint8_t* __restrict__ reset,
+                                                      PackLayout L, uint32_t* __restrict__ pk,
+                                                      uint32_t* __restrict__ clear_next) {
+    __shared__ __align__(16) float s_rows[XB * XMAX_OD];
+    __shared__ __align__(16) float s_o[XB * 17];
+    const uint32_t od = L.od(), ol = L.ol, tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
+    const uint32_t nrow = L.n - base < XB ? L.n - base : XB;
+    if (blockIdx.x == 0 && tid == 0) {
+        if (clear_next) clear_next[0] = 0u;
+        pk[1] = L.n; pk[2] = L.ol; pk[3] = L.cap;
+    }
+    rows_to_lds(s_rows, obs + (size_t)base * od, nrow * od, ((uintptr_t)obs & 15u) == 0 && (base * od) % 4u == 0);
+    __syncthreads();
+    const bool live = tid < nrow;
+    const float* row = s_rows + tid * od;
+    if (live)
+        for (uint32_t k = 0; k < ol; ++k) s_o[tid * ol + k] = row[ol + 4u + k];
+    const bool r = live && reset[i] != 0;
+    const uint64_t m = __ballot(r);
+    const uint32_t lane = tid & 63u, wbase = base + (tid & ~63u);
+    uint32_t* bits = pk + L.bits();
+    if (lane == 0 && wbase < L.n) bits[wbase / 32u] = (uint32_t)m;
+    if (lane == 32 && wbase + 32u < L.n) bits[wbase / 32u + 1u] = (uint32_t)(m >> 32);
+    if (m) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t first = 0;
+        if ((int)lane == leader) first = atomicAdd(pk, (uint32_t)__popcll(m));
+        first = __shfl(first, leader);
+        const uint32_t slot = first + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (r && slot < L.cap) {
+            uint32_t* e = pk + L.side() + slot * L.entry();
+            e[0] = tid + base;
+            float* ef = reinterpret_cast<float*>(e + 1);
+            for (uint32_t k = 0; k < ol + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
+        }
+    }
+    __syncthreads();
+    lds_to_rows(reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * ol, s_o, nrow * ol,
+                ((uintptr_t)pk & 15u) == 0 && (base * ol) % 4u == 0);
+}
+
+// Receiver, rows: one thread per global env (rank r = i / n).  The block's previous rows are read
+// coalesced into LDS, each thread rebuilds its row there, the block writes them out coalesced.
+// Reset rows get o_k here; their o_0 / A parts come from obs_unpack_resets_kernel, launched after
+// this one (NaN if the env's rank overflowed its side slab).
+__global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __restrict__ pk_all, uint32_t words,
+                                                             uint32_t world, PackLayout L,
+                                                             const float* __restrict__ act,
+                                                             const float* __restrict__ act_prev,
+                                                             uint8_t* __restrict__ age,
+                                                             const float* __restrict__ slab_prev,
+                                                             float* __restrict__ slab) {
+    __shared__ __align__(16) float s_rows[XB * XMAX_OD];
+    const uint32_t od = L.od(), ol = L.ol, tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
+    const uint32_t total = world * L.n;
+    const uint32_t nrow = total - base < XB ? total - base : XB;
+    const bool al = (base * od) % 4u == 0 && ((uintptr_t)slab_prev & 15u) == 0 && ((uintptr_t)slab & 15u) == 0;
+    rows_to_lds(s_rows, slab_prev + (size_t)base * od, nrow * od, al);
+    __syncthreads();
+    if (tid < nrow) {
+        const uint32_t r = i / L.n, li = i - r * L.n;
+        const uint32_t* pk = pk_all + (size_t)r * words;
+        const float* ok = reinterpret_cast<const float*>(pk + L.o_slab()) + (size_t)li * ol;
+        const bool rs = (pk[L.bits() + li / 32u] >> (li % 32u)) & 1u;
+        float* row = s_rows + tid * od;
+        if (rs) {
+            const bool ovf = pk[0] > L.cap;
+            for (uint32_t k = 0; k < ol; ++k) row[ol + 4u + k] = ok[k];
+            if (ovf) {                      // o_0 and A were not sent: marked unknown
+                for (uint32_t k = 0; k < ol + 4u; ++k) row[k] = __builtin_nanf("");
+                for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = __builtin_nanf("");
+            }
+            age[i] = 0;
+        } else {
+            const uint32_t a = age[i] + 1u < 3u ? age[i] + 1u : 3u;
+            const float4 ak = reinterpret_cast<const float4*>(act)[i];
+            float a0[4], a1[4];
+            if (a >= 3u) {
+                for (uint32_t k = 0; k < 4u; ++k) a0[k] = row[2u * ol + 4u + k];
+            } else {
+                a0[0] = ak.x; a0[1] = ak.y; a0[2] = ak.z; a0[3] = ak.w;
+            }
+            if (a == 1u) {
+                a1[0] = ak.x; a1[1] = ak.y; a1[2] = ak.z; a1[3] = ak.w;
+            } else {
+                const float4 ap = reinterpret_cast<const float4*>(act_prev)[i];
+                a1[0] = ap.x; a1[1] = ap.y; a1[2] = ap.z; a1[3] = ap.w;
+            }
+            for (uint32_t k = 0; k < ol; ++k) row[k] = row[ol + 4u + k];
+            for (uint32_t k = 0; k < 4u; ++k) row[ol + k] = a0[k];
+            for (uint32_t k = 0; k < ol; ++k) row[ol + 4u + k] = ok[k];
+            for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = a1[k];
+            age[i] = (uint8_t)a;
+        }
+    }
+    __syncthreads();
+    lds_to_rows(slab + (size_t)base * od, s_rows, nrow * od, al);
+}
+
+// Receiver, resets: one thread per side slot of every rank; writes the reset row's o_0 and A
+// parts (A_0 = A_1) of the listed envs.  Counts one overflow per rank whose resets exceeded cap.
+__global__ void __launch_bounds__(XB) obs_unpack_resets_kernel(const uint32_t* __restrict__ pk_all, uint32_t words,
+                                                               uint32_t world, PackLayout L, float* __restrict__ slab,
+                                                               uint32_t* __restrict__ overflow) {
+    const uint32_t e = blockIdx.x * XB + threadIdx.x;
+    if (e >= world * L.cap) return;
+    const uint32_t r = e / L.cap, s = e - r * L.cap;
+    const uint32_t* pk = pk_all + (size_t)r * words;
+    const uint32_t cnt = pk[0];
+    if (s == 0 && cnt > L.cap && overflow) atomicAdd(overflow, 1u);
+    if (cnt > L.cap || s >= cnt) return;
+    const uint32_t* en = pk + L.side() + s * L.entry();
+    const uint32_t li = en[0];
+    if (li >= L.n) return;
+    const float* ef = reinterpret_cast<const float*>(en + 1);
+    const uint32_t ol = L.ol;
+    float* row = slab + ((size_t)r * L.n + li) * L.od();
+    for (uint32_t k = 0; k < ol + 4u; ++k) row[k] = ef[k];
+    for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = ef[ol + k];
+}
+
+}  // namespace cf2
+
+using namespace cf2;
+
+static bool layout_ok(uint32_t n, uint32_t ol, uint32_t cap) {
+    return n > 0 && (ol == 13u || ol == 17u) && cap <= n && (uint64_t)n * (ol + 10u) < (1ull << 31);
+}
+
+extern "C" size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t cap) {
+    if (!layout_ok(n, obs_len, cap)) return 0;
+    return PackLayout{n, obs_len, cap}.words();
+}
+
+extern "C" int cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
+                            uint32_t* packed_dev, uint32_t* clear_next_dev, void* stream) {
+    if (!obs_dev || !reset_dev || !packed_dev || !layout_ok(n, obs_len, cap)) return CF2_ERR_INVALID_ARG;
+    if (((uintptr_t)obs_dev & 7u) || ((uintptr_t)packed_dev & 15u)) return CF2_ERR_INVALID_ARG;
+    const PackLayout L{n, obs_len, cap};
+    hipLaunchKernelGGL(obs_pack_kernel, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev, reset_dev,
+                       L, packed_dev, clear_next_dev);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len,
+                              uint32_t cap, const float* act_dev, const float* act_prev_dev, uint8_t* age_dev,
+                              const float* slab_prev_dev, float* slab_dev, uint32_t* overflow_dev, void* stream) {
+    if (!packed_all_dev || !act_dev || !act_prev_dev || !age_dev || !slab_prev_dev || !slab_dev || world == 0 ||
+        !layout_ok(n, obs_len, cap) || (uint64_t)world * n >= (1ull << 31))
+        return CF2_ERR_INVALID_ARG;
+    if (slab_prev_dev == slab_dev) return CF2_ERR_INVALID_ARG;     // rows are rebuilt from the previous slab
+    if (((uintptr_t)act_dev & 15u) || ((uintptr_t)act_prev_dev & 15u) || ((uintptr_t)packed_all_dev & 15u) ||
+        ((uintptr_t)slab_dev & 7u) || ((uintptr_t)slab_prev_dev & 7u))
+        return CF2_ERR_INVALID_ARG;
+    const PackLayout L{n, obs_len, cap};
+    const uint32_t words = L.words(), total = world * n;
+    hipLaunchKernelGGL(obs_unpack_rows_kernel, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
+                       packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && cap > 0) {
+        hipLaunchKernelGGL(obs_unpack_resets_kernel, dim3((world * cap + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
+                           packed_all_dev, words, world, L, slab_dev, overflow_dev);
+        e = hipGetLastError();
+    }
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}

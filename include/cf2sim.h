@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 4
+#define CF2SIM_ABI_VERSION 5
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -315,6 +315,30 @@ int  cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float*
 int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev, const uint8_t* done_dev,
              const uint8_t* trunc_dev, const float* trunc_val_dev, const float* last_val_dev, float gamma,
              float lam, float rew_den, float* adv_dev, float* ret_dev, float* disc_ret_dev, void* stream);
+
+/* Multi-GPU observation exchange as deltas (the north star's per-step RCCL
+ * all-gather of the obs slab).  The reference has no counterpart: its MPI ranks exchange only
+ * gradients and statistics (utils/mpi_tools.py:30-44); the rows rebuilt here are exactly what
+ * compute_history (envs/base.py:305-321) returns on every rank.
+ * A row is [o_{k-1}, A0, o_k, A1] (obs_len OL = 13 with sensor noise, 17 without); per env-step a
+ * rank packs only o_k of every env, a bitmap of the envs that auto-reset and, for up to `cap` of
+ * them, the reset row's o_0 and action part, into cf2_obs_packed_words(n, OL, cap) 32-bit words
+ * (a multiple of 4).  After an all-gather of the packed buffers ([world][words], rank order,
+ * equal shards of n envs), cf2_obs_unpack rebuilds every rank's rows from the previous slab
+ * [world n, 2 OL + 8] and the actions of the step (act [world n, 4]) and of the step before
+ * (act_prev), tracking each env's steps since its reset in age_dev (uint8 [world n], all 0 after
+ * the slab came from a full gather right after a reset of every env).  Valid under auto-reset for
+ * env-step shapes whose action buffer holds only the step's action after a step
+ * (aggregate_phy_steps a multiple of buf_size, latency on: the reference's default).  More than
+ * cap resets on a rank in one step: those rows' o_0 / A parts become NaN and *overflow_dev is
+ * incremented; later rows are exact again.  clear_next_dev: the count word (word 0) of the buffer
+ * the next pack on this stream will write (or NULL: the caller zeroes it). */
+size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t cap);
+int  cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
+                  uint32_t* packed_dev, uint32_t* clear_next_dev, void* stream);
+int  cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len, uint32_t cap,
+                    const float* act_dev, const float* act_prev_dev, uint8_t* age_dev, const float* slab_prev_dev,
+                    float* slab_dev, uint32_t* overflow_dev, void* stream);
 
 /* Measurement support (no reference counterpart): streaming kernels over `bytes` (a multiple of
  * 16, both pointers 16-B aligned) with non-temporal accesses.  mode 0: copy src -> dst; mode 1:

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_config_struct_matches(lib):
     from cf2sim.config import CF2Config
     assert lib.cf2_config_sizeof() == ctypes.sizeof(CF2Config)
-    assert lib.cf2_abi_version() == 4
+    assert lib.cf2_abi_version() == 5
 
 
 def test_status_strings_and_invalid_args(lib):
@@ -115,3 +115,14 @@ def test_kernel_sources_hold_no_ab_branches():
             m = re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b(.*)", line)
             if m:
                 assert "CF2_TIMING" in m.group(2), f"{os.path.basename(f)}: {line.strip()}"
+
+
+def test_obs_exchange_error_paths(lib):
+    """cf2_obs_pack / cf2_obs_unpack reject bad sizes and pointers without launching anything."""
+    from cf2sim.dist import packed_words
+    assert lib.cf2_obs_packed_words(32768, 13, 2458) == packed_words(32768, 13, 2458)
+    assert lib.cf2_obs_packed_words(5, 17, 3) == packed_words(5, 17, 3)
+    assert lib.cf2_obs_packed_words(0, 13, 0) == 0 and lib.cf2_obs_packed_words(8, 12, 1) == 0
+    assert lib.cf2_obs_packed_words(8, 13, 9) == 0                      # cap > n
+    assert lib.cf2_obs_pack(None, None, 8, 13, 1, None, None, None) == -1
+    assert lib.cf2_obs_unpack(None, 1, 8, 13, 1, None, None, None, None, None, None, None) == -1

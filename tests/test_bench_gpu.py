@@ -50,7 +50,12 @@ def test_bench_self_launches_two_ranks(gpu):
     assert d["config"]["gather_obs"] is True and d["scaling"] == "strong"
     assert d["value"] > 0 and d["no_gather"]["value"] > 0
     assert d["weak_scaling"]["global_envs"] == 2 * 262144 and d["weak_scaling"]["value"] > 0
-    assert d["gather"]["total_bytes_per_step"] == 262144 * 34 * 4
+    # the delta exchange (default): 2.3x fewer bytes than the rows, no side-slab overflow
+    gi = d["gather"]
+    assert gi["mode"].startswith("pipelined delta")
+    assert gi["full_rows_bytes_in_per_rank_per_step"] == 131072 * 34 * 4
+    assert gi["bytes_in_per_rank_per_step"] * 2.3 <= gi["full_rows_bytes_in_per_rank_per_step"]
+    assert gi["overflows"] == 0
 
 
 def test_bench_rccl_gather_path_one_rank(gpu):
@@ -61,7 +66,7 @@ def test_bench_rccl_gather_path_one_rank(gpu):
     assert p.returncode == 0, p.stderr[-3000:]
     d = _line(p.stdout)
     assert d["backend"] == "nccl" and d["world_size"] == 1 and d["config"]["gather_obs"] is True
-    assert d["gather"]["mode"].startswith("pipelined") and d["value"] > 0
+    assert d["gather"]["mode"].startswith("pipelined delta") and d["value"] > 0 and d["gather"]["overflows"] == 0
 
 
 def _pipe_worker(rank, world, port, out):

@@ -1,0 +1,138 @@
+"""Delta observation exchange (cf2sim.dist: pack_obs / unpack_obs / PipelinedObsGather(delta=True),
+the protocol of csrc/cf2sim_exchange.hip) on CPU: two gloo ranks step their shards of the CPU
+restatement (oracle/, which the HIP kernel matches step for step, tests/test_gpu_parity.py) and
+exchange only o_k, a reset bitmap and the reset rows' o_0 / action parts; the slab every rank
+rebuilds must equal the full all-gather of the obs rows bit for bit, over >= 200 env-steps with
+auto-resets and time-outs.  A side slab too small for a step's resets marks exactly those rows
+(NaN in their o_0 / action parts), counts the overflow, and the following steps are exact again."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ENV_ID = "DroneHoverBulletFreeEnvWithGust-v0"
+N_PER_RANK, T, SEED = 48, 220, 5
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _actions(t, n):
+    return np.random.default_rng(2000 + t).uniform(-1, 1, size=(n, 4)).astype(np.float32)
+
+
+def _worker(rank, world, port, out_dir, cap):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "disturbance-crazyfile-simulation_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    import oracle as O
+    from cf2sim.config import build_config
+    from cf2sim.dist import PipelinedObsGather, delta_supported, gather_rows
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, N = N_PER_RANK, N_PER_RANK * world
+    off = rank * n
+    cfg = build_config(ENV_ID, n, seed=SEED, env_id_offset=off, max_episode_steps=37)
+    assert delta_supported(cfg)
+    env = O.OracleEnv(cfg, precision="f32")
+    od = env.obs_dim
+    pipe = PipelinedObsGather(n, od, "cpu", delta=True, cap=cap)
+    obs0 = torch.from_numpy(env.reset().astype(np.float32))
+    slab = pipe.start(obs0)
+    full = gather_rows(obs0, sizes=[n] * world)
+    assert torch.equal(slab, full)
+    mismatch, nan_rows, resets = [], [], 0
+    a_prev = torch.from_numpy(_actions(0, N))
+    for t in range(T):
+        a = torch.from_numpy(_actions(t, N))
+        o, r, d, _ = env.step(a[off:off + n].numpy())
+        pipe.buffer().copy_(torch.from_numpy(o.astype(np.float32)))
+        pipe.done_buffer().copy_(torch.from_numpy(d.astype(np.uint8)))
+        slab = pipe.publish(a, a_prev if t > 0 else a)
+        full = gather_rows(torch.from_numpy(o.astype(np.float32)), sizes=[n] * world)
+        dall = gather_rows(torch.from_numpy(d.astype(np.uint8)), sizes=[n] * world).bool()
+        resets += int(dall.sum())
+        bad = ~(slab == full).all(dim=1)
+        if cap is None:
+            if bad.any():
+                mismatch.append((t, torch.nonzero(bad).flatten().tolist()[:5]))
+        else:
+            # only reset rows of an overflowing step may differ, and only as NaN in their o_0 / A parts
+            nan = torch.isnan(slab).any(dim=1)
+            assert bool((bad <= (nan & dall)).all()), (t, torch.nonzero(bad & ~(nan & dall)).flatten()[:5])
+            nan_rows.append(int(nan.sum()))
+        a_prev = a
+    env.close()
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "res.npz"), mismatch=np.array(len(mismatch)), resets=np.array(resets),
+                 overflows=np.array(pipe.overflows()), nan_rows=np.array(nan_rows if nan_rows else [0]),
+                 first=np.array(mismatch[:1], dtype=object) if mismatch else np.zeros(0))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_delta_exchange_matches_full_gather(tmp_path):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), None), nprocs=2, join=True)
+    res = np.load(tmp_path / "res.npz", allow_pickle=True)
+    assert int(res["mismatch"]) == 0, res["first"]
+    assert int(res["resets"]) > 100              # auto-resets (crashes and time-outs) in the window
+    assert int(res["overflows"]) == 0
+
+
+def test_delta_exchange_overflow_is_marked_and_recovers(tmp_path):
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), 1), nprocs=2, join=True)
+    res = np.load(tmp_path / "res.npz", allow_pickle=True)
+    assert int(res["overflows"]) > 0
+    assert res["nan_rows"].max() > 0
+
+
+def test_packed_layout_and_bytes():
+    from cf2sim.dist import default_cap, packed_words
+    n = 32768
+    cap = default_cap(n)
+    w = packed_words(n, 13, cap)
+    assert w % 4 == 0
+    full = n * 34 * 4
+    assert full / (4 * w) >= 2.3, full / (4 * w)        # >= 2.3x fewer bytes than the full rows
+    assert packed_words(5, 17, 3) == ((4 + 5 * 17 + 1 + 3 * 22 + 3) & ~3)
+
+
+def test_pack_unpack_single_process_roundtrip():
+    """pack -> unpack over one rank on synthetic rows that follow the history rules."""
+    from cf2sim.dist import pack_obs, packed_words, unpack_obs
+    n, ol = 70, 13
+    od = 2 * (ol + 4)
+    g = torch.Generator().manual_seed(0)
+    prev = torch.randn(n, od, generator=g)
+    a_k, a_p = torch.randn(n, 4, generator=g), torch.randn(n, 4, generator=g)
+    age = torch.tensor([(i % 4) for i in range(n)], dtype=torch.uint8)
+    reset = torch.zeros(n, dtype=torch.uint8)
+    reset[[3, 17, 40]] = 1
+    ok = torch.randn(n, ol, generator=g)
+    exp = torch.empty(n, od)
+    for i in range(n):
+        a = min(int(age[i]) + 1, 3)
+        exp[i, :ol] = prev[i, ol + 4:2 * ol + 4]
+        exp[i, ol:ol + 4] = prev[i, 2 * ol + 4:] if a >= 3 else a_k[i]
+        exp[i, ol + 4:2 * ol + 4] = ok[i]
+        exp[i, 2 * ol + 4:] = a_k[i] if a == 1 else a_p[i]
+    o0, A = torch.randn(3, ol, generator=g), torch.randn(3, 4, generator=g)
+    for j, i in enumerate([3, 17, 40]):
+        exp[i, :ol], exp[i, ol:ol + 4], exp[i, 2 * ol + 4:] = o0[j], A[j], A[j]
+    cur = exp.clone()          # the env's rows of this step: o_k in the o part, reset rows in full
+    pk = pack_obs(cur, reset, cap=8)
+    assert pk.numel() == packed_words(n, ol, 8) and int(pk[0]) == 3
+    out = torch.full((n, od), -7.0)
+    age2 = age.clone()
+    unpack_obs(pk.view(1, -1), 1, n, ol, 8, a_k, a_p, age2, prev, out)
+    assert torch.equal(out, exp)
+    assert age2[[3, 17, 40]].tolist() == [0, 0, 0]
+    assert age2[0].item() == 1 and age2[2].item() == 3 and age2[4].item() == 1
