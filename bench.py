@@ -338,7 +338,7 @@ def main(argv=None):
         delta = False
     if gather:
         if len(set(shards)) == 1:
-            pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta)
+            pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps))
             if delta:
                 pipe.start(env.obs)
                 gather_mode = (f"pipelined delta all_gather_into_tensor (o_k + reset bitmap + side slab of "

@@ -93,7 +93,7 @@ def load() -> ctypes.CDLL:
     lib.cf2_obs_packed_words.restype = ctypes.c_size_t
     lib.cf2_obs_packed_words.argtypes = [u32, u32, u32]
     lib.cf2_obs_pack.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
-    lib.cf2_obs_unpack.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp]
+    lib.cf2_obs_unpack.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
                         "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_obs_packed_words"):

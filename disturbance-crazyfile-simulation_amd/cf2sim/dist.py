@@ -139,21 +139,30 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
     return out
 
 
-def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, slab_prev, slab, overflow=None):
+NO_WATCH = 0xFFFFFFFF
+
+
+def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, slab_prev, slab, overflow=None,
+               watch_age: int = NO_WATCH, pred=None, pred_next=None):
     """Rebuild every rank's rows [world n, OD] into `slab` from the gathered packed buffers
-    (int32 [world, words]), the previous slab, the step's actions and the previous step's
-    (act, act_prev: [world n, 4]); age (uint8 [world n]) is updated in place."""
+    (int32 [world * packed_words(n, ol, cap)]), the previous slab, the step's actions and the
+    previous step's (act, act_prev: [world n, 4]); age (steps since reset; int16 storage of a
+    uint16 on GPUs, int32 on the CPU, [world n]) is updated in place.  Envs whose new age equals
+    watch_age are counted per rank into pred ([world]); pred_next is zeroed."""
     import torch
     if recv.is_cuda:
         from . import _native
         lib = _native.load()
         _native.check(lib.cf2_obs_unpack(recv.data_ptr(), world, n, ol, cap, act.data_ptr(), act_prev.data_ptr(),
                                          age.data_ptr(), slab_prev.data_ptr(), slab.data_ptr(), _native.ptr(overflow),
+                                         int(watch_age) & 0xFFFFFFFF, _native.ptr(pred), _native.ptr(pred_next),
                                          torch.cuda.current_stream(recv.device).cuda_stream), "cf2_obs_unpack")
         return slab
     words = packed_words(n, ol, cap)
-    rv = recv.reshape(world, words)
+    rv = recv[:world * words].reshape(world, words)
     nan = float("nan")
+    if pred_next is not None:
+        pred_next.zero_()
     for r in range(world):
         pk = rv[r]
         f = pk.view(torch.float32)
@@ -161,7 +170,7 @@ def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, 
         rs = _bits_to_mask(pk[4 + n * ol:4 + n * ol + (n + 31) // 32], n)
         sl = slice(r * n, (r + 1) * n)
         prev, out = slab_prev[sl], slab[sl]
-        a = torch.clamp(age[sl].to(torch.int32) + 1, max=3)
+        a = torch.clamp(age[sl].to(torch.int64) + 1, max=0xFFFF)
         out[:, :ol] = prev[:, ol + 4:2 * ol + 4]
         out[:, ol:ol + 4] = torch.where((a >= 3)[:, None], prev[:, 2 * ol + 4:], act[sl])
         out[:, ol + 4:2 * ol + 4] = ok
@@ -179,7 +188,10 @@ def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, 
                 i = int(pk[e])
                 out[i, :ol + 4] = f[e + 1:e + 1 + ol + 4]
                 out[i, 2 * ol + 4:] = f[e + 1 + ol:e + 1 + ol + 4]
-        age[sl] = torch.where(rs, torch.zeros_like(a), a).to(torch.uint8)
+        new = torch.where(rs, torch.zeros_like(a), a)
+        age[sl] = new.to(age.dtype)
+        if pred is not None:
+            pred[r] += int((new == watch_age).sum())
     return slab
 
 
@@ -201,10 +213,14 @@ class PipelinedObsGather:
     every rank rebuilds the full slab from its previous one and the actions (cf2_obs_unpack): the
     actions of step k and k - 1 for every env ([world * n, 4], the policy's own outputs) are
     arguments of ``publish``.  ``start(obs)`` gathers the observations of a reset of every env in
-    full first.  Shards must be equal (ValueError otherwise)."""
+    full first.  The side capacity of a step is ``cap`` (the crash budget, default_cap) plus the
+    time-outs that step can have at most (max_steps: the env's TimeLimit; the receivers count the
+    envs that reach max_steps - lookahead, every rank the same, and the host reads the count
+    ``lookahead`` steps later), so synchronised time-outs never overflow.  Shards must be equal
+    (ValueError otherwise)."""
 
     def __init__(self, n: int, obs_dim: int, device, group=None, depth: int = 2, delta: bool = False,
-                 cap: int | None = None):
+                 cap: int | None = None, max_steps: int = 0, lookahead: int = 8):
         import torch
         import torch.distributed as dist
         self.group = group
@@ -223,23 +239,38 @@ class PipelinedObsGather:
         self.free = [None] * self.depth      # events: the exchange of the step that used buffer j read it
         self.k = 0
         self.started = not self.delta
+        self.bytes_sent = 0                  # this rank's contribution to every gather since start()
+        self.steps_sent = 0
         if self.delta:
             self.cap = default_cap(n) if cap is None else int(cap)
-            self.words = packed_words(n, self.ol, self.cap)
+            self.max_steps = int(max_steps)
+            self.L = int(lookahead)
+            # time-outs are predicted L steps ahead from the ages (watch age max_steps - L); a
+            # TimeLimit of L steps or fewer is sent at full capacity instead
+            self.watch = self.max_steps - self.L if self.max_steps > self.L else NO_WATCH
+            wmax = packed_words(n, self.ol, n)
             self.done = [torch.zeros(n, dtype=torch.uint8, device=device) for _ in range(self.depth)]
-            self.send = [torch.zeros(self.words, dtype=torch.int32, device=device) for _ in range(self.depth)]
-            self.recv = [torch.empty(self.world * self.words, dtype=torch.int32, device=device)
-                         for _ in range(self.depth)]
+            self.send = [torch.zeros(wmax, dtype=torch.int32, device=device) for _ in range(self.depth)]
+            self.recv = [torch.empty(self.world * wmax, dtype=torch.int32, device=device) for _ in range(self.depth)]
             self.slab = [torch.zeros(self.world * n, obs_dim, device=device) for _ in range(2)]
-            self.age = torch.zeros(self.world * n, dtype=torch.uint8, device=device)
+            self.age = torch.zeros(self.world * n, dtype=torch.int16 if cuda else torch.int32, device=device)
             self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+            self.pred = torch.zeros(self.L + 1, self.world, dtype=torch.int32, device=device)
+            pin = cuda
+            self.pred_host = torch.zeros(self.L + 1, self.world, dtype=torch.int32, pin_memory=pin)
+            self.pred_ev = [None] * (self.L + 1)
         else:
             self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
 
     @property
     def bytes_per_rank_per_step(self) -> int:
-        """Bytes one rank contributes to the all-gather of one env-step."""
-        return 4 * self.words if self.delta else 4 * self.n * self.od
+        """Bytes one rank contributed to the all-gather of one env-step (delta: the mean since
+        start(); before any step, that of the base capacity)."""
+        if not self.delta:
+            return 4 * self.n * self.od
+        if self.steps_sent:
+            return self.bytes_sent / self.steps_sent
+        return 4 * packed_words(self.n, self.ol, self.cap)
 
     def _wait_free(self, j):
         import torch
@@ -266,16 +297,6 @@ class PipelinedObsGather:
         else:
             gather_rows(x.reshape(1, -1), self.group, sizes=[1] * self.world, out=out.view(self.world, -1))
 
-    def start(self, obs):
-        """delta: gather the observations of a reset of every env ([n, D]) in full; every env's
-        step count since its reset is 0 on every rank."""
-        import torch
-        self._run_on_comm(lambda: (self._gather(self.slab[1], obs.contiguous()), self.age.zero_(),
-                                   [s[:1].zero_() for s in self.send]))
-        self.started = True
-        self.k = 0
-        return self.slab[1]
-
     def _run_on_comm(self, fn):
         import torch
         if self.comm is not None:
@@ -283,6 +304,37 @@ class PipelinedObsGather:
             with torch.cuda.stream(self.comm):
                 return fn()
         return fn()
+
+    def start(self, obs):
+        """delta: gather the observations of a reset of every env ([n, D]) in full; every env's
+        step count since its reset is 0 on every rank."""
+        def run():
+            self._gather(self.slab[1], obs.contiguous())
+            self.age.zero_()
+            self.pred.zero_()
+            for s in self.send:
+                s[:1].zero_()
+        self._run_on_comm(run)
+        self.pred_host.zero_()
+        self.pred_ev = [None] * (self.L + 1)
+        self.started = True
+        self.k = 0
+        return self.slab[1]
+
+    def step_cap(self, k: int) -> int:
+        """Side capacity of env-step k (0-based since start()): the crash budget plus the time-outs
+        that step can have at most."""
+        if self.watch == NO_WATCH:
+            return self.n if 0 < self.max_steps else self.cap
+        if k < self.L:                       # before the first prediction: every env is k + 1 old
+            t = self.n if k + 1 == self.max_steps else 0
+        else:
+            s = (k - self.L) % (self.L + 1)
+            ev = self.pred_ev[s]
+            if ev is not None:
+                ev.synchronize()
+            t = int(self.pred_host[s].max())
+        return min(self.n, self.cap + t)
 
     def publish(self, act=None, act_prev=None):
         """Start the exchange of the buffer(s) the current env-step wrote; returns the slab it fills.
@@ -310,28 +362,42 @@ class PipelinedObsGather:
             raise RuntimeError("delta exchange: call start(reset observations) first")
         if act is None or act_prev is None:
             raise ValueError("delta exchange: publish needs the actions of this step and of the previous one")
-        prev, cur = self.slab[(self.k + 1) % 2], self.slab[self.k % 2]
+        k = self.k
+        cap = self.step_cap(k)
+        words = packed_words(self.n, self.ol, cap)
+        prev, cur = self.slab[(k + 1) % 2], self.slab[k % 2]
+        ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
+        send, recv = self.send[j][:words], self.recv[j][:self.world * words]
 
         def run():
-            pack_obs(self.obs[j], self.done[j], self.cap, out=self.send[j],
-                     clear_next=self.send[(j + 1) % self.depth][:1])
+            pack_obs(self.obs[j], self.done[j], cap, out=send, clear_next=self.send[(j + 1) % self.depth][:1])
             if self.comm is not None:
                 ev = torch.cuda.Event()
                 ev.record(self.comm)
                 self.free[j] = ev
-            if self.recv[j].is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
-                host = gather_rows(self.send[j].cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
-                self.recv[j].copy_(host.reshape(-1))
+            if recv.is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
+                host = gather_rows(send.cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
+                recv.copy_(host.reshape(-1))
             else:
-                self._gather(self.recv[j], self.send[j])
-            unpack_obs(self.recv[j], self.world, self.n, self.ol, self.cap, act, act_prev, self.age, prev, cur,
-                       self.overflow)
+                self._gather(recv, send)
+            watch = self.watch if self.watch != NO_WATCH else NO_WATCH
+            unpack_obs(recv, self.world, self.n, self.ol, cap, act, act_prev, self.age, prev, cur, self.overflow,
+                       watch, self.pred[ps] if watch != NO_WATCH else None,
+                       self.pred[pn] if watch != NO_WATCH else None)
+            if watch != NO_WATCH:
+                self.pred_host[ps].copy_(self.pred[ps], non_blocking=True)
+                if self.pred.is_cuda:             # the host reads it L steps later, after this event
+                    pe = torch.cuda.Event()
+                    pe.record(torch.cuda.current_stream(self.device))
+                    self.pred_ev[ps] = pe
             if self.comm is not None:
                 ev2 = torch.cuda.Event()
                 ev2.record(self.comm)
                 self._ready = ev2
             return cur
         out = self._run_on_comm(run)
+        self.bytes_sent += 4 * words
+        self.steps_sent += 1
         self.k += 1
         return out
 
@@ -343,7 +409,7 @@ class PipelinedObsGather:
             torch.cuda.current_stream(self.device).wait_event(ev)
 
     def overflows(self) -> int:
-        """delta: steps x ranks whose resets exceeded the side-slab capacity so far (host read)."""
+        """delta: steps x ranks whose resets exceeded the side capacity so far (host read)."""
         return int(self.overflow.item()) if self.delta else 0
 
     def drain(self):

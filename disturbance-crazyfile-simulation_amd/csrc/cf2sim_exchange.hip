@@ -12,7 +12,7 @@
 // and every receiver rebuilds the full [N_total, OD] slab from its previous one.  The action slots
 // follow the reference's history aliasing (compute_history with the action deque holding the
 // action buffer's last entry right after a reset, envs/base.py:455-462; the kernel's halias flags):
-// with `age` = env-steps since the env's last reset (0 = reset this step, capped at 3),
+// with `age` = env-steps since the env's last reset (0 = reset this step; uint16, saturating),
 //   age 1:  A0 = A1 = a_k           (both history slots alias the action buffer, which after the
 //                                     step holds a_k in every row: aggregate_phy_steps is a
 //                                     multiple of buf_size, as in the reference's default env)
@@ -22,6 +22,11 @@
 // bitmaps (exact: reset or not is always known).  More resets than `cap` on a rank in one step
 // (an overflow) leaves those rows' o_0 / A parts unknown: the receiver writes NaN there and counts
 // the overflow; the rows of the following steps are exact again.
+// The capacity may change from step to step (the caller sizes the all-gather): TimeLimit
+// truncations are predictable, so the receiver counts, per rank, the envs whose age reaches
+// max_steps - L this step -- at most that many time out L steps later (fewer if they crash first)
+// -- into pred[step % (L + 1)][rank], and the caller adds that count to the crash budget of step
+// + L.  Every rank holds the same ages, so every rank derives the same capacity.
 //
 // Packed buffer of one rank (32-bit words, 16-B multiple; cf2_obs_packed_words):
 //   [0] reset count (may exceed cap)   [1] n   [2] OL   [3] cap
@@ -125,18 +130,22 @@ __global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __r
                                                              uint32_t world, PackLayout L,
                                                              const float* __restrict__ act,
                                                              const float* __restrict__ act_prev,
-                                                             uint8_t* __restrict__ age,
+                                                             uint16_t* __restrict__ age,
                                                              const float* __restrict__ slab_prev,
-                                                             float* __restrict__ slab) {
+                                                             float* __restrict__ slab, uint32_t watch_age,
+                                                             uint32_t* __restrict__ pred, uint32_t* __restrict__ pred_next) {
     __shared__ __align__(16) float s_rows[XB * XMAX_OD];
     const uint32_t od = L.od(), ol = L.ol, tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
     const uint32_t total = world * L.n;
     const uint32_t nrow = total - base < XB ? total - base : XB;
     const bool al = (base * od) % 4u == 0 && ((uintptr_t)slab_prev & 15u) == 0 && ((uintptr_t)slab & 15u) == 0;
+    if (blockIdx.x == 0 && pred_next && tid < world) pred_next[tid] = 0u;     // the next step's counts
     rows_to_lds(s_rows, slab_prev + (size_t)base * od, nrow * od, al);
     __syncthreads();
+    uint32_t a_new = 0xFFFFFFFFu, rank = 0;
     if (tid < nrow) {
         const uint32_t r = i / L.n, li = i - r * L.n;
+        rank = r;
         const uint32_t* pk = pk_all + (size_t)r * words;
         const float* ok = reinterpret_cast<const float*>(pk + L.o_slab()) + (size_t)li * ol;
         const bool rs = (pk[L.bits() + li / 32u] >> (li % 32u)) & 1u;
@@ -149,8 +158,9 @@ __global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __r
                 for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = __builtin_nanf("");
             }
             age[i] = 0;
+            a_new = 0;
         } else {
-            const uint32_t a = age[i] + 1u < 3u ? age[i] + 1u : 3u;
+            const uint32_t a = age[i] < 0xFFFFu ? age[i] + 1u : 0xFFFFu;
             const float4 ak = reinterpret_cast<const float4*>(act)[i];
             float a0[4], a1[4];
             if (a >= 3u) {
@@ -168,9 +178,12 @@ __global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __r
             for (uint32_t k = 0; k < 4u; ++k) row[ol + k] = a0[k];
             for (uint32_t k = 0; k < ol; ++k) row[ol + 4u + k] = ok[k];
             for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = a1[k];
-            age[i] = (uint8_t)a;
+            age[i] = (uint16_t)a;
+            a_new = a;
         }
     }
+    // time-out look-ahead: envs at age watch_age time out (unless they crash first) L steps later
+    if (pred && a_new == watch_age) atomicAdd(pred + rank, 1u);     // ~1/max_steps of the envs per step
     __syncthreads();
     lds_to_rows(slab + (size_t)base * od, s_rows, nrow * od, al);
 }
@@ -222,8 +235,9 @@ extern "C" int cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint
 }
 
 extern "C" int cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len,
-                              uint32_t cap, const float* act_dev, const float* act_prev_dev, uint8_t* age_dev,
-                              const float* slab_prev_dev, float* slab_dev, uint32_t* overflow_dev, void* stream) {
+                              uint32_t cap, const float* act_dev, const float* act_prev_dev, uint16_t* age_dev,
+                              const float* slab_prev_dev, float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age,
+                              uint32_t* pred_dev, uint32_t* pred_next_dev, void* stream) {
     if (!packed_all_dev || !act_dev || !act_prev_dev || !age_dev || !slab_prev_dev || !slab_dev || world == 0 ||
         !layout_ok(n, obs_len, cap) || (uint64_t)world * n >= (1ull << 31))
         return CF2_ERR_INVALID_ARG;
@@ -234,7 +248,8 @@ extern "C" int cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, ui
     const PackLayout L{n, obs_len, cap};
     const uint32_t words = L.words(), total = world * n;
     hipLaunchKernelGGL(obs_unpack_rows_kernel, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
-                       packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev);
+                       packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
+                       watch_age, pred_dev, pred_next_dev);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && cap > 0) {
         hipLaunchKernelGGL(obs_unpack_resets_kernel, dim3((world * cap + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,

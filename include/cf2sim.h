@@ -326,8 +326,11 @@ int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev,
  * (a multiple of 4).  After an all-gather of the packed buffers ([world][words], rank order,
  * equal shards of n envs), cf2_obs_unpack rebuilds every rank's rows from the previous slab
  * [world n, 2 OL + 8] and the actions of the step (act [world n, 4]) and of the step before
- * (act_prev), tracking each env's steps since its reset in age_dev (uint8 [world n], all 0 after
- * the slab came from a full gather right after a reset of every env).  Valid under auto-reset for
+ * (act_prev), tracking each env's steps since its reset in age_dev (uint16 [world n], saturating;
+ * all 0 after the slab came from a full gather right after a reset of every env).  Time-out
+ * look-ahead: envs whose age becomes watch_age this step (max_episode_steps - L; 0xFFFFFFFF: off)
+ * are counted per rank into pred_dev[world] (pred_next_dev[world] is zeroed for the next step):
+ * at most that many envs time out L steps later, so the caller can size that step's cap.  Valid under auto-reset for
  * env-step shapes whose action buffer holds only the step's action after a step
  * (aggregate_phy_steps a multiple of buf_size, latency on: the reference's default).  More than
  * cap resets on a rank in one step: those rows' o_0 / A parts become NaN and *overflow_dev is
@@ -337,8 +340,9 @@ size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t cap);
 int  cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
                   uint32_t* packed_dev, uint32_t* clear_next_dev, void* stream);
 int  cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len, uint32_t cap,
-                    const float* act_dev, const float* act_prev_dev, uint8_t* age_dev, const float* slab_prev_dev,
-                    float* slab_dev, uint32_t* overflow_dev, void* stream);
+                    const float* act_dev, const float* act_prev_dev, uint16_t* age_dev, const float* slab_prev_dev,
+                    float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
+                    uint32_t* pred_next_dev, void* stream);
 
 /* Measurement support (no reference counterpart): streaming kernels over `bytes` (a multiple of
  * 16, both pointers 16-B aligned) with non-temporal accesses.  mode 0: copy src -> dst; mode 1:

@@ -125,4 +125,4 @@ def test_obs_exchange_error_paths(lib):
     assert lib.cf2_obs_packed_words(0, 13, 0) == 0 and lib.cf2_obs_packed_words(8, 12, 1) == 0
     assert lib.cf2_obs_packed_words(8, 13, 9) == 0                      # cap > n
     assert lib.cf2_obs_pack(None, None, 8, 13, 1, None, None, None) == -1
-    assert lib.cf2_obs_unpack(None, 1, 8, 13, 1, None, None, None, None, None, None, None) == -1
+    assert lib.cf2_obs_unpack(None, 1, 8, 13, 1, None, None, None, None, None, None, 0, None, None, None) == -1

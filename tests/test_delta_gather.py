@@ -44,7 +44,9 @@ def _worker(rank, world, port, out_dir, cap):
     assert delta_supported(cfg)
     env = O.OracleEnv(cfg, precision="f32")
     od = env.obs_dim
-    pipe = PipelinedObsGather(n, od, "cpu", delta=True, cap=cap)
+    # cap None: the default crash budget plus the predicted time-outs (TimeLimit 37); cap 1 with
+    # the look-ahead off: most steps with a reset overflow
+    pipe = PipelinedObsGather(n, od, "cpu", delta=True, cap=cap, max_steps=37 if cap is None else 0)
     obs0 = torch.from_numpy(env.reset().astype(np.float32))
     slab = pipe.start(obs0)
     full = gather_rows(obs0, sizes=[n] * world)
@@ -87,6 +89,33 @@ def test_delta_exchange_matches_full_gather(tmp_path):
     assert int(res["overflows"]) == 0
 
 
+def test_time_out_look_ahead_sizes_the_capacity():
+    """A TimeLimit makes resets predictable: every env that reaches max_steps - L steps since its
+    reset times out L steps later unless it crashes first, so step_cap covers them."""
+    from cf2sim.dist import unpack_obs, packed_words, pack_obs
+    n, ol, M, L = 40, 13, 12, 4
+    od = 2 * (ol + 4)
+    age = torch.zeros(n, dtype=torch.int32)
+    pred = torch.zeros(L + 1, 1, dtype=torch.int32)
+    slab = [torch.zeros(n, od), torch.zeros(n, od)]
+    a = torch.zeros(n, 4)
+    hits = []
+    for k in range(30):
+        reset = torch.zeros(n, dtype=torch.uint8)
+        if k == 5:
+            reset[:7] = 1                        # 7 envs reset at step 5: they time out at step 5 + M
+        if k + 1 == M:
+            reset[7:] = 1                        # the others time out at step M - 1 (reset at start)
+        if k == 5 + M:
+            reset[:7] = 1
+        if k >= L and int(pred[(k - L) % (L + 1)].max()):      # read before this step's unpack reuses the slot
+            hits.append((k, int(pred[(k - L) % (L + 1)].max())))
+        pk = pack_obs(slab[k % 2], reset, cap=n)
+        unpack_obs(pk, 1, n, ol, n, a, a, age, slab[k % 2], slab[(k + 1) % 2], None, M - L,
+                   pred[k % (L + 1)], pred[(k + 1) % (L + 1)])
+    assert (5 + M, 7) in hits and (M - 1 + M, 33) in hits, hits
+
+
 def test_delta_exchange_overflow_is_marked_and_recovers(tmp_path):
     mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), 1), nprocs=2, join=True)
     res = np.load(tmp_path / "res.npz", allow_pickle=True)
@@ -113,7 +142,7 @@ def test_pack_unpack_single_process_roundtrip():
     g = torch.Generator().manual_seed(0)
     prev = torch.randn(n, od, generator=g)
     a_k, a_p = torch.randn(n, 4, generator=g), torch.randn(n, 4, generator=g)
-    age = torch.tensor([(i % 4) for i in range(n)], dtype=torch.uint8)
+    age = torch.tensor([(i % 4) for i in range(n)], dtype=torch.int32)
     reset = torch.zeros(n, dtype=torch.uint8)
     reset[[3, 17, 40]] = 1
     ok = torch.randn(n, ol, generator=g)

@@ -30,7 +30,7 @@ def _synthetic(world, n, ol, seed):
     prev = torch.randn(N, od, generator=g)
     cur = torch.randn(N, od, generator=g)
     reset = (torch.rand(N, generator=g) < 0.06).to(torch.uint8)
-    age = torch.randint(0, 4, (N,), generator=g, dtype=torch.uint8)
+    age = torch.randint(0, 6, (N,), generator=g, dtype=torch.int32)
     a_k, a_p = torch.randn(N, 4, generator=g), torch.randn(N, 4, generator=g)
     return prev, cur, reset, age, a_k, a_p
 
@@ -55,16 +55,22 @@ def test_kernels_equal_torch_ops(gpu, world, n, ol, cap):
     out_c = torch.full_like(prev, -1.0)
     age_c = age.clone()
     ovf_c = torch.zeros(1, dtype=torch.int32)
-    unpack_obs(pk_cpu, world, n, ol, cap, a_k, a_p, age_c, prev, out_c, ovf_c)
+    pred_c = torch.ones(2, world, dtype=torch.int32)
+    pred_c[0].zero_()
+    unpack_obs(pk_cpu, world, n, ol, cap, a_k, a_p, age_c, prev, out_c, ovf_c, 4, pred_c[0], pred_c[1])
     out_g = torch.full_like(prev, -1.0).to(gpu)
-    age_g = age.to(gpu)
+    age_g = age.to(torch.int16).to(gpu)                    # uint16 storage on the GPU
     ovf_g = torch.zeros(1, dtype=torch.int32, device=gpu)
-    unpack_obs(pk_gpu, world, n, ol, cap, a_k.to(gpu), a_p.to(gpu), age_g, prev.to(gpu), out_g, ovf_g)
+    pred_g = torch.ones(2, world, dtype=torch.int32, device=gpu)
+    pred_g[0].zero_()
+    unpack_obs(pk_gpu, world, n, ol, cap, a_k.to(gpu), a_p.to(gpu), age_g, prev.to(gpu), out_g, ovf_g, 4, pred_g[0],
+               pred_g[1])
     torch.cuda.synchronize()
     same = (out_g.cpu() == out_c) | (torch.isnan(out_g.cpu()) & torch.isnan(out_c))
     assert bool(same.all())
-    assert torch.equal(age_g.cpu(), age_c)
+    assert torch.equal(age_g.cpu().to(torch.int32) & 0xFFFF, age_c)
     assert int(ovf_g.item()) == int(ovf_c.item())
+    assert torch.equal(pred_g.cpu(), pred_c) and int(pred_c[0].sum()) > 0 and int(pred_c[1].sum()) == 0
     if cap == 10:
         assert int(ovf_g.item()) > 0
 
@@ -84,7 +90,8 @@ def _run_env(rank, world, port, out, backend, n, T):
     N = world * n
     env = BatchedCrazyflieEnv(ENV_ID, n, seed=3, env_id_offset=rank * n, device=dev, max_episode_steps=41)
     obs0 = env.reset().clone()
-    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True)
+    # every env still flying at env-step 41 times out at once: the look-ahead sizes that step's capacity
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=41)
     g = torch.Generator(device=dev)
     g.manual_seed(5)
     acts = torch.rand(T, N, 4, device=dev, generator=g) * 2 - 1      # every rank holds every action
