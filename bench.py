@@ -177,6 +177,53 @@ def bytes_per_env_step(env) -> int:
     return algorithmic_bytes_per_env_step(env.cfg, outputs=BOUNDARY_OUTPUTS)
 
 
+MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md; no sparsity)
+POLICY_FLOPS_PER_ROW = 2 * (34 * 50 + 50 * 50 + 50 * 4 + 34 * 64 + 64 * 64 + 64)   # pi + V MLPs: 21 472
+
+
+def load_mfma_busy(workload_key: str):
+    """MFMA-busy fraction of the fused collect kernel (PMC SQ_VALU_MFMA_BUSY_CYCLES, tools/pmc_valu.sh),
+    used only if measured on this workload with this kernel build; otherwise None."""
+    p = os.path.join(ROOT, "profiles", "valu_issue.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        key = step_kernel_key()
+        for e in d.get("entries", []):
+            if e.get("workload") == workload_key and e.get("kernel_key") == key:
+                return (e.get("collect_kernel") or {}).get("mfma_busy_frac")
+    except (OSError, ValueError, ImportError):
+        pass
+    return None
+
+
+def secondary_roofline(hbm_bytes: float, seconds: float, valu_frac, flops: float = 0.0, mfma_busy=None) -> dict:
+    """Roofline of a throughput key other than the headline step kernel: the HBM roof (algorithmic
+    bytes / time against 8 TB/s), the vector-issue roof (PMC VALU issue fraction) and, with flops,
+    the matrix roof (useful bf16 FLOP/s against the dense peak; mfma_busy: the PMC MFMA-busy
+    fraction).  `bound` names the roof the kernel is closest to; `frac` is that fraction."""
+    gbs = hbm_bytes / seconds / 1e9
+    roofs = {"hbm": gbs / HBM_PEAK_GBS}
+    if valu_frac is not None:
+        roofs["valu"] = valu_frac
+    out = {"hbm": {"achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                   "algorithmic_bytes": hbm_bytes},
+           "valu": {"issue_frac": valu_frac, "source": "PMC SQ_INSTS_VALU (+TRANS) x 2 cycles / SIMDs / kernel cycles "
+                                                        "(tools/pmc_valu.sh -> profiles/valu_issue.json)"}}
+    if flops:
+        tf = flops / seconds / 1e12
+        out["mfma"] = {"achieved": tf, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / MFMA_BF16_PEAK_TFLOPS,
+                       "useful_flops": flops, "busy_frac": mfma_busy,
+                       "note": "useful FLOPs of the two MLPs; bf16x3 issues 3 bf16 MFMAs per product (and pads K)"}
+        roofs["mfma"] = max(tf / MFMA_BF16_PEAK_TFLOPS, mfma_busy or 0.0)
+    bound = max(roofs, key=roofs.get)
+    unit = {"hbm": "GB/s", "valu": "issue fraction", "mfma": "TFLOP/s"}[bound]
+    ach = {"hbm": gbs, "valu": valu_frac, "mfma": flops / seconds / 1e12 if flops else None}[bound]
+    peak = {"hbm": HBM_PEAK_GBS, "valu": 1.0, "mfma": MFMA_BF16_PEAK_TFLOPS}[bound]
+    out.update({"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": roofs[bound], "traffic": None})
+    return out
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -466,10 +513,16 @@ def main(argv=None):
         f1.record(stream)
         torch.cuda.synchronize()
         us = f0.elapsed_time(f1) * 1e3 / (reps * K)
+        vfr = load_valu_issue(f"{args.env_id}:N={n}")[1]
+        # per env-step of a K-step launch: the action in and the step() outputs; the state is read
+        # and written once per launch (1/K of it per env-step)
+        state_b = algorithmic_bytes_per_env_step(env.cfg, outputs=()) - 16
+        fb = 16 + (bytes_per_env_step(env) - state_b - 16) + state_b / K
         fused = {"value": n / (us * 1e-6), "unit": "env-steps/s", "us_per_env_step": us, "k": K,
                  "outputs": "obs, rew, done, trunc, cost, level per step (K slabs)",
                  # fraction of the kernel's cycles its SIMDs spend issuing VALU (PMC, tools/pmc_valu.sh)
-                 "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[1]}
+                 "valu_issue_frac": vfr, "algorithmic_bytes_per_env_step": fb,
+                 "roofline": secondary_roofline(fb * n, us * 1e-6, vfr)}
         del racts
 
     collect_line = None
@@ -487,23 +540,37 @@ def main(argv=None):
         for k in range(500):                 # past the synchronised-start transient
             cenv.step_raw(wact[k % 8].data_ptr())
         del wact
-        ro = collect(cenv, cac, T, obs=cenv.obs.clone())   # warm-up: kernels, the rollout storage's blocks
-        torch.cuda.synchronize()
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            ro = collect(cenv, cac, T, obs=ro.last_obs, out=ro)   # storage re-used, as every training epoch
-        torch.cuda.synchronize()
-        cus = (time.perf_counter() - t0) * 1e6 / (reps * T)
+        def time_collect(mode):
+            ro = collect(cenv, cac, T, obs=cenv.obs.clone(), fuse=mode)   # warm-up: kernels, storage blocks
+            torch.cuda.synchronize()
+            reps = 3
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ro = collect(cenv, cac, T, obs=ro.last_obs, out=ro, fuse=mode)   # storage re-used (every epoch)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) * 1e6 / (reps * T), cenv.last_collect_fused
+        # one launch per env-step first (cf2_collect_step), then the whole loop in one launch
+        # (cf2_collect_rollout), the collect() default
+        cus_steps, _ = time_collect("steps")
+        cus, mode = time_collect(True)
+        # per env-step: the env-step's bytes (state, action, obs, reward, done, truncation) and the
+        # policy's outputs (action, value, log-probability); the policy reads the observations from
+        # LDS and its weights from L2 (not HBM); 21.5 kFLOP of useful MLP work per row
+        cb = algorithmic_bytes_per_env_step(cenv.cfg, outputs=("obs", "rew", "done", "trunc")) + 16 + 4 + 4
+        cvf = load_valu_issue(f"{args.env_id}:N={n}")[2]
         collect_line = {"value": n / (cus * 1e-6), "unit": "env-steps/s", "us_per_env_step": cus,
+                        "algorithmic_bytes_per_env_step": cb, "flops_per_env_step": POLICY_FLOPS_PER_ROW,
+                        "roofline": secondary_roofline(cb * n, cus * 1e-6, cvf, POLICY_FLOPS_PER_ROW * n,
+                                                       load_mfma_busy(f"{args.env_id}:N={n}")),
                         "steps_per_collect": T, "policy": "MLP actor-critic 34-50-50-4 / 34-64-64-1, bf16x3",
-                        "one_launch_per_env_step": bool(cenv.last_collect_fused),
+                        "launches": {True: "one per collect (cf2_collect_rollout)",
+                                     "steps": "one per env-step (cf2_collect_step)"}.get(mode, "two per env-step"),
+                        "us_per_env_step_one_launch_per_step": cus_steps,
                         # fraction of the fused kernel's SIMD cycles issuing VALU (PMC, tools/pmc_valu.sh)
                         "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[2],
                         "includes": "env-step, policy forward + sampling, rollout storage (re-used across collects), GAE, "
                                     "time-out values"}
         cenv.close()
-        del ro
 
     streaming = None
     if world == 1 and args.streaming_ring > 0:

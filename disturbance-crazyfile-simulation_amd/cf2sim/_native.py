@@ -23,7 +23,7 @@ REPO_INCLUDE = os.path.abspath(os.path.join(PKG_DIR, "..", "..", "include", "cf2
 EXPORTED_SYMBOLS = (
     "cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
     "cf2_create", "cf2_destroy", "cf2_layout_get", "cf2_bind_hj_tables", "cf2_reset", "cf2_step", "cf2_collect_step",
-    "cf2_physics_step",
+    "cf2_collect_rollout", "cf2_physics_step",
     "cf2_set_ground_effect",
     "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
     "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
@@ -75,6 +75,8 @@ def load() -> ctypes.CDLL:
     lib.cf2_physics_step.argtypes = [vp, vp, vp, ctypes.c_float, vp]
     lib.cf2_collect_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64,
                                      ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp]
+    lib.cf2_collect_rollout.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_int,
+                                        ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]
     lib.cf2_set_ground_effect.argtypes = [vp, ctypes.c_int]
     lib.cf2_rollout.argtypes = [vp, ctypes.c_int, vp, ctypes.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.cf2_get_state.argtypes = [vp, vp, vp, vp]

@@ -370,24 +370,27 @@ class Rollout:
 def _fused_storage(steps: int, n: int, d: int, dev) -> dict:
     """The fused collect path's rollout storage: observations [T+1, N, D] (slab 0 = the start
     observation), final observations [T, N, D] (rows written where an episode ended), actions,
-    values, log-probabilities, rewards, uint8 done / truncation flags, GAE outputs and scratch for
-    the policy call on the last observation."""
+    values and log-probabilities [T+1, ...] (slab T: the policy call on the last observation),
+    rewards, uint8 done / truncation flags and the GAE outputs."""
     e = lambda *shape, dt=torch.float32: torch.empty(*shape, device=dev, dtype=dt)
-    return {"key": (steps, n, d, str(dev)), "obs": e(steps + 1, n, d), "fin": e(steps, n, d), "act": e(steps, n, 4),
-            "rew": e(steps, n), "val": e(steps, n), "logp": e(steps, n), "d8": e(steps, n, dt=torch.uint8),
-            "tr8": e(steps, n, dt=torch.uint8), "trunc_val": e(steps, n), "adv": e(steps, n), "ret": e(steps, n),
-            "disc": e(steps, n), "last_val": e(n), "a_last": e(n, 4), "lp_last": e(n)}
+    return {"key": (steps, n, d, str(dev)), "obs": e(steps + 1, n, d), "fin": e(steps, n, d),
+            "act": e(steps + 1, n, 4), "rew": e(steps, n), "val": e(steps + 1, n), "logp": e(steps + 1, n),
+            "d8": e(steps, n, dt=torch.uint8), "tr8": e(steps, n, dt=torch.uint8), "trunc_val": e(steps, n),
+            "adv": e(steps, n), "ret": e(steps, n), "disc": e(steps, n)}
 
 
 @torch.no_grad()
 def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float = 0.99,
-            lam: float = 0.95, generator: torch.Generator | None = None, fuse: bool = True,
+            lam: float = 0.95, generator: torch.Generator | None = None, fuse: bool | str = True,
             out: Rollout | None = None) -> Rollout:
     """``roll_out`` for all envs of a BatchedCrazyflieEnv at once; everything stays on the GPU.
     ``ac`` is an MLPActorCritic (torch layers) or a FusedActorCritic (HIP kernels).  With a
-    FusedActorCritic and ``fuse`` each env-step and the policy forward on its observations are one
-    launch (cf2_collect_step) where the config has a fused instance, else two launches; the
-    results are bit-identical either way.  ``out``: a Rollout of an earlier fused collect of the
+    FusedActorCritic, ``fuse`` picks how the loop's env-steps and policy calls are launched where
+    the config has fused instances: True -- all ``steps`` of them in one launch
+    (cf2_collect_rollout, the env state in registers throughout); "steps" -- one launch per
+    env-step (cf2_collect_step); False -- two launches per env-step.  The results are
+    bit-identical in every mode, and a config without fused instances runs the two launches.
+    ``out``: a Rollout of an earlier fused collect of the
     same shape whose storage is re-used (its tensors are overwritten; ``obs=out.last_obs`` is
     allowed), as a training loop collecting every epoch would.
     ``envs`` must have been created with want_final_obs=True (time-out bootstrapping)."""
@@ -403,16 +406,20 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         S = out.storage if out is not None and out.storage is not None else None
         if S is None or S["key"] != (steps, n, d, str(dev)):
             S = _fused_storage(steps, n, d, dev)
-        obs_buf, fin, buf_a, buf_r, buf_v, buf_lp = S["obs"], S["fin"], S["act"], S["rew"], S["val"], S["logp"]
-        d8, tr8, trunc_val, last_val = S["d8"], S["tr8"], S["trunc_val"], S["last_val"]
+        obs_buf, fin, act_all, buf_r, val_all, lp_all = S["obs"], S["fin"], S["act"], S["rew"], S["val"], S["logp"]
+        buf_a, buf_v, buf_lp, last_val = act_all[:steps], val_all[:steps], lp_all[:steps], val_all[steps]
+        d8, tr8, trunc_val = S["d8"], S["tr8"], S["trunc_val"]
         obs_buf[0].copy_(o)
         trunc_val.zero_()                 # read only where truncated; zero elsewhere, as the torch path
         # the policy of step t + 1 runs right behind the env-step of step t (fused: in its launch);
         # the last one gives V(obs_T), its sampled action and logp are not used
         roff = int(envs.cfg.env_id_offset)    # sampling noise keyed by the global env id
-        ac.step_into(obs_buf[0], buf_a[0], buf_v[0], buf_lp[0], row_offset=roff)
-        for t in range(steps):
-            nxt = (buf_a[t + 1], buf_v[t + 1], buf_lp[t + 1]) if t + 1 < steps else (S["a_last"], last_val, S["lp_last"])
+        ac.step_into(obs_buf[0], act_all[0], val_all[0], lp_all[0], row_offset=roff)
+        if fuse is True and not envs.collect_rollout_into(act_all, obs_buf[1:], buf_r, d8, tr8, fin, ac, val_all,
+                                                          lp_all):
+            fuse = False                       # no fused instance for this config: two launches per step
+        for t in range(steps if fuse is True else 0, steps):
+            nxt = (act_all[t + 1], val_all[t + 1], lp_all[t + 1])
             if fuse and t == 0:
                 # the first step goes through every buffer check; the later slabs have the same
                 # shapes, so the loop then passes raw pointers (slab strides) to keep ahead of the GPU
@@ -424,9 +431,8 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
                 a_p, o_p, r_p, v_p, l_p, f_p = (buf_a.data_ptr(), obs_buf.data_ptr(), buf_r.data_ptr(),
                                                 buf_v.data_ptr(), buf_lp.data_ptr(), fin.data_ptr())
                 dp, tp = d8.data_ptr(), tr8.data_ptr()
-                last = (S["a_last"].data_ptr(), last_val.data_ptr(), S["lp_last"].data_ptr())
                 for u in range(t, steps):
-                    nx = (a_p + (u + 1) * sa, v_p + (u + 1) * sf, l_p + (u + 1) * sf) if u + 1 < steps else last
+                    nx = (a_p + (u + 1) * sa, v_p + (u + 1) * sf, l_p + (u + 1) * sf)
                     if not envs.collect_step_raw(a_p + u * sa, o_p + (u + 1) * so, r_p + u * sf, dp + u * n, tp + u * n,
                                                  f_p + u * so, ac, *nx):
                         raise RuntimeError("cf2_collect_step stopped being supported inside a collect")
@@ -438,7 +444,7 @@ def collect(envs, ac, steps: int, obs: torch.Tensor | None = None, gamma: float 
         for t0 in range(0, steps, per):                      # V(final obs) of the time-outs only
             t1 = min(steps, t0 + per)
             ac.value_masked(fin[t0:t1].view(-1, d), tr8[t0:t1].view(-1), trunc_val[t0:t1].view(-1))
-        envs.last_collect_fused = fuse         # every env-step ran as one cf2_collect_step launch
+        envs.last_collect_fused = fuse         # True / "steps": every env-step ran fused (the mode that ran)
         o = obs_buf[steps]
         adv, ret, disc = gae_device(buf_r, buf_v, d8, tr8, last_val, trunc_val, gamma, lam, rew_den, True,
                                     out=(S["adv"], S["ret"], S["disc"]))

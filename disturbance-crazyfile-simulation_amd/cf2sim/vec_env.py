@@ -317,6 +317,42 @@ class BatchedCrazyflieEnv:
         self._obs_latest = None          # rollout.collect points it at the slab afterwards
         return True
 
+    def collect_rollout_into(self, act: torch.Tensor, obs_out: torch.Tensor, rew_out: torch.Tensor,
+                             done_out: torch.Tensor, trunc_out: torch.Tensor | None, final_obs_out: torch.Tensor | None,
+                             policy, val_out: torch.Tensor, logp_out: torch.Tensor) -> bool:
+        """K steps of the collect loop in one launch (cf2_collect_rollout): K = obs_out.shape[0].
+        act [K+1, N, 4]: slab 0 holds the first step's actions, slabs 1..K receive the policy's
+        samples on the observations after steps 0..K-1, with val_out / logp_out [K+1, N] (slab 0
+        untouched); obs_out [K, N, D] (slab k = the observation after step k), rew / done / trunc
+        [K, N], final_obs [K, N, D].  Bit-identical to K collect_step_into calls.  Returns False,
+        having launched nothing, where no fused instance is built."""
+        K = int(obs_out.shape[0])
+        n, od, dev = self.num_envs, self.obs_dim, self.device
+        _check_buf(act, "act", (K + 1, n, 4), torch.float32, dev, 16)
+        _check_buf(obs_out, "obs_out", (K, n, od), torch.float32, dev, 8)
+        _check_buf(rew_out, "rew_out", (K, n), torch.float32, dev)
+        _check_buf(done_out, "done_out", (K, n), torch.uint8, dev, 1)
+        _check_buf(trunc_out, "trunc_out", (K, n), torch.uint8, dev, 1)
+        _check_buf(final_obs_out, "final_obs_out", (K, n, od), torch.float32, dev, 8)
+        _check_buf(val_out, "val_out", (K + 1, n), torch.float32, dev)
+        _check_buf(logp_out, "logp_out", (K + 1, n), torch.float32, dev)
+        if self.cfg.disturbance == DSTB_EXTERNAL:
+            raise ValueError("this env takes an external disturbance tensor: use step(actions, dstb)")
+        if policy.obs_dim != od:
+            raise ValueError(f"policy obs_dim {policy.obs_dim} != env obs_dim {od}")
+        st = self.lib.cf2_collect_rollout(
+            self._ctx, K, act.data_ptr(), obs_out.data_ptr(), rew_out.data_ptr(), done_out.data_ptr(),
+            _native.ptr(trunc_out), _native.ptr(final_obs_out), policy.w.data_ptr(), od, policy.prec, policy.seed,
+            policy.counter & 0xFFFFFFFF, int(self.cfg.env_id_offset), val_out.data_ptr(), logp_out.data_ptr(),
+            self.stream)
+        if st == _native.CF2_ERR_UNSUPPORTED:
+            return False
+        _native.check(st, "cf2_collect_rollout")
+        policy.counter += K
+        self._state_version += 1
+        self._obs_latest = obs_out[K - 1]
+        return True
+
     def rollout(self, actions: torch.Tensor, obs_out: torch.Tensor | None = None, rew_out=None, done_out=None,
                 trunc_out=None, cost_out=None, level_out=None, final_obs_out=None):
         """K env-steps in one fused launch (cf2_rollout): actions [K, N, 4]; returns (obs [K, N, D],

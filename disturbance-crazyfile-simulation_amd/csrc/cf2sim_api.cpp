@@ -367,6 +367,27 @@ int cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* 
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
+int cf2_collect_rollout(cf2_ctx* ctx, int K, float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
+                        uint8_t* trunc_dev, float* final_obs_dev, const float* packed_dev, uint32_t obs_dim,
+                        int precision, uint64_t seed, uint32_t counter, uint32_t row_offset, float* val_dev,
+                        float* logp_dev, void* stream) {
+    if (!ctx || K < 1 || !act_dev || !obs_dev || !rew_dev || !done_dev || !packed_dev || !val_dev || !logp_dev)
+        return CF2_ERR_INVALID_ARG;
+    if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL || ctx->P.ground_effect) return CF2_ERR_UNSUPPORTED;
+    if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
+    if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 7u) != 0 || ((uintptr_t)packed_dev & 15u) != 0)
+        return CF2_ERR_INVALID_ARG;
+    if (final_obs_dev && ((uintptr_t)final_obs_dev & 7u) != 0) return CF2_ERR_INVALID_ARG;
+    const uint32_t od = ctx->P.noise ? 34u : 42u;
+    if (obs_dim != od) return CF2_ERR_INVALID_ARG;
+    if (precision != CF2_POLICY_BF16X3 || od != 34u) return CF2_ERR_UNSUPPORTED;
+    StepIO io{ctx->sf, act_dev, nullptr, obs_dev, rew_dev, done_dev, trunc_dev, nullptr, nullptr, final_obs_dev};
+    PolicyIO pio{packed_dev, (uint32_t)seed, (uint32_t)(seed >> 32), counter, row_offset, act_dev, val_dev, logp_dev};
+    const hipError_t e = launch_collect_rollout(ctx->P, io, pio, (uint32_t)K, (hipStream_t)stream);
+    if (e == hipErrorNotSupported) return CF2_ERR_UNSUPPORTED;
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
 int cf2_physics_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float time_step, void* stream) {
     if (!ctx || !act_dev || ((uintptr_t)act_dev & 15u) != 0) return CF2_ERR_INVALID_ARG;
     if (!(time_step < 1.0f)) return CF2_ERR_INVALID_ARG;       // NaN or absurd step

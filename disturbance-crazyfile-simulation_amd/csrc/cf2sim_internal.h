@@ -84,10 +84,10 @@ struct KParams {
     uint32_t late_block;          // step kernel: first block index past one residency round (set per launch)
     uint32_t out_stride;          // rollout kernel: rows per per-step output slab (set per launch)
     // host-side, set once at cf2_create for the context's device and configuration: blocks
-    // resident at once of the large-N step / fused rollout / fused collect kernels
-    // (query_occupancy), and whether the step's working set exceeds the Infinity Cache
+    // resident at once of the large-N step / fused rollout / fused collect / collect rollout
+    // kernels (query_occupancy), and whether the step's working set exceeds the Infinity Cache
     // (nt state stores)
-    uint32_t rb_step, rb_roll, rb_collect, nt_state;
+    uint32_t rb_step, rb_roll, rb_collect, rb_croll, nt_state;
     int32_t agg, obs_rate, buf_size, use_latency, use_motor_dyn, max_steps, auto_reset, reset_dist;
     int32_t dstb_mode, level_mode, num_levels, gust_dur, noise, dr, phys, held_persistent, need_level;
     float time_step, mass, ixx, iyy, izz, ft0, ft1, K, A, B, hover_x, hover_action, ou_sigma;
@@ -155,6 +155,11 @@ struct PolicyIO {
 // returns hipErrorNotSupported when the config has no fused instance (the caller then launches
 // cf2_step and cf2_policy_forward)
 hipError_t launch_collect(const KParams& P, const StepIO& io, const PolicyIO& pio, hipStream_t s);
+// K steps of the collect loop in one launch (collect_rollout_kernel): env-step k reads the actions
+// at pio.act + k * N * 4 and writes io's k-th [N, ...] slabs (obs, rew, done, trunc, final_obs);
+// the policy on its observations writes slab k + 1 of pio.act / pio.val / pio.logp ([K + 1][N]),
+// noise counter pio.counter + k.  hipErrorNotSupported where collect_kernel has no instance.
+hipError_t launch_collect_rollout(const KParams& P, const StepIO& io, const PolicyIO& pio, uint32_t K, hipStream_t s);
 // K fused env-steps (state in registers); outputs [K][N][...] slabs, actions at act + k * act_stride
 hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s);
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s);

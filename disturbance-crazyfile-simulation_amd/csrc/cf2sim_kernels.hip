@@ -116,13 +116,16 @@ __device__ __forceinline__ void normals(const RowRng<STRIDE>& g, uint32_t b0, fl
 }
 
 // The small-N kernel's helper-drawn env-step randomness ([word][env] in LDS, stride 64): what the
-// env-step draws after its first physics sub-step in the reference-default shape (SPEC 1 with
-// sensor noise), with Box-Muller already applied to the words that become normals:
+// env-step draws from its first sensor call on in the reference-default shape (SPEC 1 with sensor
+// noise), with Box-Muller already applied to the words that become normals:
 //   words  0-3   OU normals of sub-step 1              (step block 2)
 //   words  4-12  gyro normals of sub-step 1's call      (normals<9> at block 16: blocks 16-18)
 //   words 13-30  final sensor call's 18 normals         (normals<18> at block 24: blocks 24-28)
 //   words 31-36  its uniform words: block 28 .z .w, block 29 .x .y .z .w
-enum { HD_WORDS = 37, HD_OU1 = 0, HD_GYRO1 = 4, HD_FINAL = 13 };
+//   words 37-45  gyro normals 6-14 of sub-step 0's call (normals_range<6, 15> at block 8: blocks 9-11;
+//                the call is a full one whose held part is dead, compute_observation)
+// The env wave joins the helpers' LDS barrier before that first sensor call.
+enum { HD_WORDS = 46, HD_OU1 = 0, HD_GYRO1 = 4, HD_FINAL = 13, HD_GYRO0 = 37 };
 
 // Normals LO..HI-1 of the sequence normals<N>(g, b0, .) would produce, drawing only the Philox
 // blocks and Box-Muller pairs that cover them (the stream positions of all other draws are
@@ -154,9 +157,64 @@ __device__ __forceinline__ void normals_range(const TableRng& g, uint32_t b0, fl
     }
 }
 
+// The small-N kernels' helper waves 1-3 draw the env-step's randomness of the HD_* layout for the
+// env of their lane (d = its column of the [word][env] LDS table, stride 64), the step counter ctr
+// known from the state.  Sub-step 0's gyro normals first: the env wave needs them earliest.
+__device__ __forceinline__ void helper_step_draws(const Keys& K, uint32_t ctr, uint32_t gid, uint32_t wave, float* d) {
+    const RngT<Keys> g{K, ctr, gid, TAG_STEP};
+    auto bm4 = [&](uint32_t blk, int w) {          // 4 normals of one block -> words w..w+3
+        const U4 u = g.block(blk);
+        float z0, z1, z2, z3;
+        box_muller(u.x, u.y, z0, z1);
+        box_muller(u.z, u.w, z2, z3);
+        d[(w + 0) * 64] = z0; d[(w + 1) * 64] = z1; d[(w + 2) * 64] = z2; d[(w + 3) * 64] = z3;
+    };
+    if (wave == 1) {
+        bm4(2, HD_OU1);                             // OU of sub-step 1
+        bm4(16, HD_GYRO1);                          // sub-step 1 sensor call: normals 0-8
+        bm4(17, HD_GYRO1 + 4);
+        const U4 u = g.block(18);
+        float z0, z1;
+        box_muller(u.x, u.y, z0, z1);
+        d[(HD_GYRO1 + 8) * 64] = z0;
+    } else if (wave == 2) {
+        {
+            const U4 u = g.block(9);                // sub-step 0 sensor call: normals 6-7
+            float z2, z3;
+            box_muller(u.z, u.w, z2, z3);
+            d[(HD_GYRO0 + 0) * 64] = z2; d[(HD_GYRO0 + 1) * 64] = z3;
+        }
+        bm4(24, HD_FINAL);                          // final sensor call: normals 0-11
+        bm4(25, HD_FINAL + 4);
+        bm4(26, HD_FINAL + 8);
+    } else {
+        bm4(10, HD_GYRO0 + 2);                      // sub-step 0 sensor call: normals 8-11
+        {
+            const U4 u = g.block(11);               // normals 12-14
+            float z0, z1, z2, z3;
+            box_muller(u.x, u.y, z0, z1);
+            box_muller(u.z, u.w, z2, z3);
+            d[(HD_GYRO0 + 6) * 64] = z0; d[(HD_GYRO0 + 7) * 64] = z1; d[(HD_GYRO0 + 8) * 64] = z2;
+            (void)z3;
+        }
+        bm4(27, HD_FINAL + 12);                     // normals 12-15
+        const U4 u = g.block(28), v = g.block(29);
+        float z0, z1;
+        box_muller(u.x, u.y, z0, z1);               // normals 16-17, then the six uniform words
+        d[(HD_FINAL + 16) * 64] = z0; d[(HD_FINAL + 17) * 64] = z1;
+        d[(HD_FINAL + 18) * 64] = __uint_as_float(u.z); d[(HD_FINAL + 19) * 64] = __uint_as_float(u.w);
+        d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
+        d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // rotation helpers (PyBullet C-API semantics)
 // ------------------------------------------------------------------------------------
+// DIV_NOTE: a division by a constant, x / c, is compiled (fp32, -fno-hip-fp32-correctly-rounded-
+// divide-sqrt) as frexp(x), mantissa * rn(1 / c) scaled to [1, 2), ldexp: five VALU, and for every
+// normal x bit-identical to x * rn(1 / c) (scaling by a power of two commutes with rounding), which
+// is one.  The env-step divides by constants 19 times (PWM, rpm, the done test): written as products.
 // v_rcp_f32 / v_rsq_f32 (1 ulp) for well-scaled operands (no denormal pre-scaling)
 __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float rsq(float x) { return __builtin_amdgcn_rsqf(x); }
@@ -390,21 +448,23 @@ __device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, u
 // has no fence semantics the compiler could move memory operations around.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// write_obs_rows for the small-N kernel: row r comes from rrow (the reset observations the helper
-// waves staged) where bit r of mask is set, else from obs (the env-step's observations)
+// One wave's part of the small-N kernel's write-out of its 64 obs rows: the float4 chunks that touch
+// a row whose bit in mask is set (dirty: the reset observations the helper waves staged in rrow) or
+// those that do not (from obs, the env-step's observations).  A chunk straddling a reset and a
+// non-reset row is a dirty chunk, merged from both.
 template <uint32_t OD>
-__device__ __forceinline__ void write_obs_rows_merged(float* dst, const float* s_obs, const float* s_rrow, uint64_t mask,
-                                                      uint32_t nvalid, uint32_t tid, uint32_t nthreads) {
+__device__ __forceinline__ void write_obs_rows_part(float* dst, const float* s_obs, const float* s_rrow, uint64_t mask,
+                                                    uint32_t nvalid, uint32_t lane, bool dirty) {
     typedef float f4x __attribute__((ext_vector_type(4)));
     typedef float f2x __attribute__((ext_vector_type(2)));
     if (nvalid == 64u && (64u * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
         const f4x* a4 = reinterpret_cast<const f4x*>(s_obs);
         const f4x* b4 = reinterpret_cast<const f4x*>(s_rrow);
         f4x* dst4 = reinterpret_cast<f4x*>(dst);
-        for (uint32_t k = tid; k < 64u * OD / 4; k += nthreads) {
-            // the chunk's 4 floats lie in row r0, or straddle rows r0 and r0 + 1 (OD > 4)
+        for (uint32_t k = lane; k < 64u * OD / 4; k += 64u) {
             const uint32_t r0 = 4u * k / OD, r1 = (4u * k + 3u) / OD;
             const bool s0 = (mask >> r0) & 1ull, s1 = (mask >> r1) & 1ull;
+            if ((s0 || s1) != dirty) continue;
             f4x v = (s0 ? b4 : a4)[k];
             if (s0 != s1) {
                 const f4x w = (s1 ? b4 : a4)[k];
@@ -419,10 +479,10 @@ __device__ __forceinline__ void write_obs_rows_merged(float* dst, const float* s
         const f2x* a2 = reinterpret_cast<const f2x*>(s_obs);
         const f2x* b2 = reinterpret_cast<const f2x*>(s_rrow);
         f2x* dst2 = reinterpret_cast<f2x*>(dst);
-        for (uint32_t k = tid; k < nvalid * OD / 2; k += nthreads) {
-            f2x v = a2[k];
-            if ((mask >> ((2u * k) / OD)) & 1ull) v = b2[k];      // OD is even: a pair never spans rows
-            __builtin_nontemporal_store(v, dst2 + k);
+        for (uint32_t k = lane; k < nvalid * OD / 2; k += 64u) {
+            const bool sr = (mask >> ((2u * k) / OD)) & 1ull;      // OD is even: a pair never spans rows
+            if (sr != dirty) continue;
+            __builtin_nontemporal_store((sr ? b2 : a2)[k], dst2 + k);
         }
     }
 }
@@ -689,7 +749,7 @@ __device__ __forceinline__ void apply_action(const KParams& P, Env& E, const flo
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float tn = pwm[j] / 60000.0f;
+        const float tn = pwm[j] * (1.0f / 60000.0f);      // == pwm / 60000 as compiled (see DIV_NOTE)
         float noisy;
         if (P.use_motor_dyn) {
             // x(k+1) = A x(k) + B u with A = 1 - B (agents.py:288), evaluated as x += B (u - x) on the
@@ -731,7 +791,7 @@ __device__ __forceinline__ void bullet_substep(const KParams& P, Env& E, const f
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const float rpm = E.x[j] * E.x[j] * 25000.0f;
-        ssum += 2.0f * 3.141592653589793f * rpm / 60.0f;
+        ssum += 2.0f * 3.141592653589793f * rpm * (1.0f / 60.0f);     // DIV_NOTE
     }
     const float dl[3] = {-1.0f * P.drag_xy * ssum * E.v[0], -1.0f * P.drag_xy * ssum * E.v[1], -1.0f * P.drag_z * ssum * E.v[2]};
     float drag1[3], dragw[3];
@@ -975,7 +1035,7 @@ __device__ __forceinline__ bool compute_done(const KParams& P, const Env& E) {
     const bool rp = fabsf(E.rpy[0]) > P.done_rp || fabsf(E.rpy[1]) > P.done_rp;
     bool rt = false;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) rt |= (180.0f * fabsf(E.wb[k]) / 3.141592653589793f) > P.done_rate_deg;
+    for (int k = 0; k < 3; ++k) rt |= (180.0f * fabsf(E.wb[k]) * (1.0f / 3.141592653589793f)) > P.done_rate_deg;   // DIV_NOTE
     return rp || rt || (E.p[2] < P.done_zmin);
 }
 
@@ -1336,8 +1396,11 @@ enum { SEED_WORDS = 13 };
 // state as soon as it is final, the rest at the end); the fused rollout keeps it in registers.
 // HD (small-N kernel, reference-default shape with sensor noise): the draws after the first
 // sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
-// env wave joins the helpers' LDS barrier before its second sub-step.
-template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0>
+// env wave joins the helpers' LDS barrier before its second sub-step.  ROW_SCRATCH: obs_row is
+// this lane's LDS row, which also stages the final sensor call's draws (pre_final); the fused
+// collect rollout writes its rows straight to global memory and draws them inline (same blocks).
+template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0,
+          bool ROW_SCRATCH = true>
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
                                               float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
                                               const float* hd = nullptr) {
@@ -1351,7 +1414,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     const Keys K = make_keys(P.key0, P.key1);
     const Rng g{K, E.rng, gid, TAG_STEP};
     // reference-default shape: the final (full) sensor call's blocks are drawn up front (RowRng)
-    const bool pre_final = !HD && NOISE && P.agg == 2 && P.obs_rate == 2;
+    const bool pre_final = ROW_SCRATCH && !HD && NOISE && P.agg == 2 && P.obs_rate == 2;
     const uint32_t* hdw = reinterpret_cast<const uint32_t*>(hd);
     const uint32_t fbase = 8u + 8u * (uint32_t)P.agg;
     if (pre_final) {
@@ -1446,12 +1509,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
 #pragma unroll 4
     for (int s = 0; s < P.agg; ++s) {
         float on[4];
-        if (HD && s == 1) {
-            lds_barrier();                                   // the helper waves' draws are in LDS
-            normals<4>(RowRng<64>{hdw + HD_OU1 * 64, 2}, 2, on);
-        } else {
-            normals<4>(g, 1 + s, on);
-        }
+        if (HD && s == 1) normals<4>(RowRng<64>{hdw + HD_OU1 * 64, 2}, 2, on);
+        else normals<4>(g, 1 + s, on);
         float dw = 0.0f;
         if (PHYS == PHYS_BULLET_T && P.num_drones > 1 && P.downwash_on)
             dw = downwash(P, E.p, gid % (uint32_t)P.num_drones);   // mates' positions before this sub-step
@@ -1460,10 +1519,18 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         float dummy[17];
         // a sub-step's held measurement reaches an observation only if the final measurement
         // of the env-step is not a full one (aggregate_phy_steps % obs_rate != 0)
-        if (HD && s == 1)
+        if (HD && s == 0) {
+            // compute_observation of this full call with its held part dead: the gyro update alone
+            lds_barrier();                                   // the helper waves' draws are in LDS
+            float ng[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) ng[k] = hd[(HD_GYRO0 + k) * 64];
+            gyro_update(P, E, ng);
+        } else if (HD && s == 1) {
             compute_observation<NOISE>(P, E, RowRng<64>{hdw + HD_GYRO1 * 64, 16}, 16, E.ep_step * P.agg + s, dummy, false);
-        else
+        } else {
             compute_observation<NOISE>(P, E, g, 8 + 8 * s, E.ep_step * P.agg + s, dummy, P.held_persistent != 0);
+        }
     }
     // the history (o_{k-1}, last actions) is only read by compute_history: the one-step kernel
     // loads it after the physics, so its 21 registers are not live across the sub-steps (the final
@@ -1478,7 +1545,11 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         const RowRng<1> gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
         compute_observation<NOISE>(P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
     } else {
-        compute_observation<NOISE>(P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
+        // without the staged draws: an opaque copy of the counter keeps the final call's Philox
+        // blocks from being hoisted into the sub-steps, where their results would stay live
+        uint32_t ctr = E.rng;
+        if (!ROW_SCRATCH) asm volatile("" : "+v"(ctr));
+        compute_observation<NOISE>(P, E, Rng{K, ctr, gid, TAG_STEP}, fbase, (E.ep_step + 1) * P.agg, onx);
     }
     const bool term = compute_done(P, E);
     E.ep_step += 1;
@@ -2028,39 +2099,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     if (HD && wave != 0) {
         // the env-step's draws after sub-step 0 (step tag, the env's counter), split over the
         // three helper waves; Box-Muller applied where the env-step turns words into normals
-        if (live) {
-            const Rng g{K, ctr, gid, TAG_STEP};
-            float* d = s_draw + lane;
-            auto bm4 = [&](uint32_t blk, int w) {          // 4 normals of one block -> words w..w+3
-                const U4 u = g.block(blk);
-                float z0, z1, z2, z3;
-                box_muller(u.x, u.y, z0, z1);
-                box_muller(u.z, u.w, z2, z3);
-                d[(w + 0) * 64] = z0; d[(w + 1) * 64] = z1; d[(w + 2) * 64] = z2; d[(w + 3) * 64] = z3;
-            };
-            if (wave == 1) {
-                bm4(2, HD_OU1);                             // OU of sub-step 1
-                bm4(16, HD_GYRO1);                          // sub-step 1 sensor call: normals 0-8
-                bm4(17, HD_GYRO1 + 4);
-                const U4 u = g.block(18);
-                float z0, z1;
-                box_muller(u.x, u.y, z0, z1);
-                d[(HD_GYRO1 + 8) * 64] = z0;
-            } else if (wave == 2) {
-                bm4(24, HD_FINAL);                          // final sensor call: normals 0-11
-                bm4(25, HD_FINAL + 4);
-                bm4(26, HD_FINAL + 8);
-            } else {
-                bm4(27, HD_FINAL + 12);                     // normals 12-15
-                const U4 u = g.block(28), v = g.block(29);
-                float z0, z1;
-                box_muller(u.x, u.y, z0, z1);               // normals 16-17, then the six uniform words
-                d[(HD_FINAL + 16) * 64] = z0; d[(HD_FINAL + 17) * 64] = z1;
-                d[(HD_FINAL + 18) * 64] = __uint_as_float(u.z); d[(HD_FINAL + 19) * 64] = __uint_as_float(u.w);
-                d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
-                d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
-            }
-        }
+        if (live) helper_step_draws(K, ctr, gid, wave, s_draw + lane);
         TSTAMP(10);      // helper: step draws in LDS
         lds_barrier();   // joined by the env wave before its second sub-step (step_env_body)
         TSTAMP(11);
@@ -2162,10 +2201,15 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
         }
         if (wave == PARAMS_WAVE) store_reset_params<DR>(P, T, H);
     }
-    lds_barrier();
-    TSTAMP(12);  // reset rows in LDS
-    write_obs_rows_merged<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, P.N - base < 64u ? P.N - base : 64u,
-                              tid, 256u);
+    // the block's obs rows: the chunks of rows whose env did not reset by the env wave (done with
+    // its env-step), the chunks touching a reset row by wave 2 once it has completed those rows (its
+    // own LDS writes precede its reads; with sensor noise it writes the rows' gyro-LPF triples above).
+    // No second barrier: the two sets are disjoint (measured against a block barrier followed by a
+    // 256-thread merged write-out: see DESIGN.md section 3).
+    const uint32_t nvalid = P.N - base < 64u ? P.N - base : 64u;
+    if (wave == 0) write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, false);
+    else if (wave == 2) write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, true);
+    TSTAMP(12);  // rows written
 #ifdef CF2_TIMING
     TSTAMP(5);
     if (uint64_t* r = timing_row())
@@ -2209,7 +2253,8 @@ __global__ void __launch_bounds__(256, 2) collect_kernel_small(KParams P0, StepI
         reinterpret_cast<uint32_t*>(s_mem + SL::O_MASK), reinterpret_cast<double*>(s_mem + SL::O_HJ),
         s_mem + SL::O_DRAW);
     // ---- policy phase: wave w takes rows 16 w .. 16 w + 15 of the block (lane l: row 16 w + (l & 15),
-    // inputs 8 g .. 8 g + 7 and 32 + g)
+    // inputs 8 g .. 8 g + 7 and 32 + g), once wave 2 has completed the reset rows
+    lds_barrier();
     const uint32_t tid = threadIdx.x, l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
     const int g = (int)(l >> 4);
     const uint32_t br = 16u * wv + r16, base = blockIdx.x * 64u, row = base + br;
@@ -2296,6 +2341,63 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
     T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
 }
 
+// The fused rollouts' auto-resets (rollout_kernel, collect_rollout_kernel): the block lists its
+// finished envs, draws their reset tables block-parallel as step_kernel does, and each env is
+// then reset in place by its own lane (its state is in that lane's registers); the reset
+// observation goes to row (this lane's LDS row or its global obs row).  Begins and ends with a
+// block barrier; s_cnt was zeroed before the first one.
+template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C>
+__device__ __forceinline__ void rollout_resets(const KParams& P, Env& E, uint32_t base, uint32_t tid, uint32_t i,
+                                               bool do_reset, const ResetSeed& rs, uint32_t* s_cnt,
+                                               uint32_t* s_list, uint32_t* s_ctr, uint32_t* s_rand, float* row) {
+    constexpr int OD = NOISE ? 34 : 42;
+    __syncthreads();             // s_cnt initialised
+    uint32_t pos = 0;
+    const uint64_t m = __ballot(do_reset);
+    if (m) {
+        const int lane = (int)(threadIdx.x & 63);
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        if (lane == leader) pos = atomicAdd(s_cnt, (uint32_t)__popcll(m));
+        pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (do_reset) { s_list[pos] = tid; s_ctr[pos] = rs.ctr; }
+    }
+    __syncthreads();
+    const uint32_t cnt = *s_cnt;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
+        const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
+        {
+            const Keys Kk = make_keys(P.key0, P.key1);
+            for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
+                const uint32_t sl = w / nc, e = w - sl * nc, p2 = c0 + e;
+                U4 u = philox(Kk, reset_block_of_slot((int)sl), s_ctr[p2], P.gid_off + base + s_list[p2], TAG_RESET);
+                if (reset_slot_normal_xy((int)sl)) {
+                    float z0, z1;
+                    box_muller(u.x, u.y, z0, z1);
+                    u.x = __float_as_uint(z0); u.y = __float_as_uint(z1);
+                }
+                if (reset_slot_normal_zw((int)sl)) {
+                    float z2, z3;
+                    box_muller(u.z, u.w, z2, z3);
+                    u.z = __float_as_uint(z2); u.w = __float_as_uint(z3);
+                }
+                uint32_t* q = s_rand + sl * 4 * C + e;
+                q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
+            }
+        }
+        __syncthreads();
+        if (do_reset && pos >= c0 && pos < c0 + nc) {
+            // reset_env keeps what a reset inherits from the finished episode (stale body rates,
+            // gyro bias, OU state, level) from E itself
+            float o[OD];
+            const TableRng tg{s_rand + (pos - c0), C};
+            reset_env<NOISE, DR, PHYS, /*TAB=*/true>(P, E, tg, P.gid_off + i, o);
+#pragma unroll
+            for (int q = 0; q < OD; q += 2) *reinterpret_cast<float2*>(row + q) = make_float2(o[q], o[q + 1]);
+        }
+        __syncthreads();         // the next chunk reuses s_rand
+    }
+}
+
 // Fused K-step rollout (cf2_rollout): the env state is loaded once, stays in registers for K
 // env-steps and is stored once.  Step k reads its actions at act + k * act_stride and writes its
 // outputs into the k-th [N, ...] slab of each output (obs, rew, done, trunc, cost, level,
@@ -2343,55 +2445,115 @@ __global__ void __launch_bounds__(STEP_BLOCK, ROLL_MIN_WAVES) rollout_kernel(KPa
         bool do_reset = false;
         ResetSeed rs;
         if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false>(P, io, i, E, obs_row, rs, s_hjgrid);
-        __syncthreads();             // s_cnt initialised
-        uint32_t pos = 0;
-        const uint64_t m = __ballot(do_reset);
-        if (m) {
-            const int lane = (int)(threadIdx.x & 63);
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            if (lane == leader) pos = atomicAdd(&s_cnt, (uint32_t)__popcll(m));
-            pos = __shfl(pos, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (do_reset) { s_list[pos] = tid; s_ctr[pos] = rs.ctr; }
-        }
-        __syncthreads();
-        const uint32_t cnt = s_cnt;
-        for (uint32_t c0 = 0; c0 < cnt; c0 += C) {
-            const uint32_t nc = cnt - c0 < C ? cnt - c0 : C;
-            {
-                const Keys Kk = make_keys(P.key0, P.key1);
-                for (uint32_t w = tid; w < nc * RESET_SLOTS; w += B) {
-                    const uint32_t sl = w / nc, e = w - sl * nc, p2 = c0 + e;
-                    U4 u = philox(Kk, reset_block_of_slot((int)sl), s_ctr[p2], P.gid_off + base + s_list[p2], TAG_RESET);
-                    if (reset_slot_normal_xy((int)sl)) {
-                        float z0, z1;
-                        box_muller(u.x, u.y, z0, z1);
-                        u.x = __float_as_uint(z0); u.y = __float_as_uint(z1);
-                    }
-                    if (reset_slot_normal_zw((int)sl)) {
-                        float z2, z3;
-                        box_muller(u.z, u.w, z2, z3);
-                        u.z = __float_as_uint(z2); u.w = __float_as_uint(z3);
-                    }
-                    uint32_t* q = s_rand + sl * 4 * C + e;
-                    q[0] = u.x; q[C] = u.y; q[2 * C] = u.z; q[3 * C] = u.w;
-                }
-            }
-            __syncthreads();
-            if (do_reset && pos >= c0 && pos < c0 + nc) {
-                // in place on this lane's registers: reset_env keeps what a reset inherits from the
-                // finished episode (stale body rates, gyro bias, OU state, level) from E itself
-                float o[OD];
-                const TableRng tg{s_rand + (pos - c0), C};
-                reset_env<NOISE, DR, PHYS, /*TAB=*/true>(P, E, tg, P.gid_off + i, o);
-#pragma unroll
-                for (int q = 0; q < OD; q += 2) *reinterpret_cast<float2*>(obs_row + q) = make_float2(o[q], o[q + 1]);
-            }
-            __syncthreads();         // the next chunk reuses s_rand
-        }
+        rollout_resets<NOISE, DR, PHYS, B, C>(P, E, base, tid, i, do_reset, rs, &s_cnt, s_list, s_ctr, s_rand, obs_row);
         // coalesced write of the block's obs rows into step k's slab
         write_obs_rows(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs, P.N - base < EPB ? P.N - base : EPB,
                        EPB, OD, tid, B);
         __syncthreads();             // the write-out read s_obs before the next step's rows
+    }
+    if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
+}
+
+// K steps of the collect loop in one launch (cf2_collect_rollout): per
+// step the env-step of rollout_kernel (state in registers for all K steps) and then, on the
+// block's new observations, the actor-critic forward and sampling of collect_kernel, whose actions
+// the next step reads.  It replaces K iterations of IWPGAlgorithm.roll_out's env.step + ac.step
+// (algs/iwpg/iwpg.py:372-410, ActorCritic.step algs/core.py:371-395) and its outputs are
+// bit-identical to K cf2_collect_step launches (same device code for both halves).
+//   * LDS holds every packed fragment (layer 3 included, 60.8 KB), staged once per launch, plus the
+//     reset tables; 2 blocks per CU (2 x 75 KB), so one block's policy phase runs beside the other
+//     block's env phase on the CU;
+//   * there is no LDS row buffer: each lane writes its obs row straight into step k's slab (the
+//     final sensor call's draws are made inline instead of being staged in that row), and after a
+//     block barrier each wave reads its 64 rows back from there (L2) as MFMA operands;
+//   * the policy phase: per wave 4 row tiles of 16 rows, policy_standardize / policy_layers /
+//     policy_emit_eps of cf2sim_policy.h, the noise of row 64 wv + l drawn by lane l.
+// Envs run in slices that fit one residency round (launch_collect_rollout_t), as cf2_rollout.
+constexpr uint32_t CROLL_MIN_WAVES = 2;
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(STEP_BLOCK, CROLL_MIN_WAVES) collect_rollout_kernel(KParams P0, StepIO io0,
+                                                                                     PolicyIO pio, uint32_t K) {
+    static_assert(NOISE, "the fused collect kernels are built for the 34-wide observation");
+    const KParams P = shape_view<SPEC>(P0);
+    constexpr int OD = 34;
+    constexpr uint32_t B = STEP_BLOCK, C = RESET_CHUNK;
+    using PK = Packed<OD, CF2_POLICY_BF16X3>;
+    static_assert(PK::TOTAL % 4 == 0, "float4 staging");
+    __shared__ __align__(16) float s_frag[PK::TOTAL];
+    __shared__ uint32_t s_list[B];
+    __shared__ uint32_t s_ctr[B];
+    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];
+    __shared__ uint32_t s_cnt;
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    {
+        const float4* src = reinterpret_cast<const float4*>(pio.w);
+        float4* dst = reinterpret_cast<float4*>(s_frag);
+        for (uint32_t q = tid; q < PK::TOTAL / 4; q += B) dst[q] = src[q];
+    }
+    const bool live = i < P.N;
+    Env E;
+    if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, P.need_level, /*with_hist=*/true);
+    const size_t n = P0.out_stride;              // rows per output slab (the whole population)
+    const uint32_t l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
+    const int g = (int)(l >> 4);
+    const uint32_t nrows = P.N - base < B ? P.N - base : B;      // rows of this block (> 0)
+    for (uint32_t k = 0; k < K; ++k) {
+        if (tid == 0) s_cnt = 0;     // every reader of the previous step passed its last barrier
+        StepIO io = io0;
+        io.act = pio.act + (size_t)k * n * 4;
+        io.obs = io0.obs + (size_t)k * n * OD;
+        io.rew = io0.rew + (size_t)k * n;
+        io.done = io0.done + (size_t)k * n;
+        if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
+        if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+        float* row = io.obs + (size_t)i * OD;
+        bool do_reset = false;
+        ResetSeed rs;
+        if (live)
+            do_reset = step_env_body<NOISE, DR, PHYS, false, false, false, 0, /*ROW_SCRATCH=*/false>(P, io, i, E, row, rs,
+                                                                                                  s_hjgrid);
+        rollout_resets<NOISE, DR, PHYS, B, C>(P, E, base, tid, i, do_reset, rs, &s_cnt, s_list, s_ctr, s_rand, row);
+        // (the last barrier of rollout_resets orders every row write of the block before the reads)
+        // ---- policy phase: lane l of wave wv, row tile c: row 64 wv + 16 c + (l & 15), inputs
+        // 8 g .. 8 g + 7 and 32 + g (as collect_kernel)
+        float ep[4];
+        policy_noise(pio.key0, pio.key1, pio.counter + k, pio.row_offset + base + 64u * wv + l, ep);
+        PolicyLane<OD, CF2_POLICY_BF16X3> CL;
+        policy_lane_init<OD, CF2_POLICY_BF16X3>(s_frag + PK::O_BIAS, g, CL);
+        float* act_out = pio.act + (size_t)(k + 1) * n * 4;
+        float* val_out = pio.val + (size_t)(k + 1) * n;
+        float* logp_out = pio.logp + (size_t)(k + 1) * n;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t wr = 16u * (uint32_t)c + r16, r = 64u * wv + wr;
+            ObsRegs<OD, CF2_POLICY_BF16X3, 1> Xc;
+            {
+                const float* src = io.obs + (size_t)(base + __builtin_elementwise_min(r, nrows - 1u)) * OD;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float2 v = *reinterpret_cast<const float2*>(src + 8 * g + 2 * q);
+                    Xc.x8[0][0][2 * q] = v.x;
+                    Xc.x8[0][0][2 * q + 1] = v.y;
+                }
+                Xc.x1[0][0] = src[__builtin_elementwise_min(32 + g, OD - 1)];
+            }
+            int off = 0;
+            asm volatile("" : "+v"(off));        // keep the fragment reads inside the loop (policy_kernel)
+            const float* sw = s_frag + off;
+            policy_standardize<OD, CF2_POLICY_BF16X3, 1>(sw + PK::O_BIAS, g, CL, Xc);
+            f4v o[1];
+            policy_layers<OD, CF2_POLICY_BF16X3, 0, 1>(sw, sw + PK::O_BIAS, sw + PK::O_L3, (int)l, Xc, o);
+            float e[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)          // row wr's noise from lane wr
+                e[q] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(wr << 2), __float_as_int(ep[q])));
+            if (r < nrows)
+                policy_emit_eps<OD, CF2_POLICY_BF16X3, 0>(o[0], base + r, g, CL, e, 1, act_out, val_out, logp_out,
+                                                          nullptr);
+        }
+        __syncthreads();             // step k + 1's actions (written by other lanes) are visible
     }
     if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
 }
@@ -2547,39 +2709,7 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
     const Keys Kh = make_keys(P.key0, P.key1);
     for (uint32_t k = 0; k < K; ++k, ++ctr) {
         if (HD) {
-            if (live) {
-                const Rng g{Kh, ctr, gid, TAG_STEP};
-                float* d = s_draw + lane;
-                auto bm4 = [&](uint32_t blk, int w) {
-                    const U4 u = g.block(blk);
-                    float z0, z1, z2, z3;
-                    box_muller(u.x, u.y, z0, z1);
-                    box_muller(u.z, u.w, z2, z3);
-                    d[(w + 0) * 64] = z0; d[(w + 1) * 64] = z1; d[(w + 2) * 64] = z2; d[(w + 3) * 64] = z3;
-                };
-                if (wave == 1) {
-                    bm4(2, HD_OU1);
-                    bm4(16, HD_GYRO1);
-                    bm4(17, HD_GYRO1 + 4);
-                    const U4 u = g.block(18);
-                    float z0, z1;
-                    box_muller(u.x, u.y, z0, z1);
-                    d[(HD_GYRO1 + 8) * 64] = z0;
-                } else if (wave == 2) {
-                    bm4(24, HD_FINAL);
-                    bm4(25, HD_FINAL + 4);
-                    bm4(26, HD_FINAL + 8);
-                } else {
-                    bm4(27, HD_FINAL + 12);
-                    const U4 u = g.block(28), v = g.block(29);
-                    float z0, z1;
-                    box_muller(u.x, u.y, z0, z1);
-                    d[(HD_FINAL + 16) * 64] = z0; d[(HD_FINAL + 17) * 64] = z1;
-                    d[(HD_FINAL + 18) * 64] = __uint_as_float(u.z); d[(HD_FINAL + 19) * 64] = __uint_as_float(u.w);
-                    d[(HD_FINAL + 20) * 64] = __uint_as_float(v.x); d[(HD_FINAL + 21) * 64] = __uint_as_float(v.y);
-                    d[(HD_FINAL + 22) * 64] = __uint_as_float(v.z); d[(HD_FINAL + 23) * 64] = __uint_as_float(v.w);
-                }
-            }
+            if (live) helper_step_draws(Kh, ctr, gid, wave, s_draw + lane);
         }
         lds_barrier();                               // A_k
         Env H;
@@ -2774,7 +2904,7 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 // and the slice size of the fused rollout.
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t occupancy_t(KParams& P) {
-    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0;
+    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0, per_croll = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
@@ -2785,10 +2915,15 @@ static hipError_t occupancy_t(KParams& P) {
         if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_collect, collect_kernel<NOISE, DR, PHYS, SPEC>,
                                                              STEP_BLOCK, 0);
+    if constexpr (NOISE && SPEC == 1 && PHYS == PHYS_BULLET_T)
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_croll, collect_rollout_kernel<NOISE, DR, PHYS, SPEC>,
+                                                             STEP_BLOCK, 0);
     if (e != hipSuccess) return e;
     P.rb_step = (uint32_t)(cus * (per_step > 0 ? per_step : 1));
     P.rb_roll = (uint32_t)(cus * (per_roll > 0 ? per_roll : 1));
     P.rb_collect = (uint32_t)(cus * (per_collect > 0 ? per_collect : 1));
+    P.rb_croll = (uint32_t)(cus * (per_croll > 0 ? per_croll : 1));
     return hipSuccess;
 }
 
@@ -2876,6 +3011,69 @@ static hipError_t launch_rollout_t(const KParams& P, const StepIO& io, uint32_t 
     return hipSuccess;
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
+static hipError_t launch_collect_rollout_t(const KParams& P, const StepIO& io, const PolicyIO& pio, uint32_t K,
+                                           hipStream_t s) {
+    if constexpr (!NOISE || SPEC != 1 || PHYS != PHYS_BULLET_T) {
+        return hipErrorNotSupported;
+    } else {
+        constexpr uint32_t OD = 34;
+        if (P.N <= SMALL_N_MAX) {
+            // small N: K collect_kernel_small launches (64 envs per block with the helper waves), whose
+            // chain is shorter than a 256-env block's here, and which fill all CUs at the node shard
+            for (uint32_t k = 0; k < K; ++k) {
+                StepIO iok = io;
+                iok.act = pio.act + (size_t)k * P.N * 4;
+                iok.obs = io.obs + (size_t)k * P.N * OD;
+                iok.rew = io.rew + (size_t)k * P.N;
+                iok.done = io.done + (size_t)k * P.N;
+                if (io.trunc) iok.trunc = io.trunc + (size_t)k * P.N;
+                if (io.final_obs) iok.final_obs = io.final_obs + (size_t)k * P.N * OD;
+                PolicyIO pk = pio;
+                pk.counter = pio.counter + k;
+                pk.act = pio.act + (size_t)(k + 1) * P.N * 4;
+                pk.val = pio.val + (size_t)(k + 1) * P.N;
+                pk.logp = pio.logp + (size_t)(k + 1) * P.N;
+                hipLaunchKernelGGL((collect_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0,
+                                   s, P, iok, pk);
+                const hipError_t e = hipGetLastError();
+                if (e != hipSuccess) return e;
+            }
+            return hipSuccess;
+        }
+        // slices of one residency round each (as launch_rollout_t): a slice's blocks run all K steps
+        // together.  Every output slab keeps the whole population's stride.
+        const uint32_t blocks = (P.N + STEP_BLOCK - 1) / STEP_BLOCK;
+        const uint32_t round_blocks = P.rb_croll > 0 ? P.rb_croll : 1u;
+        const uint32_t nslices = (blocks + round_blocks - 1) / round_blocks;
+        const uint32_t per = (blocks + nslices - 1) / nslices;
+        for (uint32_t b0 = 0; b0 < blocks; b0 += per) {
+            const uint32_t nb = blocks - b0 < per ? blocks - b0 : per;
+            const uint32_t e0 = b0 * STEP_BLOCK;
+            KParams Ps = P;
+            Ps.N = (P.N - e0 < nb * STEP_BLOCK) ? P.N - e0 : nb * STEP_BLOCK;
+            Ps.gid_off = P.gid_off + e0;
+            Ps.out_stride = P.N;
+            StepIO ios = io;
+            ios.sf = io.sf + (size_t)(e0 / 64u) * (NG * 256);
+            ios.obs = io.obs + (size_t)e0 * OD;
+            ios.rew = io.rew + e0;
+            ios.done = io.done + e0;
+            if (io.trunc) ios.trunc = io.trunc + e0;
+            if (io.final_obs) ios.final_obs = io.final_obs + (size_t)e0 * OD;
+            PolicyIO ps = pio;
+            ps.row_offset = pio.row_offset + e0;
+            ps.act = pio.act + (size_t)e0 * 4;
+            ps.val = pio.val + e0;
+            ps.logp = pio.logp + e0;
+            hipLaunchKernelGGL((collect_rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(STEP_BLOCK), 0, s, Ps, ios,
+                               ps, K);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+}
+template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t launch_reset_t(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     const dim3 grid((P.N + 255) / 256), block(256);
     hipLaunchKernelGGL((reset_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, P, sf, mask, obs);
@@ -2932,6 +3130,9 @@ hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32
 }
 hipError_t launch_collect(const KParams& P, const StepIO& io, const PolicyIO& pio, hipStream_t s) {
     CF2_DISPATCH(launch_collect_t, P, io, pio, s);
+}
+hipError_t launch_collect_rollout(const KParams& P, const StepIO& io, const PolicyIO& pio, uint32_t K, hipStream_t s) {
+    CF2_DISPATCH(launch_collect_rollout_t, P, io, pio, K, s);
 }
 hipError_t launch_reset(const KParams& P, float* sf, const uint8_t* mask, float* obs, hipStream_t s) {
     CF2_DISPATCH(launch_reset_t, P, sf, mask, obs, s);

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 5
+#define CF2SIM_ABI_VERSION 6
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -305,6 +305,23 @@ int  cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float*
                       uint8_t* trunc_dev, float* final_obs_dev, const float* packed_dev, uint32_t obs_dim,
                       int precision, uint64_t seed, uint32_t counter, uint32_t row_offset, float* act_out_dev,
                       float* val_out_dev, float* logp_out_dev, void* stream);
+
+/* K steps of the collect loop in one launch: env-step k (actions act_dev + k*N*4) and then the
+ * policy forward + sampling on its observations (noise counter counter + k), whose actions the
+ * next env-step takes; the env state stays in registers for the K steps.  At N <= 32768 (the
+ * 8-GPU node shard) the call issues K launches of the per-step fused kernel instead (64-env blocks
+ * with helper waves, a shorter chain at that size); the outputs are the same either way.  Buffers, slab-major:
+ * act_dev [K+1,N,4] (slab 0 in: the first step's actions; slabs 1..K out), val_dev / logp_dev
+ * [K+1,N] (slabs 1..K out, slab 0 untouched), obs_dev [K,N,obs_dim] (slab k = the observation
+ * after env-step k), rew_dev / done_dev [K,N], trunc_dev / final_obs_dev [K,N] / [K,N,obs_dim]
+ * or NULL.  Every output is bit-identical to K cf2_collect_step calls with act_out = the next
+ * slab and counters counter, counter + 1, ... (IWPGAlgorithm.roll_out's loop,
+ * phoenix_drone_simulation/algs/iwpg/iwpg.py:372-410, ActorCritic.step algs/core.py:371-395).
+ * Built where cf2_collect_step is (else CF2_ERR_UNSUPPORTED, nothing launched). */
+int  cf2_collect_rollout(cf2_ctx* ctx, int K, float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
+                         uint8_t* trunc_dev, float* final_obs_dev, const float* packed_dev, uint32_t obs_dim,
+                         int precision, uint64_t seed, uint32_t counter, uint32_t row_offset, float* val_dev,
+                         float* logp_dev, void* stream);
 
 /* Batched GAE over [T, n] rollout buffers (algs/core.py:459-535 finish_path on every env's
  * episode slices): done/trunc uint8 (terminal -> bootstrap 0, time-out -> trunc_val), the end of

@@ -5,15 +5,16 @@ import numpy as np
 CLEAN = dict(observation_noise=0, domain_randomization=-1, motor_thrust_noise=0, max_episode_steps=0)
 
 
-def pd_actions(state17, hover):
+def pd_actions(state17, hover, kp=0.5, kd=0.08, kz=0.05):
     """A stabilising attitude/altitude PD controller on obs17 = [p, q, v, w_body, a] (test helper;
-    stands in for a trained policy closing the loop on the env's own observations)."""
+    stands in for a trained policy closing the loop on the env's own observations).  kp / kd: roll
+    and pitch angle / rate gains, kz: yaw-rate gain."""
     p, q, v, w = state17[:, 0:3], state17[:, 3:7], state17[:, 7:10], state17[:, 10:13]
     x, y, z, qw = q.T
     roll = np.arctan2(2 * (qw * x + y * z), 1 - 2 * (x * x + y * y))
     pitch = np.arcsin(np.clip(2 * (qw * y - z * x), -1, 1))
     T = hover + 0.5 * (1.0 - p[:, 2]) - 0.4 * v[:, 2]
-    tx, ty, tz = -0.5 * roll - 0.08 * w[:, 0], -0.5 * pitch - 0.08 * w[:, 1], -0.05 * w[:, 2]
+    tx, ty, tz = -kp * roll - kd * w[:, 0], -kp * pitch - kd * w[:, 1], -kz * w[:, 2]
     a = (T[:, None] + tx[:, None] * np.array([-1, -1, 1, 1]) + ty[:, None] * np.array([-1, 1, 1, -1])
          + tz[:, None] * np.array([-1, 1, -1, 1]))
     return np.clip(a, -1, 1).astype(np.float32)

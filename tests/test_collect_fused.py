@@ -1,8 +1,10 @@
-"""cf2_collect_step: the collect loop's env-step and the policy forward on its observations in one
-launch (collect_kernel) must equal the two launches (cf2_step + cf2_policy_forward) bit for bit --
-observations, actions, values, log-probabilities, rewards, flags, final observations, the GAE
-outputs and the env state afterwards -- across auto-resets, time-outs, a partial last block and the
-HJ path; configs without a fused instance must fall back to the two launches.
+"""The fused collect paths must equal the two launches per env-step (cf2_step +
+cf2_policy_forward) bit for bit -- observations, actions, values, log-probabilities, rewards,
+flags, final observations, the GAE outputs and the env state afterwards -- across auto-resets,
+time-outs, a partial last block, several residency slices and the HJ path:
+  * cf2_collect_rollout: all K steps of the loop in one launch (collect_rollout_kernel);
+  * cf2_collect_step: one launch per env-step (collect_kernel / collect_kernel_small).
+Configs without a fused instance must fall back to the two launches.
 The collect loop being restated is IWPGAlgorithm.roll_out (algs/iwpg/iwpg.py:372-410)."""
 import pytest
 import torch
@@ -20,10 +22,10 @@ CASES = [
 ]
 
 
-def _pair(env_id, n, kw, setup=None):
+def _pair(env_id, n, kw, setup=None, count=2):
     from cf2sim.rollout import FusedActorCritic, MLPActorCritic
     from cf2sim.vec_env import BatchedCrazyflieEnv
-    envs = [BatchedCrazyflieEnv(env_id, n, seed=11, want_final_obs=True, **kw) for _ in range(2)]
+    envs = [BatchedCrazyflieEnv(env_id, n, seed=11, want_final_obs=True, **kw) for _ in range(count)]
     torch.manual_seed(5)
     ac = MLPActorCritic(obs_dim=envs[0].obs_dim).cuda()
     with torch.no_grad():                    # non-trivial standardisation, as after a few epochs
@@ -45,54 +47,72 @@ def _check_equal(ra, rb):
         assert torch.equal(a, b), f"{f}: max |diff| {(a.float() - b.float()).abs().max().item()}"
 
 
-def _run(env_id, n, kw, setup=None, T=24):
-    from cf2sim.rollout import collect
-    (ea, pa), (eb, pb) = _pair(env_id, n, kw, setup)
-    oa, ob = ea.reset(), eb.reset()
-    launched = []
-    orig = ea.collect_step_into
+def _spy(env, name, log):
+    orig = getattr(env, name)
 
     def spy(*args, **kwargs):
         ok = orig(*args, **kwargs)
-        launched.append(ok)
+        log.append(ok)
         return ok
-    ea.collect_step_into = spy
+    setattr(env, name, spy)
+
+
+def _run(env_id, n, kw, setup=None, T=24):
+    """One collect per mode (one launch / one launch per step / two launches per step) from the
+    same state; returns the fused calls' support flags (rollout, per-step)."""
+    from cf2sim.rollout import collect
+    (ea, pa), (es, ps), (eb, pb) = _pair(env_id, n, kw, setup, count=3)
+    oa, os_, ob = ea.reset(), es.reset(), eb.reset()
+    launched_roll, launched_step = [], []
+    _spy(ea, "collect_rollout_into", launched_roll)
+    _spy(es, "collect_step_into", launched_step)
     ra = collect(ea, pa, T, obs=oa.clone(), fuse=True)
+    rs_ = collect(es, ps, T, obs=os_.clone(), fuse="steps")
     rb = collect(eb, pb, T, obs=ob.clone(), fuse=False)
     torch.cuda.synchronize()
-    assert ra.done.any(), "no auto-reset inside the window"
+    assert rb.done.any(), "no auto-reset inside the window"
     _check_equal(ra, rb)
-    gs, gi = ea.get_state()
-    rs, ri = eb.get_state()
-    assert torch.equal(gi, ri) and torch.equal(gs, rs)
-    assert pa.counter == pb.counter
+    _check_equal(rs_, rb)
+    gb, ib = eb.get_state()
+    for e in (ea, es):
+        g, i = e.get_state()
+        assert torch.equal(i, ib) and torch.equal(g, gb)
+    assert pa.counter == pb.counter == ps.counter
     # a second collect continues from the first one's last observation
     ra2 = collect(ea, pa, 5, obs=ra.last_obs, fuse=True)
+    rs2 = collect(es, ps, 5, obs=rs_.last_obs, fuse="steps")
     rb2 = collect(eb, pb, 5, obs=rb.last_obs, fuse=False)
     _check_equal(ra2, rb2)
+    _check_equal(rs2, rb2)
     # a collect that re-uses an earlier rollout's storage (out=) gives the same results
     ra3 = collect(ea, pa, 5, obs=ra2.last_obs, fuse=True, out=ra2)
     rb3 = collect(eb, pb, 5, obs=rb2.last_obs, fuse=False)
     assert ra3.storage is ra2.storage
     _check_equal(ra3, rb3)
-    ea.close()
-    eb.close()
-    return launched
+    for e in (ea, es, eb):
+        e.close()
+    return launched_roll, launched_step
 
 
 @pytest.mark.parametrize("env_id,n,kw", CASES)
 def test_fused_collect_equals_two_launches(gpu, env_id, n, kw):
-    launched = _run(env_id, n, kw)
-    assert launched and all(launched), "the fused kernel did not run"
+    roll, step = _run(env_id, n, kw)
+    assert roll and all(roll) and step and all(step), "a fused kernel did not run"
+
+
+def test_collect_rollout_over_several_slices(gpu):
+    """More blocks than one residency round holds: cf2_collect_rollout runs the envs in slices."""
+    roll, step = _run("DroneHoverBulletFreeEnvWithGust-v0", 200000, dict(max_episode_steps=5), T=7)
+    assert roll and all(roll) and step and all(step)
 
 
 def test_fused_collect_hj_boltzmann(gpu):
     from test_gpu_parity import _synthetic_tables
     V = torch.from_numpy(_synthetic_tables(tuple(range(3)), seed=1)).cuda()
     tol = [lv % 3 for lv in range(21)]
-    launched = _run("DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", 40000, dict(max_episode_steps=6),
-                    setup=lambda e: e.bind_hj_tables(V, tol), T=12)
-    assert launched and all(launched)
+    roll, step = _run("DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", 40000, dict(max_episode_steps=6),
+                      setup=lambda e: e.bind_hj_tables(V, tol), T=12)
+    assert roll and all(roll) and step and all(step)
 
 
 @pytest.mark.parametrize("env_id,n,kw", [
@@ -101,8 +121,9 @@ def test_fused_collect_hj_boltzmann(gpu):
     ("DroneHoverSimpleEnv-v0", 40000, {}),
 ])
 def test_unfused_configs_fall_back(gpu, env_id, n, kw):
-    launched = _run(env_id, n, kw, T=8)
-    assert launched == [False] * 3, "an unsupported config launches nothing and is probed once per collect"
+    roll, step = _run(env_id, n, kw, T=8)
+    assert roll == [False] * 3 and step == [False] * 2, \
+        "an unsupported config launches nothing and is probed once per collect"
 
 
 def test_collect_step_rejects_bad_args(gpu):
@@ -124,6 +145,19 @@ def test_collect_step_rejects_bad_args(gpu):
                                 p.w.data_ptr(), d + 8, p.prec, 0, 0, 0, torch.empty(n, 4, device=gpu).data_ptr(),
                                 v.data_ptr(), lp.data_ptr(), e.stream)
     assert st != 0 and st != _native.CF2_ERR_UNSUPPORTED, "an obs_dim that is not the env's is an error"
+    # cf2_collect_rollout: K < 1, misaligned actions and a wrong obs_dim are errors, nothing launched
+    K = 3
+    A = torch.zeros(K + 1, n, 4, device=gpu)
+    O = torch.empty(K, n, d, device=gpu)
+    R, V, L = torch.empty(K, n, device=gpu), torch.empty(K + 1, n, device=gpu), torch.empty(K + 1, n, device=gpu)
+    D = torch.empty(K, n, dtype=torch.uint8, device=gpu)
+    args = lambda k, a, od: (e._ctx, k, a, O.data_ptr(), R.data_ptr(), D.data_ptr(), None, None, p.w.data_ptr(), od,
+                             p.prec, 0, 0, 0, V.data_ptr(), L.data_ptr(), e.stream)
+    for bad in (args(0, A.data_ptr(), d), args(K, A.data_ptr() + 4, d), args(K, A.data_ptr(), d + 8)):
+        st = e.lib.cf2_collect_rollout(*bad)
+        assert st != 0 and st != _native.CF2_ERR_UNSUPPORTED
+    with pytest.raises(ValueError):           # act needs K + 1 slabs
+        e.collect_rollout_into(A[:K], O, R, D, None, None, p, V, L)
     e.close()
 
 

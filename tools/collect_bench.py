@@ -1,6 +1,7 @@
 """Per-launch time of the fused collect step (cf2_collect_step: env-step + actor-critic forward) at N
 envs, HIP events on the env's stream over `--steps` launches after a random-action warm-up past the
-start transient; the two-launch pair (cf2_step + cf2_policy_forward) is timed the same way.  Prints
+start transient; the two-launch pair (cf2_step + cf2_policy_forward) is timed the same way, and the
+whole loop in one launch (cf2_collect_rollout, K = --slabs steps per launch) per env-step.  Prints
 one JSON line.  CF2SIM_LIB selects an A/B build."""
 import argparse
 import json
@@ -35,7 +36,8 @@ def main():
     S, od = args.slabs, env.obs_dim
     act = torch.rand(S + 1, n, 4, device=dev, generator=g) * 2 - 1
     obs, fin = torch.empty(S, n, od, device=dev), torch.empty(S, n, od, device=dev)
-    rew, val, lp = (torch.empty(S, n, device=dev) for _ in range(3))
+    rew = torch.empty(S, n, device=dev)
+    val, lp = (torch.empty(S + 1, n, device=dev) for _ in range(2))
     dn, tr = (torch.empty(S, n, dtype=torch.uint8, device=dev) for _ in range(2))
 
     def fused(k):
@@ -47,18 +49,23 @@ def main():
         env.step_into(act[s], obs[s], rew[s], dn[s], tr[s], final_obs_out=fin[s])
         pol.step_into(obs[s], act[s + 1], val[s], lp[s])
 
-    out = {"envs": n, "steps": args.steps, "env_id": args.env_id}
-    for name, fn in (("fused_us", fused), ("two_launch_us", pair), ("fused_us_again", fused)):
-        for k in range(20):
+    def rollout(k):
+        assert env.collect_rollout_into(act, obs, rew, dn, tr, fin, pol, val, lp)
+
+    out = {"envs": n, "steps": args.steps, "env_id": args.env_id, "rollout_k": S}
+    for name, fn, per in (("fused_us", fused, 1), ("two_launch_us", pair, 1), ("rollout_us_per_env_step", rollout, S),
+                          ("fused_us_again", fused, 1)):
+        calls = max(2, args.steps // per)
+        for k in range(min(20, calls)):
             fn(k)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
-        e0.record()
-        for k in range(args.steps):
+        e0.record()                  # the env launches on torch's current stream
+        for k in range(calls):
             fn(k)
         e1.record()
         torch.cuda.synchronize()
-        out[name] = e0.elapsed_time(e1) * 1e3 / args.steps
+        out[name] = e0.elapsed_time(e1) * 1e3 / (calls * per)
     print(json.dumps(out))
     env.close()
 

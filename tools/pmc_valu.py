@@ -21,15 +21,27 @@ SIMDS = 1024
 NAMES = ["SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
 
 
-def per_dispatch(kern, sub="pmc"):
+def per_dispatch(kern, sub="pmc", names=NAMES):
     per = {}
     for f in glob.glob(os.path.join(out, sub, "**", "*counter_collection.csv"), recursive=True):
         for i, row in enumerate(csv.DictReader(open(f))):
-            if kern in row.get("Kernel_Name", "") and row["Counter_Name"] in NAMES:
+            if kern in row.get("Kernel_Name", "") and row["Counter_Name"] in names:
                 key = int(row.get("Dispatch_Id") or i)
-                d = per.setdefault(key, {k: 0.0 for k in NAMES})
+                d = per.setdefault(key, {k: 0.0 for k in names})
                 d[row["Counter_Name"]] += float(row["Counter_Value"])
     return [per[k] for k in sorted(per)]
+
+
+def mfma_busy(kern, sub="pmc_mfma"):
+    """MFMA-busy fraction: SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over SIMDs) / SIMDs / kernel
+    cycles at 2.4 GHz, over the dispatches of the pass."""
+    rows = per_dispatch(kern, sub, ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVES"])
+    dur = durations(kern, sub)
+    if not rows or not dur:
+        return None
+    busy = sum(r["SQ_VALU_MFMA_BUSY_CYCLES"] for r in rows)
+    return {"mfma_busy_cycles_per_simd": busy / SIMDS / len(rows),
+            "mfma_busy_frac": busy / SIMDS / (sum(dur) * 1e-9 * 2.4e9)}
 
 
 def durations(kern, sub="pmc"):
@@ -65,8 +77,9 @@ roll = per_dispatch("rollout_kernel")
 res = {"workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}", "kernel_key": key,
        "step_kernel": summarize(step, "step_kernel", 1, durations("step_kernel")[-30:]),
        "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations("rollout_kernel")),
-       "collect_kernel": (summarize(per_dispatch("collect_kernel", "pmc_collect"), "collect_kernel (env-step + policy)",
-                                    1, durations("collect_kernel", "pmc_collect"))
+       "collect_kernel": (dict(summarize(per_dispatch("collect_kernel", "pmc_collect"),
+                                         "collect_kernel (env-step + policy)", 1, durations("collect_kernel", "pmc_collect")),
+                               **(mfma_busy("collect_kernel") or {}))
                           if per_dispatch("collect_kernel", "pmc_collect") else None),
        "note": __doc__.split("\n\n")[1]}
 prof = os.path.join(ROOT, "profiles", "valu_issue.json")
