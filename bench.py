@@ -156,9 +156,9 @@ def load_traffic(workload_key: str):
     return None
 
 
-def load_valu_issue(workload_key: str):
-    """VALU issue fractions of the step and rollout kernels from tools/pmc_valu.sh (PMC), used only
-    if measured on this workload with this very kernel build; otherwise (None, None)."""
+def load_pmc(workload_key: str) -> dict:
+    """The PMC entry of tools/pmc_valu.sh (profiles/valu_issue.json) for this workload, used only if
+    measured with this very kernel build; otherwise {}."""
     p = os.path.join(ROOT, "profiles", "valu_issue.json")
     try:
         with open(p) as f:
@@ -166,11 +166,21 @@ def load_valu_issue(workload_key: str):
         key = step_kernel_key()
         for e in d.get("entries", []):
             if e.get("workload") == workload_key and e.get("kernel_key") == key:
-                return (e["step_kernel"]["valu_issue_frac"], e["rollout_kernel"]["valu_issue_frac"],
-                        (e.get("collect_kernel") or {}).get("valu_issue_frac"))
-    except (OSError, ValueError, ImportError, KeyError):
+                return e
+    except (OSError, ValueError, ImportError):
         pass
-    return None, None, None
+    return {}
+
+
+def load_valu_issue(workload_key: str, kernel: str):
+    """VALU issue fraction of one kernel (step_kernel, rollout_kernel, collect_kernel,
+    collect_rollout_kernel) from load_pmc, or None."""
+    return (load_pmc(workload_key).get(kernel) or {}).get("valu_issue_frac")
+
+
+def load_mfma_busy(workload_key: str, kernel: str):
+    """MFMA-busy fraction (PMC SQ_VALU_MFMA_BUSY_CYCLES) of a fused collect kernel, or None."""
+    return (load_pmc(workload_key).get(kernel) or {}).get("mfma_busy_frac")
 
 
 def bytes_per_env_step(env) -> int:
@@ -179,22 +189,6 @@ def bytes_per_env_step(env) -> int:
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 matrix peak (MI355X_MICROARCH.md; no sparsity)
 POLICY_FLOPS_PER_ROW = 2 * (34 * 50 + 50 * 50 + 50 * 4 + 34 * 64 + 64 * 64 + 64)   # pi + V MLPs: 21 472
-
-
-def load_mfma_busy(workload_key: str):
-    """MFMA-busy fraction of the fused collect kernel (PMC SQ_VALU_MFMA_BUSY_CYCLES, tools/pmc_valu.sh),
-    used only if measured on this workload with this kernel build; otherwise None."""
-    p = os.path.join(ROOT, "profiles", "valu_issue.json")
-    try:
-        with open(p) as f:
-            d = json.load(f)
-        key = step_kernel_key()
-        for e in d.get("entries", []):
-            if e.get("workload") == workload_key and e.get("kernel_key") == key:
-                return (e.get("collect_kernel") or {}).get("mfma_busy_frac")
-    except (OSError, ValueError, ImportError):
-        pass
-    return None
 
 
 def secondary_roofline(hbm_bytes: float, seconds: float, valu_frac, flops: float = 0.0, mfma_busy=None) -> dict:
@@ -513,7 +507,7 @@ def main(argv=None):
         f1.record(stream)
         torch.cuda.synchronize()
         us = f0.elapsed_time(f1) * 1e3 / (reps * K)
-        vfr = load_valu_issue(f"{args.env_id}:N={n}")[1]
+        vfr = load_valu_issue(f"{args.env_id}:N={n}", "rollout_kernel")
         # per env-step of a K-step launch: the action in and the step() outputs; the state is read
         # and written once per launch (1/K of it per env-step)
         state_b = algorithmic_bytes_per_env_step(env.cfg, outputs=()) - 16
@@ -553,21 +547,28 @@ def main(argv=None):
         # (cf2_collect_rollout), the collect() default
         cus_steps, _ = time_collect("steps")
         cus, mode = time_collect(True)
-        # per env-step: the env-step's bytes (state, action, obs, reward, done, truncation) and the
-        # policy's outputs (action, value, log-probability); the policy reads the observations from
-        # LDS and its weights from L2 (not HBM); 21.5 kFLOP of useful MLP work per row
-        cb = algorithmic_bytes_per_env_step(cenv.cfg, outputs=("obs", "rew", "done", "trunc")) + 16 + 4 + 4
-        cvf = load_valu_issue(f"{args.env_id}:N={n}")[2]
+        # per env-step: the env-step's bytes (action, obs, reward, done, truncation; the state once
+        # per collect in the one-launch mode, every step in the per-step mode) and the policy's
+        # outputs (action, value, log-probability); the policy reads the observations back from
+        # L2 / LDS and its weights from LDS (staged once per launch); 21.5 kFLOP of useful MLP work
+        # per row
+        state_b = algorithmic_bytes_per_env_step(cenv.cfg, outputs=()) - 16
+        step_b = algorithmic_bytes_per_env_step(cenv.cfg, outputs=("obs", "rew", "done", "trunc")) + 16 + 4 + 4
+        one = mode is True
+        cb = step_b - state_b + state_b / T if one else step_b
+        wk = f"{args.env_id}:N={n}"
+        ck = "collect_rollout_kernel" if one and n > 32768 else "collect_kernel"
+        cvf = load_valu_issue(wk, ck)
         collect_line = {"value": n / (cus * 1e-6), "unit": "env-steps/s", "us_per_env_step": cus,
                         "algorithmic_bytes_per_env_step": cb, "flops_per_env_step": POLICY_FLOPS_PER_ROW,
-                        "roofline": secondary_roofline(cb * n, cus * 1e-6, cvf, POLICY_FLOPS_PER_ROW * n,
-                                                       load_mfma_busy(f"{args.env_id}:N={n}")),
+                        "roofline": dict(secondary_roofline(cb * n, cus * 1e-6, cvf, POLICY_FLOPS_PER_ROW * n,
+                                                            load_mfma_busy(wk, ck)), pmc_kernel=ck),
                         "steps_per_collect": T, "policy": "MLP actor-critic 34-50-50-4 / 34-64-64-1, bf16x3",
                         "launches": {True: "one per collect (cf2_collect_rollout)",
                                      "steps": "one per env-step (cf2_collect_step)"}.get(mode, "two per env-step"),
                         "us_per_env_step_one_launch_per_step": cus_steps,
                         # fraction of the fused kernel's SIMD cycles issuing VALU (PMC, tools/pmc_valu.sh)
-                        "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[2],
+                        "valu_issue_frac": cvf,
                         "includes": "env-step, policy forward + sampling, rollout storage (re-used across collects), GAE, "
                                     "time-out values"}
         cenv.close()
@@ -735,7 +736,7 @@ def main(argv=None):
                          "traffic": traffic,
                          "traffic_source": "rocprofv3 PMC FETCH_SIZE/WRITE_SIZE passes of this kernel build "
                                            "(tools/pmc_traffic.sh -> profiles/step_kernel_traffic.json)" if traffic else None,
-                         "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}")[0],
+                         "valu_issue_frac": load_valu_issue(f"{args.env_id}:N={n}", "step_kernel"),
                          "algorithmic_bytes_per_env_step": bytes_per,
                          "kernel_ms_per_launch": kern_ms,
                          "working_set_bytes": wset,

@@ -2577,6 +2577,169 @@ enum { RP_DT = 0, RP_M = 1, RP_J = 2, RP_K0 = 5, RP_K1 = 6, RP_B = 7, RP_K = 11,
        RP_LEVEL_IDX = 19, RP_WORDS = 20 };
 enum { RO_HELD1 = 0, RO_NG1 = 10, RO_HELD2 = 19, RO_NG2 = 29, RO_WORDS = 38 };
 
+// LDS records of one 64-env group of the small-N fused rollouts ([word][env] columns)
+struct SmallRollLds {
+    float* obs;          // [64][OD] the group's obs rows
+    float* kin;          // [RK_WORDS][64]
+    float* par;          // [RP_WORDS][64]
+    float* ho;           // [RO_WORDS][64] (sensor noise only)
+    float* draw;         // [HD_WORDS][64] (HD only)
+    uint32_t* mask;      // [2] the group's finished envs (ballot of its env wave)
+};
+
+// The env wave's part of one step of the small-N fused rollouts: the env-step (barrier A_k inside
+// it with HD, else at the top), the ballot, barrier B_k, and a finishing env's reset copied from
+// the helpers' records into its registers, its reset observation row into L.obs.
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__device__ __forceinline__ void small_roll_env_step(const KParams& P, const StepIO& io, uint32_t i, uint32_t lane,
+                                                    bool live, Env& E, const SmallRollLds& L, const double* s_hjgrid) {
+    constexpr int OL = NOISE ? 13 : 17;
+    constexpr int OD = 2 * (OL + 4);
+    constexpr bool HD = SPEC == 1 && NOISE;
+    float* obs_row = L.obs + lane * OD;
+    if (!HD) lds_barrier();                  // A_k (HD: inside the env-step, before sub-step 1)
+    bool do_reset = false;
+    ResetSeed rs;
+    if (live)
+        do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD>(P, io, i, E, obs_row, rs, s_hjgrid, L.draw + lane);
+    const uint64_t m = __ballot(do_reset);
+    if (lane == 0) { L.mask[0] = (uint32_t)m; L.mask[1] = (uint32_t)(m >> 32); }
+    lds_barrier();                           // B_k: the helpers' records of step k are in LDS
+    if (do_reset) {
+        const float stale[3] = {rs.wb[0], rs.wb[1], rs.wb[2]};   // the gyro LPF seed
+        const float* kin = L.kin + lane;
+        const float* par = L.par + lane;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            E.p[c] = kin[(RK_P + c) * 64]; E.v[c] = kin[(RK_V + c) * 64]; E.w[c] = kin[(RK_W + c) * 64];
+            E.rpy[c] = kin[(RK_RPY + c) * 64]; E.wb[c] = kin[(RK_WB + c) * 64];
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            E.q[c] = kin[(RK_Q + c) * 64]; E.x[c] = kin[(RK_X + c) * 64]; E.xl[c] = 0.0f;
+            E.la[c] = kin[(RK_LA + c) * 64];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) E.abuf[r][c] = r < P.buf_size ? kin[(RK_ABUF + 4 * r + c) * 64] : 0.0f;
+        E.ep_step = 0; E.aidx = 0; E.props_on = 0; E.la_view = 1;
+        E.dt = par[RP_DT * 64]; E.m = par[RP_M * 64];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { E.J[c] = par[(RP_J + c) * 64]; E.dstb[c] = par[(RP_DSTB + c) * 64]; }
+        E.k0 = par[RP_K0 * 64]; E.k1 = par[RP_K1 * 64];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { E.B[c] = par[(RP_B + c) * 64]; E.K[c] = par[(RP_K + c) * 64]; }
+        E.level = par[RP_LEVEL * 64];
+        E.level_idx = bi(par[RP_LEVEL_IDX * 64]);
+        E.gust_left = 0;
+        // the reset observation (reset_observe): two sensor calls, then the history row
+        float o0[17], o1[17];
+        if (NOISE) {
+            const float* ho = L.ho + lane;
+            float ng1[9], ng2[9];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) { ng1[c] = ho[(RO_NG1 + c) * 64]; ng2[c] = ho[(RO_NG2 + c) * 64]; }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) E.lpf[c] = stale[c];
+#pragma unroll
+            for (int c = 0; c < 10; ++c) { o0[c] = ho[(RO_HELD1 + c) * 64]; o1[c] = ho[(RO_HELD2 + c) * 64]; }
+#pragma unroll
+            for (int c = 0; c < 10; ++c) E.held[c] = o1[c];
+            gyro_update(P, E, ng1);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o0[10 + c] = E.lpf[c];
+            gyro_update(P, E, ng2);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o1[10 + c] = E.lpf[c];
+        } else {
+            const float o[17] = {E.p[0], E.p[1], E.p[2], E.q[0], E.q[1], E.q[2], E.q[3], E.v[0], E.v[1],
+                                 E.v[2], E.wb[0], E.wb[1], E.wb[2], E.la[0], E.la[1], E.la[2], E.la[3]};
+#pragma unroll
+            for (int c = 0; c < 17; ++c) { o0[c] = o[c]; o1[c] = o[c]; }
+        }
+        float row[OD];
+#pragma unroll
+        for (int c = 0; c < OL; ++c) { row[c] = o0[c]; row[OL + 4 + c] = o1[c]; E.obs_prev[c] = o1[c]; }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            row[OL + c] = E.la[c]; row[2 * OL + 4 + c] = E.la[c];
+            E.hact[0][c] = E.la[c]; E.hact[1][c] = E.la[c];
+        }
+        E.halias0 = E.halias1 = 1;
+#pragma unroll
+        for (int c = 0; c < OD; c += 2) *reinterpret_cast<float2*>(obs_row + c) = make_float2(row[c], row[c + 1]);
+    }
+}
+
+// A helper wave's part of one step (wave 1-3 of a group): the HD draws of step k, barrier A_k, the
+// speculative reset of every env of the group into the LDS records, barrier B_k, and the level a
+// finishing env's new episode keeps.  ctr: the env's RNG counter at step k.
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__device__ __forceinline__ void small_roll_helper_step(const KParams& P, const Keys& Kh, uint32_t ctr, uint32_t gid,
+                                                       uint32_t wave, uint32_t lane, bool live, float& lvl,
+                                                       int& lvl_idx, const SmallRollLds& L) {
+    constexpr bool HD = SPEC == 1 && NOISE;
+    constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
+    if (HD) {
+        if (live) helper_step_draws(Kh, ctr, gid, wave, L.draw + lane);
+    }
+    lds_barrier();                               // A_k
+    Env H;
+    if (P.auto_reset && live) {
+        const Rng gr{Kh, ctr, gid, TAG_RESET};
+        HeldNoise hn;
+        float ngs[9];
+        if (NOISE && wave >= 2) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
+        reset_kinematics<PHYS, true>(P, H, gr, gid);
+        if (wave == 1) {
+            float* kin = L.kin + lane;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                kin[(RK_P + c) * 64] = H.p[c]; kin[(RK_V + c) * 64] = H.v[c]; kin[(RK_W + c) * 64] = H.w[c];
+                kin[(RK_RPY + c) * 64] = H.rpy[c]; kin[(RK_WB + c) * 64] = H.wb[c];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                kin[(RK_Q + c) * 64] = H.q[c]; kin[(RK_X + c) * 64] = H.x[c]; kin[(RK_LA + c) * 64] = H.la[c];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (r < P.buf_size) kin[(RK_ABUF + 4 * r + c) * 64] = H.abuf[r][c];
+        } else if (NOISE) {
+            float held[10];
+            held_combine(H, hn, held);
+            float* ho = L.ho + lane;
+            const int hb = wave == 2 ? RO_HELD1 : RO_HELD2, nb = wave == 2 ? RO_NG1 : RO_NG2;
+#pragma unroll
+            for (int c = 0; c < 10; ++c) ho[(hb + c) * 64] = held[c];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) ho[(nb + c) * 64] = ngs[c];
+        }
+        if (wave == PARAMS_WAVE) {
+            H.level = lvl;
+            H.level_idx = lvl_idx;
+            reset_params<DR, true>(P, H, gr);
+            float* par = L.par + lane;
+            par[RP_DT * 64] = H.dt; par[RP_M * 64] = H.m;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { par[(RP_J + c) * 64] = H.J[c]; par[(RP_DSTB + c) * 64] = H.dstb[c]; }
+            par[RP_K0 * 64] = H.k0; par[RP_K1 * 64] = H.k1;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { par[(RP_B + c) * 64] = H.B[c]; par[(RP_K + c) * 64] = H.K[c]; }
+            par[RP_LEVEL * 64] = H.level;
+            par[RP_LEVEL_IDX * 64] = ib(H.level_idx);
+        }
+    }
+    lds_barrier();                               // B_k
+    if (P.auto_reset && live && wave == PARAMS_WAVE) {
+        const uint64_t mask = ((uint64_t)L.mask[1] << 32) | (uint64_t)L.mask[0];
+        if ((mask >> lane) & 1ull) { lvl = H.level; lvl_idx = H.level_idx; }   // the new episode's level
+    }
+}
+
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepIO io0, uint32_t K, uint32_t act_stride) {
     const KParams P = shape_view<SPEC>(P0);
@@ -2591,6 +2754,7 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
     __shared__ float s_draw[HD ? HD_WORDS * 64 : 1];
     __shared__ uint32_t s_mask[2];
     __shared__ double s_hjgrid[6 * HJ_PTS];
+    const SmallRollLds L{s_obs, s_kin, s_par, s_ho, s_draw, s_mask};
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
     const uint32_t base = blockIdx.x * 64u, i = base + lane, gid = P.gid_off + i;
     const bool live = i < P.N;
@@ -2601,7 +2765,6 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
         __builtin_amdgcn_s_setprio(3);
         Env E;
         if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, need_level, /*with_hist=*/true);
-        float* obs_row = s_obs + lane * OD;
         for (uint32_t k = 0; k < K; ++k) {
             StepIO io = io0;
             io.act = io0.act + (size_t)k * act_stride;
@@ -2611,80 +2774,7 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
             if (io0.cost) io.cost = io0.cost + (size_t)k * n;
             if (io0.level) io.level = io0.level + (size_t)k * n;
             if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
-            if (!HD) lds_barrier();                  // A_k (HD: inside the env-step, before sub-step 1)
-            bool do_reset = false;
-            ResetSeed rs;
-            if (live)
-                do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD>(P, io, i, E, obs_row, rs, s_hjgrid,
-                                                                                     s_draw + lane);
-            const uint64_t m = __ballot(do_reset);
-            if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
-            lds_barrier();                           // B_k: the helpers' records of step k are in LDS
-            if (do_reset) {
-                const float stale[3] = {rs.wb[0], rs.wb[1], rs.wb[2]};   // the gyro LPF seed
-                const float* kin = s_kin + lane;
-                const float* par = s_par + lane;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    E.p[c] = kin[(RK_P + c) * 64]; E.v[c] = kin[(RK_V + c) * 64]; E.w[c] = kin[(RK_W + c) * 64];
-                    E.rpy[c] = kin[(RK_RPY + c) * 64]; E.wb[c] = kin[(RK_WB + c) * 64];
-                }
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    E.q[c] = kin[(RK_Q + c) * 64]; E.x[c] = kin[(RK_X + c) * 64]; E.xl[c] = 0.0f;
-                    E.la[c] = kin[(RK_LA + c) * 64];
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) E.abuf[r][c] = r < P.buf_size ? kin[(RK_ABUF + 4 * r + c) * 64] : 0.0f;
-                E.ep_step = 0; E.aidx = 0; E.props_on = 0; E.la_view = 1;
-                E.dt = par[RP_DT * 64]; E.m = par[RP_M * 64];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) { E.J[c] = par[(RP_J + c) * 64]; E.dstb[c] = par[(RP_DSTB + c) * 64]; }
-                E.k0 = par[RP_K0 * 64]; E.k1 = par[RP_K1 * 64];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) { E.B[c] = par[(RP_B + c) * 64]; E.K[c] = par[(RP_K + c) * 64]; }
-                E.level = par[RP_LEVEL * 64];
-                E.level_idx = bi(par[RP_LEVEL_IDX * 64]);
-                E.gust_left = 0;
-                // the reset observation (reset_observe): two sensor calls, then the history row
-                float o0[17], o1[17];
-                if (NOISE) {
-                    const float* ho = s_ho + lane;
-                    float ng1[9], ng2[9];
-#pragma unroll
-                    for (int c = 0; c < 9; ++c) { ng1[c] = ho[(RO_NG1 + c) * 64]; ng2[c] = ho[(RO_NG2 + c) * 64]; }
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) E.lpf[c] = stale[c];
-#pragma unroll
-                    for (int c = 0; c < 10; ++c) { o0[c] = ho[(RO_HELD1 + c) * 64]; o1[c] = ho[(RO_HELD2 + c) * 64]; }
-#pragma unroll
-                    for (int c = 0; c < 10; ++c) E.held[c] = o1[c];
-                    gyro_update(P, E, ng1);
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) o0[10 + c] = E.lpf[c];
-                    gyro_update(P, E, ng2);
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) o1[10 + c] = E.lpf[c];
-                } else {
-                    const float o[17] = {E.p[0], E.p[1], E.p[2], E.q[0], E.q[1], E.q[2], E.q[3], E.v[0], E.v[1],
-                                         E.v[2], E.wb[0], E.wb[1], E.wb[2], E.la[0], E.la[1], E.la[2], E.la[3]};
-#pragma unroll
-                    for (int c = 0; c < 17; ++c) { o0[c] = o[c]; o1[c] = o[c]; }
-                }
-                float row[OD];
-#pragma unroll
-                for (int c = 0; c < OL; ++c) { row[c] = o0[c]; row[OL + 4 + c] = o1[c]; E.obs_prev[c] = o1[c]; }
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    row[OL + c] = E.la[c]; row[2 * OL + 4 + c] = E.la[c];
-                    E.hact[0][c] = E.la[c]; E.hact[1][c] = E.la[c];
-                }
-                E.halias0 = E.halias1 = 1;
-#pragma unroll
-                for (int c = 0; c < OD; c += 2) *reinterpret_cast<float2*>(obs_row + c) = make_float2(row[c], row[c + 1]);
-            }
+            small_roll_env_step<NOISE, DR, PHYS, SPEC>(P, io, i, lane, live, E, L, s_hjgrid);
             // this wave's 64 rows, written by this wave only: its LDS writes land before its reads
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             write_obs_rows(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs, P.N - base < 64u ? P.N - base : 64u,
@@ -2707,64 +2797,125 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
         }
     }
     const Keys Kh = make_keys(P.key0, P.key1);
+    for (uint32_t k = 0; k < K; ++k, ++ctr)
+        small_roll_helper_step<NOISE, DR, PHYS, SPEC>(P, Kh, ctr, gid, wave, lane, live, lvl, lvl_idx, L);
+}
+
+// The collect loop in one launch at small N (N <= 32 768: the 8-GPU node shard, C2).  A 512-thread
+// block holds two 64-env groups, each run as rollout_kernel_small runs its block (wave 0 of the
+// group steps its envs with the state in registers, waves 1-3 compute the potential resets and the
+// step's draws), and after each env-step all 8 waves run the policy forward, one 16-row tile each,
+// on the block's 128 new observations (still in LDS), whose actions the next env-step reads.
+// Per step: barriers A_k, B_k (rollout_kernel_small's), P_k (every reset row is in LDS) and Q_k
+// (the step's actions are visible to the env waves).  LDS: the fragments (60.8 KB, staged once)
+// and two groups' records (2 x 46.6 KB): one block per CU, 8 waves, as two blocks of
+// step_kernel_small; 32 768 envs are one residency round of 256 blocks.  Outputs bit-identical
+// to K cf2_collect_step launches (the same device code for both halves).
+constexpr uint32_t CROLL_SMALL_BLOCK = 512;
+template <bool NOISE, bool DR, int PHYS, int SPEC>
+__global__ void __launch_bounds__(CROLL_SMALL_BLOCK, 1) collect_rollout_kernel_small(KParams P0, StepIO io0,
+                                                                                    PolicyIO pio, uint32_t K) {
+    static_assert(NOISE && SPEC == 1, "the fused collect kernels are built for the reference-default shape with noise");
+    const KParams P = shape_view<SPEC>(P0);
+    constexpr int OD = 34;
+    constexpr uint32_t PARAMS_WAVE = 1u;
+    using PK = Packed<OD, CF2_POLICY_BF16X3>;
+    static_assert(PK::TOTAL % 4 == 0, "float4 staging");
+    __shared__ __align__(16) float s_frag[PK::TOTAL];
+    __shared__ __align__(16) float s_obs[2][64 * OD];
+    __shared__ float s_kin[2][RK_WORDS * 64];
+    __shared__ float s_par[2][RP_WORDS * 64];
+    __shared__ float s_ho[2][RO_WORDS * 64];
+    __shared__ float s_draw[2][HD_WORDS * 64];
+    __shared__ uint32_t s_mask[2][2];
+    __shared__ double s_hjgrid[6 * HJ_PTS];
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, grp = wv >> 2, wave = wv & 3u, lane = tid & 63u;
+    const uint32_t base = blockIdx.x * 128u, gbase = base + 64u * grp, i = gbase + lane, gid = P.gid_off + i;
+    const bool live = i < P.N;
+    const SmallRollLds L{s_obs[grp], s_kin[grp], s_par[grp], s_ho[grp], s_draw[grp], s_mask[grp]};
+    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
+    {
+        const float4* src = reinterpret_cast<const float4*>(pio.w);
+        float4* dst = reinterpret_cast<float4*>(s_frag);
+        for (uint32_t q = tid; q < PK::TOTAL / 4; q += CROLL_SMALL_BLOCK) dst[q] = src[q];
+    }
+    __syncthreads();                             // the fragments are in LDS
+    const size_t n = P0.out_stride;              // rows per output slab (the whole population)
+    const uint32_t nrows = P.N - base < 128u ? P.N - base : 128u;    // rows of this block (> 0)
+    // policy tile of this wave: block rows 16 wv .. 16 wv + 15 (group wv / 4, its rows 16 (wv & 3) ..)
+    const uint32_t r16 = lane & 15u, trow = 16u * wv + r16;
+    const int g = (int)(lane >> 4);
+    const float* trow_lds = &s_obs[wv >> 2][(16u * (wv & 3u) + r16) * OD];
+    auto policy_tile = [&](uint32_t k) {
+        float ep[4];
+        policy_noise(pio.key0, pio.key1, pio.counter + k, pio.row_offset + base + trow, ep);   // lanes 0-15 use it
+        PolicyLane<OD, CF2_POLICY_BF16X3> CL;
+        policy_lane_init<OD, CF2_POLICY_BF16X3>(s_frag + PK::O_BIAS, g, CL);
+        ObsRegs<OD, CF2_POLICY_BF16X3, 1> Xc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float2 v = *reinterpret_cast<const float2*>(trow_lds + 8 * g + 2 * q);
+            Xc.x8[0][0][2 * q] = v.x;
+            Xc.x8[0][0][2 * q + 1] = v.y;
+        }
+        Xc.x1[0][0] = trow_lds[__builtin_elementwise_min(32 + g, OD - 1)];
+        policy_standardize<OD, CF2_POLICY_BF16X3, 1>(s_frag + PK::O_BIAS, g, CL, Xc);
+        f4v o[1];
+        policy_layers<OD, CF2_POLICY_BF16X3, 0, 1>(s_frag, s_frag + PK::O_BIAS, s_frag + PK::O_L3, (int)lane, Xc, o);
+        if (trow < nrows)
+            policy_emit_eps<OD, CF2_POLICY_BF16X3, 0>(o[0], base + trow, g, CL, ep, 1,
+                                                      pio.act + (size_t)(k + 1) * n * 4, pio.val + (size_t)(k + 1) * n,
+                                                      pio.logp + (size_t)(k + 1) * n, nullptr);
+    };
+    // the block's rows of step k into its obs slab: this wave's 16 rows (read from LDS after P_k)
+    auto write_rows = [&](uint32_t k) {
+        const uint32_t r0 = 16u * wv;
+        if (r0 >= nrows) return;
+        const uint32_t nr = nrows - r0 < 16u ? nrows - r0 : 16u;
+        const float2* src = reinterpret_cast<const float2*>(&s_obs[wv >> 2][16u * (wv & 3u) * OD]);
+        float2* dst = reinterpret_cast<float2*>(io0.obs + (size_t)k * n * OD + (size_t)(base + r0) * OD);
+        for (uint32_t q = lane; q < nr * (OD / 2); q += 64u) dst[q] = src[q];
+    };
+    if (wave == 0) {
+        __builtin_amdgcn_s_setprio(3);
+        Env E;
+        if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, P.need_level, /*with_hist=*/true);
+        for (uint32_t k = 0; k < K; ++k) {
+            StepIO io = io0;
+            io.act = pio.act + (size_t)k * n * 4;
+            io.rew = io0.rew + (size_t)k * n;
+            io.done = io0.done + (size_t)k * n;
+            if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
+            if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+            small_roll_env_step<NOISE, DR, PHYS, SPEC>(P, io, i, lane, live, E, L, s_hjgrid);
+            lds_barrier();                       // P_k: every row of the block is in LDS
+            write_rows(k);
+            policy_tile(k);
+            __syncthreads();                     // Q_k: step k + 1's actions are visible, s_obs is free
+        }
+        if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
+        return;
+    }
+    // helper waves 1-3 of the group
+    __builtin_amdgcn_s_setprio(0);
+    uint32_t ctr = 0;
+    float lvl = 0.0f;
+    int lvl_idx = 0;
+    if (live) {
+        const Tile T(io0.sf, P.N, i);
+        ctr = (uint32_t)bi(T.ld(G_CORE3).z);
+        if (wave == PARAMS_WAVE) {
+            lvl = P.need_level ? T.ld(G_LEVEL).w : P.level_fixed;
+            lvl_idx = P.need_level && P.level_mode != LEVEL_FIXED_T ? bi(T.ld(G_LEVEL_IDX).x) : 0;
+        }
+    }
+    const Keys Kh = make_keys(P.key0, P.key1);
     for (uint32_t k = 0; k < K; ++k, ++ctr) {
-        if (HD) {
-            if (live) helper_step_draws(Kh, ctr, gid, wave, s_draw + lane);
-        }
-        lds_barrier();                               // A_k
-        Env H;
-        if (P.auto_reset && live) {
-            const Rng gr{Kh, ctr, gid, TAG_RESET};
-            HeldNoise hn;
-            float ngs[9];
-            if (NOISE && wave >= 2) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
-            reset_kinematics<PHYS, true>(P, H, gr, gid);
-            if (wave == 1) {
-                float* kin = s_kin + lane;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    kin[(RK_P + c) * 64] = H.p[c]; kin[(RK_V + c) * 64] = H.v[c]; kin[(RK_W + c) * 64] = H.w[c];
-                    kin[(RK_RPY + c) * 64] = H.rpy[c]; kin[(RK_WB + c) * 64] = H.wb[c];
-                }
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    kin[(RK_Q + c) * 64] = H.q[c]; kin[(RK_X + c) * 64] = H.x[c]; kin[(RK_LA + c) * 64] = H.la[c];
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        if (r < P.buf_size) kin[(RK_ABUF + 4 * r + c) * 64] = H.abuf[r][c];
-            } else if (NOISE) {
-                float held[10];
-                held_combine(H, hn, held);
-                float* ho = s_ho + lane;
-                const int hb = wave == 2 ? RO_HELD1 : RO_HELD2, nb = wave == 2 ? RO_NG1 : RO_NG2;
-#pragma unroll
-                for (int c = 0; c < 10; ++c) ho[(hb + c) * 64] = held[c];
-#pragma unroll
-                for (int c = 0; c < 9; ++c) ho[(nb + c) * 64] = ngs[c];
-            }
-            if (wave == PARAMS_WAVE) {
-                H.level = lvl;
-                H.level_idx = lvl_idx;
-                reset_params<DR, true>(P, H, gr);
-                float* par = s_par + lane;
-                par[RP_DT * 64] = H.dt; par[RP_M * 64] = H.m;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) { par[(RP_J + c) * 64] = H.J[c]; par[(RP_DSTB + c) * 64] = H.dstb[c]; }
-                par[RP_K0 * 64] = H.k0; par[RP_K1 * 64] = H.k1;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) { par[(RP_B + c) * 64] = H.B[c]; par[(RP_K + c) * 64] = H.K[c]; }
-                par[RP_LEVEL * 64] = H.level;
-                par[RP_LEVEL_IDX * 64] = ib(H.level_idx);
-            }
-        }
-        lds_barrier();                               // B_k
-        if (P.auto_reset && live && wave == PARAMS_WAVE) {
-            const uint64_t mask = ((uint64_t)s_mask[1] << 32) | (uint64_t)s_mask[0];
-            if ((mask >> lane) & 1ull) { lvl = H.level; lvl_idx = H.level_idx; }   // the new episode's level
-        }
+        small_roll_helper_step<NOISE, DR, PHYS, SPEC>(P, Kh, ctr, gid, wave, lane, live, lvl, lvl_idx, L);
+        lds_barrier();                           // P_k
+        write_rows(k);
+        policy_tile(k);
+        __syncthreads();                         // Q_k
     }
 }
 
@@ -2904,7 +3055,7 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 // and the slice size of the fused rollout.
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t occupancy_t(KParams& P) {
-    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0, per_croll = 0;
+    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0, per_croll = 0, per_croll_small = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
@@ -2919,11 +3070,16 @@ static hipError_t occupancy_t(KParams& P) {
         if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_croll, collect_rollout_kernel<NOISE, DR, PHYS, SPEC>,
                                                              STEP_BLOCK, 0);
+    if constexpr (NOISE && SPEC == 1 && PHYS == PHYS_BULLET_T)
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_croll_small, collect_rollout_kernel_small<NOISE, DR, PHYS, SPEC>, CROLL_SMALL_BLOCK, 0);
     if (e != hipSuccess) return e;
     P.rb_step = (uint32_t)(cus * (per_step > 0 ? per_step : 1));
     P.rb_roll = (uint32_t)(cus * (per_roll > 0 ? per_roll : 1));
     P.rb_collect = (uint32_t)(cus * (per_collect > 0 ? per_collect : 1));
     P.rb_croll = (uint32_t)(cus * (per_croll > 0 ? per_croll : 1));
+    P.rb_croll_small = (uint32_t)(cus * (per_croll_small > 0 ? per_croll_small : 1));
     return hipSuccess;
 }
 
@@ -3017,40 +3173,21 @@ static hipError_t launch_collect_rollout_t(const KParams& P, const StepIO& io, c
         return hipErrorNotSupported;
     } else {
         constexpr uint32_t OD = 34;
-        if (P.N <= SMALL_N_MAX) {
-            // small N: K collect_kernel_small launches (64 envs per block with the helper waves), whose
-            // chain is shorter than a 256-env block's here, and which fill all CUs at the node shard
-            for (uint32_t k = 0; k < K; ++k) {
-                StepIO iok = io;
-                iok.act = pio.act + (size_t)k * P.N * 4;
-                iok.obs = io.obs + (size_t)k * P.N * OD;
-                iok.rew = io.rew + (size_t)k * P.N;
-                iok.done = io.done + (size_t)k * P.N;
-                if (io.trunc) iok.trunc = io.trunc + (size_t)k * P.N;
-                if (io.final_obs) iok.final_obs = io.final_obs + (size_t)k * P.N * OD;
-                PolicyIO pk = pio;
-                pk.counter = pio.counter + k;
-                pk.act = pio.act + (size_t)(k + 1) * P.N * 4;
-                pk.val = pio.val + (size_t)(k + 1) * P.N;
-                pk.logp = pio.logp + (size_t)(k + 1) * P.N;
-                hipLaunchKernelGGL((collect_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0,
-                                   s, P, iok, pk);
-                const hipError_t e = hipGetLastError();
-                if (e != hipSuccess) return e;
-            }
-            return hipSuccess;
-        }
         // slices of one residency round each (as launch_rollout_t): a slice's blocks run all K steps
-        // together.  Every output slab keeps the whole population's stride.
-        const uint32_t blocks = (P.N + STEP_BLOCK - 1) / STEP_BLOCK;
-        const uint32_t round_blocks = P.rb_croll > 0 ? P.rb_croll : 1u;
+        // together.  Every output slab keeps the whole population's stride.  Small N: 128-env blocks
+        // of two helper-wave groups (collect_rollout_kernel_small), one per CU.
+        const bool small = P.N <= SMALL_N_MAX;
+        const uint32_t epb = small ? 128u : STEP_BLOCK;
+        const uint32_t blocks = (P.N + epb - 1) / epb;
+        const uint32_t round_blocks = small ? (P.rb_croll_small > 0 ? P.rb_croll_small : 1u)
+                                            : (P.rb_croll > 0 ? P.rb_croll : 1u);
         const uint32_t nslices = (blocks + round_blocks - 1) / round_blocks;
         const uint32_t per = (blocks + nslices - 1) / nslices;
         for (uint32_t b0 = 0; b0 < blocks; b0 += per) {
             const uint32_t nb = blocks - b0 < per ? blocks - b0 : per;
-            const uint32_t e0 = b0 * STEP_BLOCK;
+            const uint32_t e0 = b0 * epb;
             KParams Ps = P;
-            Ps.N = (P.N - e0 < nb * STEP_BLOCK) ? P.N - e0 : nb * STEP_BLOCK;
+            Ps.N = (P.N - e0 < nb * epb) ? P.N - e0 : nb * epb;
             Ps.gid_off = P.gid_off + e0;
             Ps.out_stride = P.N;
             StepIO ios = io;
@@ -3065,8 +3202,12 @@ static hipError_t launch_collect_rollout_t(const KParams& P, const StepIO& io, c
             ps.act = pio.act + (size_t)e0 * 4;
             ps.val = pio.val + e0;
             ps.logp = pio.logp + e0;
-            hipLaunchKernelGGL((collect_rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(STEP_BLOCK), 0, s, Ps, ios,
-                               ps, K);
+            if (small)
+                hipLaunchKernelGGL((collect_rollout_kernel_small<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(CROLL_SMALL_BLOCK),
+                                   0, s, Ps, ios, ps, K);
+            else
+                hipLaunchKernelGGL((collect_rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(STEP_BLOCK), 0, s, Ps,
+                                   ios, ps, K);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -308,9 +308,8 @@ int  cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float*
 
 /* K steps of the collect loop in one launch: env-step k (actions act_dev + k*N*4) and then the
  * policy forward + sampling on its observations (noise counter counter + k), whose actions the
- * next env-step takes; the env state stays in registers for the K steps.  At N <= 32768 (the
- * 8-GPU node shard) the call issues K launches of the per-step fused kernel instead (64-env blocks
- * with helper waves, a shorter chain at that size); the outputs are the same either way.  Buffers, slab-major:
+ * next env-step takes; the env state stays in registers for the K steps (N <= 32768, the 8-GPU
+ * node shard: 64-env groups with helper waves computing the auto-resets, as cf2_step there).  Buffers, slab-major:
  * act_dev [K+1,N,4] (slab 0 in: the first step's actions; slabs 1..K out), val_dev / logp_dev
  * [K+1,N] (slabs 1..K out, slab 0 untouched), obs_dev [K,N,obs_dim] (slab k = the observation
  * after env-step k), rew_dev / done_dev [K,N], trunc_dev / final_obs_dev [K,N] / [K,N,obs_dim]

@@ -77,11 +77,27 @@ static double spread_us(uint64_t* d, std::vector<uint64_t>& h, int blocks, float
     return sp[sp.size() / 2];
 }
 
-int main() {
-    const int waves = 2048;
+int main(int argc, char** argv) {
+    const int max_waves = 4096;
     uint64_t* d;
-    (void)hipMalloc(&d, (size_t)waves * 16);
-    std::vector<uint64_t> h((size_t)waves * 2);
+    (void)hipMalloc(&d, (size_t)max_waves * 16);
+    std::vector<uint64_t> h((size_t)max_waves * 2);
+    if (argc > 1) {
+        // sweep: start spread and back-to-back launch time against the number of waves per launch
+        // (how much of a short kernel's time the dispatch ramp of its waves is)
+        for (int pass = 0; pass < 2; ++pass)
+            for (int threads : {256, 64})
+                for (int waves : {256, 512, 1024, 2048, 4096}) {
+                    double t;
+                    const int blocks = waves * 64 / threads;
+                    const double sp = spread_us<688>(d, h, blocks, 2000.0f, 11, &t, threads);
+                    printf("%4d waves as %4d blocks x %4d threads: median start spread %.2f us, back-to-back %.2f us per launch\n",
+                           waves, blocks, threads, sp, t);
+                }
+        (void)hipFree(d);
+        return 0;
+    }
+    const int waves = 2048;
     for (int pass = 0; pass < 2; ++pass) {
         double t;
         double s16 = spread_us<16>(d, h, 512, 2000.0f, 15, &t);

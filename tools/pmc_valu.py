@@ -72,15 +72,26 @@ def summarize(rows, label, env_steps_per_dispatch, dur_ns=None):
 sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
 from cf2sim.build import _obj_key
 key = _obj_key("cf2sim_kernels.hip")
-step = per_dispatch("step_kernel")[-30:]
-roll = per_dispatch("rollout_kernel")
+# kernel names as the trace prints them (cf2::name<...>): exact, so that "rollout_kernel" does not
+# also match collect_rollout_kernel
+STEP, ROLL, COLL, CROLL = "cf2::step_kernel<", "cf2::rollout_kernel<", "cf2::collect_kernel<", "cf2::collect_rollout_kernel<"
+
+
+def collect_entry(kern, label, steps_per_dispatch):
+    rows = per_dispatch(kern, "pmc_collect")
+    if not rows:
+        return None
+    return dict(summarize(rows, label, steps_per_dispatch, durations(kern, "pmc_collect")), **(mfma_busy(kern) or {}))
+
+
+step = per_dispatch(STEP)[-30:]
+roll = per_dispatch(ROLL)
+K = int(os.environ.get("CF2_COLLECT_K", "32"))       # tools/collect_bench.py --slabs
 res = {"workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}", "kernel_key": key,
-       "step_kernel": summarize(step, "step_kernel", 1, durations("step_kernel")[-30:]),
-       "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations("rollout_kernel")),
-       "collect_kernel": (dict(summarize(per_dispatch("collect_kernel", "pmc_collect"),
-                                         "collect_kernel (env-step + policy)", 1, durations("collect_kernel", "pmc_collect")),
-                               **(mfma_busy("collect_kernel") or {}))
-                          if per_dispatch("collect_kernel", "pmc_collect") else None),
+       "step_kernel": summarize(step, "step_kernel", 1, durations(STEP)[-30:]),
+       "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations(ROLL)),
+       "collect_kernel": collect_entry(COLL, "collect_kernel (env-step + policy)", 1),
+       "collect_rollout_kernel": collect_entry(CROLL, f"collect_rollout_kernel (K={K} env-steps + policy)", K),
        "note": __doc__.split("\n\n")[1]}
 prof = os.path.join(ROOT, "profiles", "valu_issue.json")
 try:
