@@ -608,15 +608,17 @@ def main(argv=None):
         rows, dn = env.obs.clone(), env.done.clone()
         prev = rows.clone()
         cur = torch.empty_like(rows)
-        age = torch.full((n,), 3, dtype=torch.uint8, device=dev)
+        age = torch.full((n,), 3, dtype=torch.int16, device=dev)          # uint16 storage, as the exchange keeps it
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         reps = 20
         torch.cuda.synchronize()
         ev[0].record(stream)
         for _ in range(reps):
             for r in range(W8):
-                send[r * words:r * words + 1].zero_()
-                pack_obs(rows[r * n8:(r + 1) * n8], dn[r * n8:(r + 1) * n8], cap, out=send[r * words:(r + 1) * words])
+                # each pack zeroes the next buffer's count word (clear_next), as the ranks' packs do
+                nx = (r + 1) % W8
+                pack_obs(rows[r * n8:(r + 1) * n8], dn[r * n8:(r + 1) * n8], cap, out=send[r * words:(r + 1) * words],
+                         clear_next=send[nx * words:nx * words + 1])
         ev[1].record(stream)
         for _ in range(reps):
             unpack_obs(send, W8, n8, ol, cap, acts_g[1], acts_g[0], age, prev, cur)

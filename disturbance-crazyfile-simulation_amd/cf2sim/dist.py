@@ -100,6 +100,11 @@ def _bits_to_mask(words, n):
     return torch.from_numpy(np.unpackbits(b, bitorder="little")[:n].astype(bool))
 
 
+def _need(ok: bool, what: str):
+    if not ok:
+        raise ValueError(f"delta exchange: {what}")
+
+
 def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
     """One rank's packed buffer (int32 [packed_words]) from its step's obs rows [n, OD] and
     auto-reset flags [n] (uint8 or bool)."""
@@ -113,6 +118,12 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
     if obs.is_cuda:
         from . import _native
         lib = _native.load()
+        # the kernel indexes by these sizes: check them on the host before the launch
+        _need(obs.is_contiguous() and obs.dtype == torch.float32, "obs must be contiguous float32 [n, OD]")
+        _need(reset.numel() >= n and reset.is_cuda, "reset needs n flags on the GPU")
+        _need(out.dtype == torch.int32 and out.is_contiguous() and out.numel() >= words and out.is_cuda,
+              f"out needs {words} int32 words on the GPU")
+        _need(clear_next is None or (clear_next.is_cuda and clear_next.numel() >= 1), "clear_next needs 1 word")
         r8 = reset if reset.dtype == torch.uint8 else reset.to(torch.uint8)
         _native.check(lib.cf2_obs_pack(obs.data_ptr(), r8.contiguous().data_ptr(), n, ol, cap, out.data_ptr(),
                                        _native.ptr(clear_next), torch.cuda.current_stream(obs.device).cuda_stream),
@@ -153,6 +164,17 @@ def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, 
     if recv.is_cuda:
         from . import _native
         lib = _native.load()
+        # the kernels index by these sizes: check them on the host before the launch
+        N, od = world * n, 2 * (ol + 4)
+        _need(recv.dtype == torch.int32 and recv.is_contiguous() and recv.numel() >= world * packed_words(n, ol, cap),
+              "recv needs world * packed_words int32 words")
+        _need(age.dtype == torch.int16 and age.is_contiguous() and age.numel() >= N and age.is_cuda,
+              "age must be int16 (uint16 storage) [world * n] on the GPU")
+        for name, t, cols in (("act", act, 4), ("act_prev", act_prev, 4), ("slab_prev", slab_prev, od), ("slab", slab, od)):
+            _need(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= N * cols,
+                  f"{name} must be contiguous float32 [world * n, {cols}] on the GPU")
+        for name, t, k in (("overflow", overflow, 1), ("pred", pred, world), ("pred_next", pred_next, world)):
+            _need(t is None or (t.is_cuda and t.dtype == torch.int32 and t.numel() >= k), f"{name} needs {k} int32")
         _native.check(lib.cf2_obs_unpack(recv.data_ptr(), world, n, ol, cap, act.data_ptr(), act_prev.data_ptr(),
                                          age.data_ptr(), slab_prev.data_ptr(), slab.data_ptr(), _native.ptr(overflow),
                                          int(watch_age) & 0xFFFFFFFF, _native.ptr(pred), _native.ptr(pred_next),
@@ -236,6 +258,10 @@ class PipelinedObsGather:
         cuda = self.device.type == "cuda"
         self.obs = [torch.empty(n, obs_dim, device=device) for _ in range(self.depth)]
         self.comm = torch.cuda.Stream(device=self.device) if (self.nccl and cuda) else None
+        # delta: the unpack (every rank rebuilds all rows) runs on a stream of its own, so that the
+        # all-gather of step k + 1 overlaps the rebuild of step k
+        self.ustream = torch.cuda.Stream(device=self.device) if (self.comm is not None and delta) else None
+        self.recv_free = [None] * self.depth  # events: the unpack that read recv buffer j is done
         self.free = [None] * self.depth      # events: the exchange of the step that used buffer j read it
         self.k = 0
         self.started = not self.delta
@@ -308,6 +334,10 @@ class PipelinedObsGather:
     def start(self, obs):
         """delta: gather the observations of a reset of every env ([n, D]) in full; every env's
         step count since its reset is 0 on every rank."""
+        if self.ustream is not None:                 # a restart: no rebuild still in flight
+            self.comm.wait_stream(self.ustream)
+        self.recv_free = [None] * self.depth
+
         def run():
             self._gather(self.slab[1], obs.contiguous())
             self.age.zero_()
@@ -369,17 +399,7 @@ class PipelinedObsGather:
         ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
         send, recv = self.send[j][:words], self.recv[j][:self.world * words]
 
-        def run():
-            pack_obs(self.obs[j], self.done[j], cap, out=send, clear_next=self.send[(j + 1) % self.depth][:1])
-            if self.comm is not None:
-                ev = torch.cuda.Event()
-                ev.record(self.comm)
-                self.free[j] = ev
-            if recv.is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
-                host = gather_rows(send.cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
-                recv.copy_(host.reshape(-1))
-            else:
-                self._gather(recv, send)
+        def unpack():
             watch = self.watch if self.watch != NO_WATCH else NO_WATCH
             unpack_obs(recv, self.world, self.n, self.ol, cap, act, act_prev, self.age, prev, cur, self.overflow,
                        watch, self.pred[ps] if watch != NO_WATCH else None,
@@ -392,8 +412,29 @@ class PipelinedObsGather:
                     self.pred_ev[ps] = pe
             if self.comm is not None:
                 ev2 = torch.cuda.Event()
-                ev2.record(self.comm)
+                ev2.record(torch.cuda.current_stream(self.device))
                 self._ready = ev2
+                self.recv_free[j] = ev2
+
+        def run():
+            pack_obs(self.obs[j], self.done[j], cap, out=send, clear_next=self.send[(j + 1) % self.depth][:1])
+            if self.comm is not None:
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+                self.free[j] = ev
+                if self.recv_free[j] is not None:  # the unpack of step k - depth read recv[j]
+                    self.comm.wait_event(self.recv_free[j])
+            if recv.is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
+                host = gather_rows(send.cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
+                recv.copy_(host.reshape(-1))
+            else:
+                self._gather(recv, send)
+            if self.ustream is None:
+                unpack()
+            else:                                   # after the gather, beside the next step's gather
+                self.ustream.wait_stream(self.comm)
+                with torch.cuda.stream(self.ustream):
+                    unpack()
             return cur
         out = self._run_on_comm(run)
         self.bytes_sent += 4 * words
@@ -417,6 +458,8 @@ class PipelinedObsGather:
         import torch
         if self.comm is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm)
+        if self.ustream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.ustream)
         for j in range(self.depth):
             self.free[j] = None
 

@@ -52,10 +52,9 @@ struct PackLayout {
 };
 
 constexpr uint32_t XB = 256;        // rows per block
-constexpr uint32_t XMAX_OD = 42;    // 34 with sensor noise, 42 without
 
-// Coalesced copy of `rows` rows of `od` floats (contiguous, 16-B aligned when `al`) between global
-// memory and LDS, all threads of the block
+// Coalesced copy of `count` floats (16-B aligned, a multiple of 4) between global memory and LDS,
+// all threads of the block; the scalar form for a ragged tail block
 __device__ __forceinline__ void rows_to_lds(float* s, const float* g, uint32_t count, bool al) {
     if (al && (count & 3u) == 0) {
         const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -75,57 +74,68 @@ __device__ __forceinline__ void lds_to_rows(float* g, const float* s, uint32_t c
     }
 }
 
-// Sender: one thread per env of this rank.  The block's obs rows are read coalesced into LDS, o_k
-// extracted into an LDS stage and written as one contiguous run of the o_k slab; the reset bitmap
-// comes from wave ballots; a reset env takes a side slot by a wave-aggregated atomic (the slot
-// order is immaterial: each entry carries its env index).  clear_next: the count word of the
-// buffer the next pack on this stream writes (its previous contents were gathered already), so the
-// counts need no separate memset.
+// Sender: one thread per env of this rank (OL: 13 with sensor noise, 17 without).  The block's obs
+// rows are read coalesced into LDS, o_k extracted into an LDS stage and written as one contiguous
+// run of the o_k slab; the reset bitmap comes from wave ballots; the block's resets take
+// consecutive side slots from one atomic per block on the count word (per-wave atomics on that one
+// word serialised at the L2: 19.5 us per 32 768-env pack), in an order that is immaterial (each
+// entry carries its env index).  clear_next: the count word of the buffer the next pack on this
+// stream writes (its previous contents were gathered already), so the counts need no memset.
+template <uint32_t OL>
 __global__ void __launch_bounds__(XB) obs_pack_kernel(const float* __restrict__ obs, const uint8_t* __restrict__ reset,
                                                       PackLayout L, uint32_t* __restrict__ pk,
                                                       uint32_t* __restrict__ clear_next) {
-    __shared__ __align__(16) float s_rows[XB * XMAX_OD];
-    __shared__ __align__(16) float s_o[XB * 17];
-    const uint32_t od = L.od(), ol = L.ol, tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
+    constexpr uint32_t OD = 2u * (OL + 4u);
+    __shared__ __align__(16) float s_rows[XB * OD];
+    __shared__ __align__(16) float s_o[XB * OL];
+    __shared__ uint32_t s_wcnt[XB / 64u + 1u];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid, lane = tid & 63u, wv = tid >> 6;
     const uint32_t nrow = L.n - base < XB ? L.n - base : XB;
     if (blockIdx.x == 0 && tid == 0) {
         if (clear_next) clear_next[0] = 0u;
-        pk[1] = L.n; pk[2] = L.ol; pk[3] = L.cap;
+        pk[1] = L.n; pk[2] = OL; pk[3] = L.cap;
     }
-    rows_to_lds(s_rows, obs + (size_t)base * od, nrow * od, ((uintptr_t)obs & 15u) == 0 && (base * od) % 4u == 0);
-    __syncthreads();
     const bool live = tid < nrow;
-    const float* row = s_rows + tid * od;
-    if (live)
-        for (uint32_t k = 0; k < ol; ++k) s_o[tid * ol + k] = row[ol + 4u + k];
     const bool r = live && reset[i] != 0;
     const uint64_t m = __ballot(r);
-    const uint32_t lane = tid & 63u, wbase = base + (tid & ~63u);
+    if (lane == 0) s_wcnt[wv] = (uint32_t)__popcll(m);
+    rows_to_lds(s_rows, obs + (size_t)base * OD, nrow * OD, ((uintptr_t)obs & 15u) == 0 && (base * OD) % 4u == 0);
+    __syncthreads();
+    const float* row = s_rows + tid * OD;
+    if (live) {
+#pragma unroll
+        for (uint32_t k = 0; k < OL; ++k) s_o[tid * OL + k] = row[OL + 4u + k];
+    }
     uint32_t* bits = pk + L.bits();
+    const uint32_t wbase = base + (tid & ~63u);
     if (lane == 0 && wbase < L.n) bits[wbase / 32u] = (uint32_t)m;
     if (lane == 32 && wbase + 32u < L.n) bits[wbase / 32u + 1u] = (uint32_t)(m >> 32);
-    if (m) {
-        const int leader = __ffsll((unsigned long long)m) - 1;
-        uint32_t first = 0;
-        if ((int)lane == leader) first = atomicAdd(pk, (uint32_t)__popcll(m));
-        first = __shfl(first, leader);
-        const uint32_t slot = first + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (r && slot < L.cap) {
-            uint32_t* e = pk + L.side() + slot * L.entry();
-            e[0] = tid + base;
-            float* ef = reinterpret_cast<float*>(e + 1);
-            for (uint32_t k = 0; k < ol + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
-        }
+    if (tid == 0) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < XB / 64u; ++w) { const uint32_t c = s_wcnt[w]; s_wcnt[w] = tot; tot += c; }
+        s_wcnt[XB / 64u] = tot ? atomicAdd(pk, tot) : 0u;      // the block's first side slot
     }
     __syncthreads();
-    lds_to_rows(reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * ol, s_o, nrow * ol,
-                ((uintptr_t)pk & 15u) == 0 && (base * ol) % 4u == 0);
+    if (r) {
+        const uint32_t slot = s_wcnt[XB / 64u] + s_wcnt[wv] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (slot < L.cap) {
+            uint32_t* e = pk + L.side() + slot * L.entry();
+            e[0] = i;
+            float* ef = reinterpret_cast<float*>(e + 1);
+#pragma unroll
+            for (uint32_t k = 0; k < OL + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
+        }
+    }
+    lds_to_rows(reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * OL, s_o, nrow * OL,
+                ((uintptr_t)pk & 15u) == 0 && (base * OL) % 4u == 0);
 }
 
 // Receiver, rows: one thread per global env (rank r = i / n).  The block's previous rows are read
 // coalesced into LDS, each thread rebuilds its row there, the block writes them out coalesced.
 // Reset rows get o_k here; their o_0 / A parts come from obs_unpack_resets_kernel, launched after
 // this one (NaN if the env's rank overflowed its side slab).
+template <uint32_t OL>
 __global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __restrict__ pk_all, uint32_t words,
                                                              uint32_t world, PackLayout L,
                                                              const float* __restrict__ act,
@@ -134,58 +144,68 @@ __global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __r
                                                              const float* __restrict__ slab_prev,
                                                              float* __restrict__ slab, uint32_t watch_age,
                                                              uint32_t* __restrict__ pred, uint32_t* __restrict__ pred_next) {
-    __shared__ __align__(16) float s_rows[XB * XMAX_OD];
-    const uint32_t od = L.od(), ol = L.ol, tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
+    constexpr uint32_t OD = 2u * (OL + 4u);
+    __shared__ __align__(16) float s_rows[XB * OD];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
     const uint32_t total = world * L.n;
     const uint32_t nrow = total - base < XB ? total - base : XB;
-    const bool al = (base * od) % 4u == 0 && ((uintptr_t)slab_prev & 15u) == 0 && ((uintptr_t)slab & 15u) == 0;
+    const bool al = (base * OD) % 4u == 0 && ((uintptr_t)slab_prev & 15u) == 0 && ((uintptr_t)slab & 15u) == 0;
     if (blockIdx.x == 0 && pred_next && tid < world) pred_next[tid] = 0u;     // the next step's counts
-    rows_to_lds(s_rows, slab_prev + (size_t)base * od, nrow * od, al);
+    // this thread's inputs first (their latency overlaps the block's row copy)
+    const bool live = tid < nrow;
+    const uint32_t ic = live ? i : total - 1u;
+    const uint32_t r = ic / L.n, li = ic - r * L.n;
+    const uint32_t* pk = pk_all + (size_t)r * words;
+    const float* okp = reinterpret_cast<const float*>(pk + L.o_slab()) + (size_t)li * OL;
+    float ok[OL];
+#pragma unroll
+    for (uint32_t k = 0; k < OL; ++k) ok[k] = okp[k];
+    const bool rs = (pk[L.bits() + li / 32u] >> (li % 32u)) & 1u;
+    const uint32_t a_old = age[ic];
+    const float4 ak = reinterpret_cast<const float4*>(act)[ic];
+    const float4 ap = reinterpret_cast<const float4*>(act_prev)[ic];
+    const bool ovf = pk[0] > L.cap;
+    rows_to_lds(s_rows, slab_prev + (size_t)base * OD, nrow * OD, al);
     __syncthreads();
-    uint32_t a_new = 0xFFFFFFFFu, rank = 0;
-    if (tid < nrow) {
-        const uint32_t r = i / L.n, li = i - r * L.n;
-        rank = r;
-        const uint32_t* pk = pk_all + (size_t)r * words;
-        const float* ok = reinterpret_cast<const float*>(pk + L.o_slab()) + (size_t)li * ol;
-        const bool rs = (pk[L.bits() + li / 32u] >> (li % 32u)) & 1u;
-        float* row = s_rows + tid * od;
+    uint32_t a_new = 0xFFFFFFFFu;
+    if (live) {
+        float* row = s_rows + tid * OD;
         if (rs) {
-            const bool ovf = pk[0] > L.cap;
-            for (uint32_t k = 0; k < ol; ++k) row[ol + 4u + k] = ok[k];
+#pragma unroll
+            for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = ok[k];
             if (ovf) {                      // o_0 and A were not sent: marked unknown
-                for (uint32_t k = 0; k < ol + 4u; ++k) row[k] = __builtin_nanf("");
-                for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = __builtin_nanf("");
+#pragma unroll
+                for (uint32_t k = 0; k < OL + 4u; ++k) row[k] = __builtin_nanf("");
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; ++k) row[2u * OL + 4u + k] = __builtin_nanf("");
             }
             age[i] = 0;
             a_new = 0;
         } else {
-            const uint32_t a = age[i] < 0xFFFFu ? age[i] + 1u : 0xFFFFu;
-            const float4 ak = reinterpret_cast<const float4*>(act)[i];
+            const uint32_t a = a_old < 0xFFFFu ? a_old + 1u : 0xFFFFu;
+            const float akv[4] = {ak.x, ak.y, ak.z, ak.w}, apv[4] = {ap.x, ap.y, ap.z, ap.w};
             float a0[4], a1[4];
-            if (a >= 3u) {
-                for (uint32_t k = 0; k < 4u; ++k) a0[k] = row[2u * ol + 4u + k];
-            } else {
-                a0[0] = ak.x; a0[1] = ak.y; a0[2] = ak.z; a0[3] = ak.w;
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k) {
+                a0[k] = a >= 3u ? row[2u * OL + 4u + k] : akv[k];
+                a1[k] = a == 1u ? akv[k] : apv[k];
             }
-            if (a == 1u) {
-                a1[0] = ak.x; a1[1] = ak.y; a1[2] = ak.z; a1[3] = ak.w;
-            } else {
-                const float4 ap = reinterpret_cast<const float4*>(act_prev)[i];
-                a1[0] = ap.x; a1[1] = ap.y; a1[2] = ap.z; a1[3] = ap.w;
-            }
-            for (uint32_t k = 0; k < ol; ++k) row[k] = row[ol + 4u + k];
-            for (uint32_t k = 0; k < 4u; ++k) row[ol + k] = a0[k];
-            for (uint32_t k = 0; k < ol; ++k) row[ol + 4u + k] = ok[k];
-            for (uint32_t k = 0; k < 4u; ++k) row[2u * ol + 4u + k] = a1[k];
+#pragma unroll
+            for (uint32_t k = 0; k < OL; ++k) row[k] = row[OL + 4u + k];
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k) row[OL + k] = a0[k];
+#pragma unroll
+            for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = ok[k];
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k) row[2u * OL + 4u + k] = a1[k];
             age[i] = (uint16_t)a;
             a_new = a;
         }
     }
     // time-out look-ahead: envs at age watch_age time out (unless they crash first) L steps later
-    if (pred && a_new == watch_age) atomicAdd(pred + rank, 1u);     // ~1/max_steps of the envs per step
+    if (pred && a_new == watch_age) atomicAdd(pred + r, 1u);     // ~1/max_steps of the envs per step
     __syncthreads();
-    lds_to_rows(slab + (size_t)base * od, s_rows, nrow * od, al);
+    lds_to_rows(slab + (size_t)base * OD, s_rows, nrow * OD, al);
 }
 
 // Receiver, resets: one thread per side slot of every rank; writes the reset row's o_0 and A
@@ -228,8 +248,12 @@ extern "C" int cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint
     if (!obs_dev || !reset_dev || !packed_dev || !layout_ok(n, obs_len, cap)) return CF2_ERR_INVALID_ARG;
     if (((uintptr_t)obs_dev & 7u) || ((uintptr_t)packed_dev & 15u)) return CF2_ERR_INVALID_ARG;
     const PackLayout L{n, obs_len, cap};
-    hipLaunchKernelGGL(obs_pack_kernel, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev, reset_dev,
-                       L, packed_dev, clear_next_dev);
+    if (obs_len == 13u)
+        hipLaunchKernelGGL(obs_pack_kernel<13>, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev,
+                           reset_dev, L, packed_dev, clear_next_dev);
+    else
+        hipLaunchKernelGGL(obs_pack_kernel<17>, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev,
+                           reset_dev, L, packed_dev, clear_next_dev);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
@@ -247,9 +271,14 @@ extern "C" int cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, ui
         return CF2_ERR_INVALID_ARG;
     const PackLayout L{n, obs_len, cap};
     const uint32_t words = L.words(), total = world * n;
-    hipLaunchKernelGGL(obs_unpack_rows_kernel, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
-                       packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
-                       watch_age, pred_dev, pred_next_dev);
+    if (obs_len == 13u)
+        hipLaunchKernelGGL(obs_unpack_rows_kernel<13>, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
+                           packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
+                           watch_age, pred_dev, pred_next_dev);
+    else
+        hipLaunchKernelGGL(obs_unpack_rows_kernel<17>, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
+                           packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
+                           watch_age, pred_dev, pred_next_dev);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && cap > 0) {
         hipLaunchKernelGGL(obs_unpack_resets_kernel, dim3((world * cap + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,

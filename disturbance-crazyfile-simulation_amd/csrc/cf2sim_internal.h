@@ -84,10 +84,10 @@ struct KParams {
     uint32_t late_block;          // step kernel: first block index past one residency round (set per launch)
     uint32_t out_stride;          // rollout kernel: rows per per-step output slab (set per launch)
     // host-side, set once at cf2_create for the context's device and configuration: blocks
-    // resident at once of the large-N step / fused rollout / fused collect / collect rollout
-    // kernels (query_occupancy), and whether the step's working set exceeds the Infinity Cache
+    // resident at once of the large-N step / fused rollout / fused collect kernels and of the
+    // small-N collect rollout kernel (query_occupancy), and whether the step's working set exceeds the Infinity Cache
     // (nt state stores)
-    uint32_t rb_step, rb_roll, rb_collect, rb_croll, rb_croll_small, nt_state;
+    uint32_t rb_step, rb_roll, rb_collect, rb_croll_small, nt_state;
     int32_t agg, obs_rate, buf_size, use_latency, use_motor_dyn, max_steps, auto_reset, reset_dist;
     int32_t dstb_mode, level_mode, num_levels, gust_dur, noise, dr, phys, held_persistent, need_level;
     float time_step, mass, ixx, iyy, izz, ft0, ft1, K, A, B, hover_x, hover_action, ou_sigma;

@@ -1396,11 +1396,8 @@ enum { SEED_WORDS = 13 };
 // state as soon as it is final, the rest at the end); the fused rollout keeps it in registers.
 // HD (small-N kernel, reference-default shape with sensor noise): the draws after the first
 // sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
-// env wave joins the helpers' LDS barrier before its second sub-step.  ROW_SCRATCH: obs_row is
-// this lane's LDS row, which also stages the final sensor call's draws (pre_final); the fused
-// collect rollout writes its rows straight to global memory and draws them inline (same blocks).
-template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0,
-          bool ROW_SCRATCH = true>
+// env wave joins the helpers' LDS barrier before its second sub-step.
+template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0>
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
                                               float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
                                               const float* hd = nullptr) {
@@ -1414,7 +1411,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     const Keys K = make_keys(P.key0, P.key1);
     const Rng g{K, E.rng, gid, TAG_STEP};
     // reference-default shape: the final (full) sensor call's blocks are drawn up front (RowRng)
-    const bool pre_final = ROW_SCRATCH && !HD && NOISE && P.agg == 2 && P.obs_rate == 2;
+    const bool pre_final = !HD && NOISE && P.agg == 2 && P.obs_rate == 2;
     const uint32_t* hdw = reinterpret_cast<const uint32_t*>(hd);
     const uint32_t fbase = 8u + 8u * (uint32_t)P.agg;
     if (pre_final) {
@@ -1545,11 +1542,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         const RowRng<1> gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
         compute_observation<NOISE>(P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
     } else {
-        // without the staged draws: an opaque copy of the counter keeps the final call's Philox
-        // blocks from being hoisted into the sub-steps, where their results would stay live
-        uint32_t ctr = E.rng;
-        if (!ROW_SCRATCH) asm volatile("" : "+v"(ctr));
-        compute_observation<NOISE>(P, E, Rng{K, ctr, gid, TAG_STEP}, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>(P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
     }
     const bool term = compute_done(P, E);
     E.ep_step += 1;
@@ -2341,7 +2334,7 @@ __global__ void __launch_bounds__(256) physics_kernel(KParams P, float* __restri
     T.st(G_CORE3, f4(E.w[2], ib(E.ep_step), ib((int)E.rng), ib(fl)));
 }
 
-// The fused rollouts' auto-resets (rollout_kernel, collect_rollout_kernel): the block lists its
+// The fused rollout's auto-resets (rollout_kernel): the block lists its
 // finished envs, draws their reset tables block-parallel as step_kernel does, and each env is
 // then reset in place by its own lane (its state is in that lane's registers); the reset
 // observation goes to row (this lane's LDS row or its global obs row).  Begins and ends with a
@@ -2450,110 +2443,6 @@ __global__ void __launch_bounds__(STEP_BLOCK, ROLL_MIN_WAVES) rollout_kernel(KPa
         write_obs_rows(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs, P.N - base < EPB ? P.N - base : EPB,
                        EPB, OD, tid, B);
         __syncthreads();             // the write-out read s_obs before the next step's rows
-    }
-    if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
-}
-
-// K steps of the collect loop in one launch (cf2_collect_rollout): per
-// step the env-step of rollout_kernel (state in registers for all K steps) and then, on the
-// block's new observations, the actor-critic forward and sampling of collect_kernel, whose actions
-// the next step reads.  It replaces K iterations of IWPGAlgorithm.roll_out's env.step + ac.step
-// (algs/iwpg/iwpg.py:372-410, ActorCritic.step algs/core.py:371-395) and its outputs are
-// bit-identical to K cf2_collect_step launches (same device code for both halves).
-//   * LDS holds every packed fragment (layer 3 included, 60.8 KB), staged once per launch, plus the
-//     reset tables; 2 blocks per CU (2 x 75 KB), so one block's policy phase runs beside the other
-//     block's env phase on the CU;
-//   * there is no LDS row buffer: each lane writes its obs row straight into step k's slab (the
-//     final sensor call's draws are made inline instead of being staged in that row), and after a
-//     block barrier each wave reads its 64 rows back from there (L2) as MFMA operands;
-//   * the policy phase: per wave 4 row tiles of 16 rows, policy_standardize / policy_layers /
-//     policy_emit_eps of cf2sim_policy.h, the noise of row 64 wv + l drawn by lane l.
-// Envs run in slices that fit one residency round (launch_collect_rollout_t), as cf2_rollout.
-constexpr uint32_t CROLL_MIN_WAVES = 2;
-template <bool NOISE, bool DR, int PHYS, int SPEC>
-__global__ void __launch_bounds__(STEP_BLOCK, CROLL_MIN_WAVES) collect_rollout_kernel(KParams P0, StepIO io0,
-                                                                                     PolicyIO pio, uint32_t K) {
-    static_assert(NOISE, "the fused collect kernels are built for the 34-wide observation");
-    const KParams P = shape_view<SPEC>(P0);
-    constexpr int OD = 34;
-    constexpr uint32_t B = STEP_BLOCK, C = RESET_CHUNK;
-    using PK = Packed<OD, CF2_POLICY_BF16X3>;
-    static_assert(PK::TOTAL % 4 == 0, "float4 staging");
-    __shared__ __align__(16) float s_frag[PK::TOTAL];
-    __shared__ uint32_t s_list[B];
-    __shared__ uint32_t s_ctr[B];
-    __shared__ uint32_t s_rand[RESET_SLOTS * 4 * C];
-    __shared__ uint32_t s_cnt;
-    __shared__ double s_hjgrid[6 * HJ_PTS];
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * B, i = base + tid;
-    if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    {
-        const float4* src = reinterpret_cast<const float4*>(pio.w);
-        float4* dst = reinterpret_cast<float4*>(s_frag);
-        for (uint32_t q = tid; q < PK::TOTAL / 4; q += B) dst[q] = src[q];
-    }
-    const bool live = i < P.N;
-    Env E;
-    if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, P.need_level, /*with_hist=*/true);
-    const size_t n = P0.out_stride;              // rows per output slab (the whole population)
-    const uint32_t l = tid & 63u, wv = tid >> 6, r16 = l & 15u;
-    const int g = (int)(l >> 4);
-    const uint32_t nrows = P.N - base < B ? P.N - base : B;      // rows of this block (> 0)
-    for (uint32_t k = 0; k < K; ++k) {
-        if (tid == 0) s_cnt = 0;     // every reader of the previous step passed its last barrier
-        StepIO io = io0;
-        io.act = pio.act + (size_t)k * n * 4;
-        io.obs = io0.obs + (size_t)k * n * OD;
-        io.rew = io0.rew + (size_t)k * n;
-        io.done = io0.done + (size_t)k * n;
-        if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
-        if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
-        float* row = io.obs + (size_t)i * OD;
-        bool do_reset = false;
-        ResetSeed rs;
-        if (live)
-            do_reset = step_env_body<NOISE, DR, PHYS, false, false, false, 0, /*ROW_SCRATCH=*/false>(P, io, i, E, row, rs,
-                                                                                                  s_hjgrid);
-        rollout_resets<NOISE, DR, PHYS, B, C>(P, E, base, tid, i, do_reset, rs, &s_cnt, s_list, s_ctr, s_rand, row);
-        // (the last barrier of rollout_resets orders every row write of the block before the reads)
-        // ---- policy phase: lane l of wave wv, row tile c: row 64 wv + 16 c + (l & 15), inputs
-        // 8 g .. 8 g + 7 and 32 + g (as collect_kernel)
-        float ep[4];
-        policy_noise(pio.key0, pio.key1, pio.counter + k, pio.row_offset + base + 64u * wv + l, ep);
-        PolicyLane<OD, CF2_POLICY_BF16X3> CL;
-        policy_lane_init<OD, CF2_POLICY_BF16X3>(s_frag + PK::O_BIAS, g, CL);
-        float* act_out = pio.act + (size_t)(k + 1) * n * 4;
-        float* val_out = pio.val + (size_t)(k + 1) * n;
-        float* logp_out = pio.logp + (size_t)(k + 1) * n;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t wr = 16u * (uint32_t)c + r16, r = 64u * wv + wr;
-            ObsRegs<OD, CF2_POLICY_BF16X3, 1> Xc;
-            {
-                const float* src = io.obs + (size_t)(base + __builtin_elementwise_min(r, nrows - 1u)) * OD;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float2 v = *reinterpret_cast<const float2*>(src + 8 * g + 2 * q);
-                    Xc.x8[0][0][2 * q] = v.x;
-                    Xc.x8[0][0][2 * q + 1] = v.y;
-                }
-                Xc.x1[0][0] = src[__builtin_elementwise_min(32 + g, OD - 1)];
-            }
-            int off = 0;
-            asm volatile("" : "+v"(off));        // keep the fragment reads inside the loop (policy_kernel)
-            const float* sw = s_frag + off;
-            policy_standardize<OD, CF2_POLICY_BF16X3, 1>(sw + PK::O_BIAS, g, CL, Xc);
-            f4v o[1];
-            policy_layers<OD, CF2_POLICY_BF16X3, 0, 1>(sw, sw + PK::O_BIAS, sw + PK::O_L3, (int)l, Xc, o);
-            float e[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)          // row wr's noise from lane wr
-                e[q] = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(wr << 2), __float_as_int(ep[q])));
-            if (r < nrows)
-                policy_emit_eps<OD, CF2_POLICY_BF16X3, 0>(o[0], base + r, g, CL, e, 1, act_out, val_out, logp_out,
-                                                          nullptr);
-        }
-        __syncthreads();             // step k + 1's actions (written by other lanes) are visible
     }
     if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
 }
@@ -3055,7 +2944,7 @@ __global__ void hj_kernel(HjGrid G, double3 umax, const float* __restrict__ V, c
 // and the slice size of the fused rollout.
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 static hipError_t occupancy_t(KParams& P) {
-    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0, per_croll = 0, per_croll_small = 0;
+    int dev = 0, cus = 0, per_step = 0, per_roll = 0, per_collect = 0, per_croll_small = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
@@ -3068,17 +2957,12 @@ static hipError_t occupancy_t(KParams& P) {
                                                              STEP_BLOCK, 0);
     if constexpr (NOISE && SPEC == 1 && PHYS == PHYS_BULLET_T)
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_croll, collect_rollout_kernel<NOISE, DR, PHYS, SPEC>,
-                                                             STEP_BLOCK, 0);
-    if constexpr (NOISE && SPEC == 1 && PHYS == PHYS_BULLET_T)
-        if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
                 &per_croll_small, collect_rollout_kernel_small<NOISE, DR, PHYS, SPEC>, CROLL_SMALL_BLOCK, 0);
     if (e != hipSuccess) return e;
     P.rb_step = (uint32_t)(cus * (per_step > 0 ? per_step : 1));
     P.rb_roll = (uint32_t)(cus * (per_roll > 0 ? per_roll : 1));
     P.rb_collect = (uint32_t)(cus * (per_collect > 0 ? per_collect : 1));
-    P.rb_croll = (uint32_t)(cus * (per_croll > 0 ? per_croll : 1));
     P.rb_croll_small = (uint32_t)(cus * (per_croll_small > 0 ? per_croll_small : 1));
     return hipSuccess;
 }
@@ -3173,14 +3057,35 @@ static hipError_t launch_collect_rollout_t(const KParams& P, const StepIO& io, c
         return hipErrorNotSupported;
     } else {
         constexpr uint32_t OD = 34;
-        // slices of one residency round each (as launch_rollout_t): a slice's blocks run all K steps
-        // together.  Every output slab keeps the whole population's stride.  Small N: 128-env blocks
-        // of two helper-wave groups (collect_rollout_kernel_small), one per CU.
-        const bool small = P.N <= SMALL_N_MAX;
-        const uint32_t epb = small ? 128u : STEP_BLOCK;
+        if (P.N > SMALL_N_MAX) {
+            // large N: one collect_kernel launch per env-step.  A one-launch version (rollout_kernel's
+            // env-step with the state in registers + this policy phase, 2 blocks per CU) was
+            // bit-identical but slower at 262 144 envs, 65.0 against 60.3 us per env-step
+            // (tools/variants/collect_rollout_large.hip.txt, profiles/r04_collect_ab.txt)
+            for (uint32_t k = 0; k < K; ++k) {
+                StepIO iok = io;
+                iok.act = pio.act + (size_t)k * P.N * 4;
+                iok.obs = io.obs + (size_t)k * P.N * OD;
+                iok.rew = io.rew + (size_t)k * P.N;
+                iok.done = io.done + (size_t)k * P.N;
+                if (io.trunc) iok.trunc = io.trunc + (size_t)k * P.N;
+                if (io.final_obs) iok.final_obs = io.final_obs + (size_t)k * P.N * OD;
+                PolicyIO pk = pio;
+                pk.counter = pio.counter + k;
+                pk.act = pio.act + (size_t)(k + 1) * P.N * 4;
+                pk.val = pio.val + (size_t)(k + 1) * P.N;
+                pk.logp = pio.logp + (size_t)(k + 1) * P.N;
+                const hipError_t e = launch_collect_t<NOISE, DR, PHYS, SPEC>(P, iok, pk, s);
+                if (e != hipSuccess) return e;
+            }
+            return hipSuccess;
+        }
+        // small N: 128-env blocks of two helper-wave groups (collect_rollout_kernel_small), one per
+        // CU, in slices of one residency round each (as launch_rollout_t): a slice's blocks run all
+        // K steps together.  Every output slab keeps the whole population's stride.
+        constexpr uint32_t epb = 128u;
         const uint32_t blocks = (P.N + epb - 1) / epb;
-        const uint32_t round_blocks = small ? (P.rb_croll_small > 0 ? P.rb_croll_small : 1u)
-                                            : (P.rb_croll > 0 ? P.rb_croll : 1u);
+        const uint32_t round_blocks = P.rb_croll_small > 0 ? P.rb_croll_small : 1u;
         const uint32_t nslices = (blocks + round_blocks - 1) / round_blocks;
         const uint32_t per = (blocks + nslices - 1) / nslices;
         for (uint32_t b0 = 0; b0 < blocks; b0 += per) {
@@ -3202,12 +3107,8 @@ static hipError_t launch_collect_rollout_t(const KParams& P, const StepIO& io, c
             ps.act = pio.act + (size_t)e0 * 4;
             ps.val = pio.val + e0;
             ps.logp = pio.logp + e0;
-            if (small)
-                hipLaunchKernelGGL((collect_rollout_kernel_small<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(CROLL_SMALL_BLOCK),
-                                   0, s, Ps, ios, ps, K);
-            else
-                hipLaunchKernelGGL((collect_rollout_kernel<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(STEP_BLOCK), 0, s, Ps,
-                                   ios, ps, K);
+            hipLaunchKernelGGL((collect_rollout_kernel_small<NOISE, DR, PHYS, SPEC>), dim3(nb), dim3(CROLL_SMALL_BLOCK), 0,
+                               s, Ps, ios, ps, K);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -306,10 +306,11 @@ int  cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float*
                       int precision, uint64_t seed, uint32_t counter, uint32_t row_offset, float* act_out_dev,
                       float* val_out_dev, float* logp_out_dev, void* stream);
 
-/* K steps of the collect loop in one launch: env-step k (actions act_dev + k*N*4) and then the
- * policy forward + sampling on its observations (noise counter counter + k), whose actions the
- * next env-step takes; the env state stays in registers for the K steps (N <= 32768, the 8-GPU
- * node shard: 64-env groups with helper waves computing the auto-resets, as cf2_step there).  Buffers, slab-major:
+/* K steps of the collect loop: env-step k (actions act_dev + k*N*4) and then the policy forward +
+ * sampling on its observations (noise counter counter + k), whose actions the next env-step
+ * takes.  N <= 32768 (C2, the 8-GPU node shard): one launch, the env state in registers for the K
+ * steps (64-env groups with helper waves computing the auto-resets, as cf2_step there); larger N:
+ * one cf2_collect_step launch per step (faster there than a one-launch loop).  Buffers, slab-major:
  * act_dev [K+1,N,4] (slab 0 in: the first step's actions; slabs 1..K out), val_dev / logp_dev
  * [K+1,N] (slabs 1..K out, slab 0 untouched), obs_dev [K,N,obs_dim] (slab k = the observation
  * after env-step k), rew_dev / done_dev [K,N], trunc_dev / final_obs_dev [K,N] / [K,N,obs_dim]

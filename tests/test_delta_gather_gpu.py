@@ -137,3 +137,26 @@ def test_delta_exchange_two_gloo_ranks_on_one_gpu(gpu, tmp_path):
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 240), nprocs=2, join=True)
     _check(out, 240)
+
+
+def test_unpack_rejects_operands_the_kernel_would_overrun(gpu):
+    """Host-side checks before the launch: a uint8 age vector (half the bytes the kernel indexes),
+    a short slab or a short packed buffer raise ValueError instead of faulting on the device."""
+    from cf2sim.dist import pack_obs, packed_words, unpack_obs
+    n, ol, cap = 256, 13, 16
+    od = 2 * (ol + 4)
+    prev = torch.zeros(n, od, device=gpu)
+    cur = torch.empty_like(prev)
+    a = torch.zeros(n, 4, device=gpu)
+    pk = pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap)
+    good_age = torch.zeros(n, dtype=torch.int16, device=gpu)
+    unpack_obs(pk, 1, n, ol, cap, a, a, good_age, prev, cur)
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError):
+        unpack_obs(pk, 1, n, ol, cap, a, a, torch.zeros(n, dtype=torch.uint8, device=gpu), prev, cur)
+    with pytest.raises(ValueError):
+        unpack_obs(pk, 1, n, ol, cap, a, a, good_age, prev, cur[: n // 2])
+    with pytest.raises(ValueError):
+        unpack_obs(pk[: packed_words(n, ol, cap) // 2], 1, n, ol, cap, a, a, good_age, prev, cur)
+    with pytest.raises(ValueError):
+        pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap, out=torch.zeros(8, dtype=torch.int32, device=gpu))

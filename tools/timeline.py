@@ -99,6 +99,15 @@ def analyze(t: np.ndarray, small: bool) -> dict:
             for a, b in v:
                 occ += (grid >= a) & (grid < b)
         occ /= len(simds)
+        if small:
+            # how the env waves (the ones that stamped 'loads landed') share SIMDs with each other
+            env_ran = (stamp(t, 1) != 0)[ran]
+            per_env = defaultdict(int)
+            for w in range(int(ran.sum())):
+                if env_ran[w]:
+                    per_env[int(key[w])] += 1
+            counts = np.bincount(np.array(list(per_env.values()), dtype=np.int64))
+            res["env_waves_per_simd_hist"] = {int(c): int(n) for c, n in enumerate(counts) if n}
         res["simds_used"] = len(simds)
         res["waves_per_simd"] = [int(per.min()), float(per.mean()), int(per.max())]
         res["residency_20_buckets"] = [float(x) for x in occ.reshape(20, 10).mean(1)]
@@ -118,6 +127,9 @@ def report(res: dict) -> str:
     if "simds_used" in res:
         lo, mean, hi = res["waves_per_simd"]
         lines.append(f"  SIMDs used {res['simds_used']}; waves per SIMD min {lo} mean {mean:.2f} max {hi}")
+        if "env_waves_per_simd_hist" in res:
+            lines.append("  SIMDs holding k env waves (k: count): " +
+                         " ".join(f"{k}: {v}" for k, v in res["env_waves_per_simd_hist"].items()))
         lines.append("  mean resident waves/SIMD over time (20 buckets): " +
                      " ".join(f"{x:.2f}" for x in res["residency_20_buckets"]))
     return "\n".join(lines)
