@@ -557,7 +557,9 @@ def main(argv=None):
         one = mode is True
         cb = step_b - state_b + state_b / T if one else step_b
         wk = f"{args.env_id}:N={n}"
-        ck = "collect_rollout_kernel" if one and n > 32768 else "collect_kernel"
+        # the kernel the PMC entry describes: cf2_collect_rollout runs collect_rollout_kernel_small
+        # at N <= 32 768 and one collect_kernel launch per env-step above
+        ck = "collect_rollout_kernel_small" if one and n <= 32768 else "collect_kernel"
         cvf = load_valu_issue(wk, ck)
         collect_line = {"value": n / (cus * 1e-6), "unit": "env-steps/s", "us_per_env_step": cus,
                         "algorithmic_bytes_per_env_step": cb, "flops_per_env_step": POLICY_FLOPS_PER_ROW,

@@ -74,7 +74,8 @@ from cf2sim.build import _obj_key
 key = _obj_key("cf2sim_kernels.hip")
 # kernel names as the trace prints them (cf2::name<...>): exact, so that "rollout_kernel" does not
 # also match collect_rollout_kernel
-STEP, ROLL, COLL, CROLL = "cf2::step_kernel<", "cf2::rollout_kernel<", "cf2::collect_kernel<", "cf2::collect_rollout_kernel<"
+STEP, ROLL, COLL = "cf2::step_kernel<", "cf2::rollout_kernel<", "cf2::collect_kernel<"
+POL = "cf2::policy_kernel<34, 1, 0>"          # the standalone policy forward (bf16x3, sampling)
 
 
 def collect_entry(kern, label, steps_per_dispatch):
@@ -86,12 +87,11 @@ def collect_entry(kern, label, steps_per_dispatch):
 
 step = per_dispatch(STEP)[-30:]
 roll = per_dispatch(ROLL)
-K = int(os.environ.get("CF2_COLLECT_K", "32"))       # tools/collect_bench.py --slabs
 res = {"workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}", "kernel_key": key,
        "step_kernel": summarize(step, "step_kernel", 1, durations(STEP)[-30:]),
        "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations(ROLL)),
        "collect_kernel": collect_entry(COLL, "collect_kernel (env-step + policy)", 1),
-       "collect_rollout_kernel": collect_entry(CROLL, f"collect_rollout_kernel (K={K} env-steps + policy)", K),
+       "policy_kernel": collect_entry(POL, "policy_kernel (actor-critic forward + sampling, 34-wide obs, bf16x3)", 1),
        "note": __doc__.split("\n\n")[1]}
 prof = os.path.join(ROOT, "profiles", "valu_issue.json")
 try:
