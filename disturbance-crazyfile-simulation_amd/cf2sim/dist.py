@@ -73,10 +73,17 @@ def run_ranks(plan, timeout: float | None = None) -> int:
 # cf2_obs_unpack run it on GPU tensors, the torch-op versions below on CPU tensors for the gloo
 # rehearsal of the multi-rank path; both produce the same rows bit for bit) ----
 
+PACK_BLOCK = 256      # envs per pack block: one block-table word each (the block's first side slot)
+
+
+def _side(n: int, ol: int) -> int:
+    """Word offset of the side entries: header, o_k rows, bitmap, block table."""
+    return 4 + n * ol + (n + 31) // 32 + (n + PACK_BLOCK - 1) // PACK_BLOCK
+
+
 def packed_words(n: int, ol: int, cap: int) -> int:
     """32-bit words of one rank's packed buffer (cf2_obs_packed_words)."""
-    side = 4 + n * ol + (n + 31) // 32
-    return (side + cap * (ol + 5) + 3) & ~3
+    return (_side(n, ol) + cap * (ol + 5) + 3) & ~3
 
 
 def default_cap(n: int) -> int:
@@ -140,7 +147,13 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
     out[4 + n * ol:4 + n * ol + nb] = torch.from_numpy(bits.view(np.int32))
     idx = torch.nonzero(r).flatten()
     out[0], out[1], out[2], out[3] = int(idx.numel()), n, ol, cap
-    side = 4 + n * ol + nb
+    # block table: the first side slot of each pack block's resets (blocks in env order here; the
+    # GPU kernel hands slots out per block in any order, so only the slots differ, not the rows)
+    nblk = (n + PACK_BLOCK - 1) // PACK_BLOCK
+    per_blk = torch.zeros(nblk, dtype=torch.int64)
+    per_blk.index_add_(0, idx // PACK_BLOCK, torch.ones_like(idx))
+    out[4 + n * ol + nb:4 + n * ol + nb + nblk] = (torch.cumsum(per_blk, 0) - per_blk).to(torch.int32)
+    side = _side(n, ol)
     for s, i in enumerate(idx[:cap].tolist()):
         e = side + s * (ol + 5)
         out[e] = i
@@ -204,7 +217,7 @@ def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, 
             if overflow is not None:
                 overflow += 1
         else:
-            side = 4 + n * ol + (n + 31) // 32
+            side = _side(n, ol)
             for s in range(cnt):
                 e = side + s * (ol + 5)
                 i = int(pk[e])

@@ -131,7 +131,7 @@ def test_packed_layout_and_bytes():
     assert w % 4 == 0
     full = n * 34 * 4
     assert full / (4 * w) >= 2.3, full / (4 * w)        # >= 2.3x fewer bytes than the full rows
-    assert packed_words(5, 17, 3) == ((4 + 5 * 17 + 1 + 3 * 22 + 3) & ~3)
+    assert packed_words(5, 17, 3) == ((4 + 5 * 17 + 1 + 1 + 3 * 22 + 3) & ~3)     # + one block-table word
 
 
 def test_pack_unpack_single_process_roundtrip():
@@ -165,3 +165,12 @@ def test_pack_unpack_single_process_roundtrip():
     assert torch.equal(out, exp)
     assert age2[[3, 17, 40]].tolist() == [0, 0, 0]
     assert age2[0].item() == 1 and age2[2].item() == 3 and age2[4].item() == 1
+
+
+def test_packed_words_match_the_c_abi():
+    """The torch-op layout and the kernels' layout (cf2_obs_packed_words, a host function) agree."""
+    from cf2sim import _native
+    from cf2sim.dist import packed_words
+    lib = _native.load()
+    for n, ol, cap in ((32768, 13, 2458), (5, 17, 3), (1000, 13, 75), (333, 17, 40), (256, 13, 256), (257, 13, 1)):
+        assert lib.cf2_obs_packed_words(n, ol, cap) == packed_words(n, ol, cap), (n, ol, cap)
