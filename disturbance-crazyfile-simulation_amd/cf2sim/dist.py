@@ -475,6 +475,7 @@ class PipelinedObsGather:
             torch.cuda.current_stream(self.device).wait_stream(self.ustream)
         for j in range(self.depth):
             self.free[j] = None
+            self.recv_free[j] = None
 
 
 def shard_range(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:
