@@ -244,11 +244,6 @@ def parse_args(argv=None):
     ap.add_argument("--no-gather-obs", dest="gather_obs", action="store_false")
     ap.add_argument("--gather-mode", choices=("delta", "full"), default="delta",
                     help="delta: o_k + reset side slab, every rank rebuilds the rows (default); full: the rows")
-    ap.add_argument("--gather-graph", choices=("auto", "on", "off"), default="auto",
-                    help="with the RCCL gather: replay the timed env-steps + exchanges from hipGraphs of up to 40 "
-                         "steps (auto: whenever the gather runs over RCCL), so the eager path's per-step host work "
-                         "(Python, 60-110 us per step) is not what the timed region measures; the delta exchange "
-                         "then sizes its side slab by the fixed crash budget (no time-out look-ahead)")
     ap.add_argument("--weak-envs", type=int, default=262144,
                     help="N > 1: the weak_scaling key times this many envs per rank; 0 = skip")
     ap.add_argument("--weak-steps", type=int, default=1000)
@@ -382,13 +377,9 @@ def main(argv=None):
         raise SystemExit("bench.py: --graph is for the env-step alone (no --gather-obs)")
     if delta and (len(set(shards)) != 1 or not delta_supported(env.cfg) or args.envs_per_gpu):
         delta = False
-    gather_graph = (gather and len(set(shards)) == 1 and backend == "nccl" and args.gather_graph != "off")
-    gather_graph_note = None
     if gather:
         if len(set(shards)) == 1:
-            # graph replay: a fixed side capacity (the look-ahead reads counts on the host per step)
-            pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta,
-                                      max_steps=0 if gather_graph else int(env.cfg.max_episode_steps))
+            pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps))
             if delta:
                 pipe.start(env.obs)
                 gather_mode = (f"pipelined delta all_gather_into_tensor (o_k + reset bitmap + side slab of "
@@ -460,19 +451,6 @@ def main(argv=None):
     graph = None
     if args.graph:
         graph = [capture(args.steps)]
-    elif gather_graph:
-        # units of 40 env-steps (a multiple of the action ring and of the double buffers, so every
-        # replay meets the buffers as the capture left them) plus the remainder: exactly K steps
-        try:
-            U = args.steps if args.steps <= 64 else 40
-            units = [U] * (args.steps // U) + ([args.steps % U] if args.steps % U else [])
-            graphs = {u: capture(u) for u in dict.fromkeys(units)}
-            graph = [graphs[u] for u in units]
-            gather_graph_note = f"timed steps replayed from hipGraphs ({len(units)} replays of {sorted(graphs)} steps)"
-        except Exception as ex:           # capture refused: the eager path, said so in the line
-            graph = None
-            torch.cuda.synchronize()
-            gather_graph_note = f"hipGraph capture failed, eager per-step launches: {type(ex).__name__}: {ex}"[:300]
 
     # ---- timed region: exactly K steps between barrier + synchronize, max over ranks ----
     elapsed, ev_ms = run(args.steps, gather, graph)
@@ -736,7 +714,7 @@ def main(argv=None):
                        "overflows": pipe.overflows() if pipe is not None else 0,
                        "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
                        "rx_frac_of_xgmi": rx / (elapsed / args.steps) / 1e9 / XGMI_PEAK_GBS,
-                       "launch": gather_graph_note or "eager per-step launches"}
+                       "launch": "eager per-step launches"}
 
     if rank == 0:
         cpu = None

@@ -67,8 +67,6 @@ def test_bench_rccl_gather_path_one_rank(gpu):
     d = _line(p.stdout)
     assert d["backend"] == "nccl" and d["world_size"] == 1 and d["config"]["gather_obs"] is True
     assert d["gather"]["mode"].startswith("pipelined delta") and d["value"] > 0 and d["gather"]["overflows"] == 0
-    # the timed steps are replayed from hipGraphs (the RCCL all-gather captured with the kernels)
-    assert "hipGraphs" in d["gather"]["launch"], d["gather"]["launch"]
 
 
 def _pipe_worker(rank, world, port, out):
