@@ -389,21 +389,29 @@ def main(argv=None):
         else:
             gather_mode = "ragged shards: synchronous padded all_gather"
     kk = [0]                               # env-steps taken (the delta exchange needs a_{k-1})
+    # per-step host work kept small (at the node shard an env-step is ~10 us of GPU time): the
+    # action ring's addresses and views resolved once
+    act_p = [acts[r].data_ptr() for r in range(ring)]
+    act_g = [acts_g[r] for r in range(ring)]
+    pipe_p = None
+    if pipe is not None:
+        pipe_p = ([b.data_ptr() for b in pipe.obs], [b.data_ptr() for b in pipe.done] if delta else None)
 
     def one_step(k, with_gather):
         j = kk[0]
         kk[0] += 1
-        a = acts[j % ring]
+        r = j % ring
         if with_gather and pipe is not None:
-            buf = pipe.buffer()
+            b = pipe.k % pipe.depth
+            pipe.buffer()                  # waits (on the device) until the exchange that read it is done
             if delta:
-                env.step_raw(a.data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=pipe.done_buffer().data_ptr())
-                pipe.publish(acts_g[j % ring], acts_g[(j - 1) % ring])
+                env.step_raw(act_p[r], obs_ptr=pipe_p[0][b], done_ptr=pipe_p[1][b])
+                pipe.publish(act_g[r], act_g[(j - 1) % ring])
             else:
-                env.step_raw(a.data_ptr(), obs_ptr=buf.data_ptr())
+                env.step_raw(act_p[r], obs_ptr=pipe_p[0][b])
                 pipe.publish()
         else:
-            env.step_raw(a.data_ptr())
+            env.step_raw(act_p[r])
             if with_gather:
                 env.gather_observations()
 

@@ -300,6 +300,27 @@ class PipelinedObsGather:
             self.pred_ev = [None] * (self.L + 1)
         else:
             self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
+        # the RCCL delta path's per-step host work is kept small (the eager step is host-bound at
+        # the node shard otherwise): buffers checked once here, raw pointers, reused events, views
+        # cached per side capacity
+        self._fast = self.delta and self.comm is not None
+        if self._fast:
+            from . import _native
+            self._lib = _native.load()
+            E = torch.cuda.Event
+            self._ev_fork = [E() for _ in range(self.depth)]
+            self._ev_free = [E() for _ in range(self.depth)]
+            self._ev_gath = [E() for _ in range(self.depth)]
+            self._ev_unp = [E() for _ in range(self.depth)]
+            self._views = {}
+            self._comm_h = self.comm.cuda_stream
+            self._u_h = self.ustream.cuda_stream
+            self._p_send = [t.data_ptr() for t in self.send]
+            self._p_recv = [t.data_ptr() for t in self.recv]
+            self._p_obs = [t.data_ptr() for t in self.obs]
+            self._p_done = [t.data_ptr() for t in self.done]
+            self._p_slab = [t.data_ptr() for t in self.slab]
+            self._p_pred = [self.pred[r].data_ptr() for r in range(self.L + 1)]
 
     @property
     def bytes_per_rank_per_step(self) -> int:
@@ -405,6 +426,8 @@ class PipelinedObsGather:
             raise RuntimeError("delta exchange: call start(reset observations) first")
         if act is None or act_prev is None:
             raise ValueError("delta exchange: publish needs the actions of this step and of the previous one")
+        if self._fast:
+            return self._publish_fast(act, act_prev)
         k = self.k
         cap = self.step_cap(k)
         words = packed_words(self.n, self.ol, cap)
@@ -454,6 +477,66 @@ class PipelinedObsGather:
         self.steps_sent += 1
         self.k += 1
         return out
+
+    def _publish_fast(self, act, act_prev):
+        """publish() of the RCCL delta path: the same operations on the same streams as the general
+        path (pack on the exchange stream, the all-gather there, the rebuild on its own stream),
+        with pre-checked buffers, raw pointers and reused events."""
+        import torch
+        import torch.distributed as dist
+        k, j, D = self.k, self.k % self.depth, self.depth
+        N = self.world * self.n
+        if act.numel() < N * 4 or act_prev.numel() < N * 4 or not (act.is_cuda and act_prev.is_cuda):
+            raise ValueError("delta exchange: act / act_prev must be [world * n, 4] on the GPU")
+        cap = self.step_cap(k)
+        key = (j, cap)
+        v = self._views.get(key)
+        if v is None:
+            words = packed_words(self.n, self.ol, cap)
+            v = self._views[key] = (words, self.send[j][:words], self.recv[j][:self.world * words])
+        words, send, recv = v
+        lib, comm = self._lib, self.comm
+        ef = self._ev_fork[j]
+        ef.record(torch.cuda.current_stream(self.device))
+        comm.wait_event(ef)
+        if self.recv_free[j] is not None:      # the rebuild of step k - depth read recv[j]
+            comm.wait_event(self.recv_free[j])
+        st = lib.cf2_obs_pack(self._p_obs[j], self._p_done[j], self.n, self.ol, cap, self._p_send[j],
+                              self._p_send[(j + 1) % D], self._comm_h)
+        if st != 0:
+            from . import _native
+            _native.check(st, "cf2_obs_pack")
+        self._ev_free[j].record(comm)
+        self.free[j] = self._ev_free[j]
+        with torch.cuda.stream(comm):
+            dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True).wait()
+        eg = self._ev_gath[j]
+        eg.record(comm)
+        self.ustream.wait_event(eg)
+        watch = self.watch
+        ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
+        w = watch != NO_WATCH
+        st = lib.cf2_obs_unpack(self._p_recv[j], self.world, self.n, self.ol, cap, act.data_ptr(), act_prev.data_ptr(),
+                                self.age.data_ptr(), self._p_slab[(k + 1) % 2], self._p_slab[k % 2],
+                                self.overflow.data_ptr(), int(watch) & 0xFFFFFFFF, self._p_pred[ps] if w else None,
+                                self._p_pred[pn] if w else None, self._u_h)
+        if st != 0:
+            from . import _native
+            _native.check(st, "cf2_obs_unpack")
+        if w:
+            with torch.cuda.stream(self.ustream):
+                self.pred_host[ps].copy_(self.pred[ps], non_blocking=True)
+                pe = torch.cuda.Event()
+                pe.record(self.ustream)
+                self.pred_ev[ps] = pe
+        eu = self._ev_unp[j]
+        eu.record(self.ustream)
+        self._ready = eu
+        self.recv_free[j] = eu
+        self.bytes_sent += 4 * words
+        self.steps_sent += 1
+        self.k += 1
+        return self.slab[k % 2]
 
     def ready(self):
         """Make the current stream wait for the latest published slab."""

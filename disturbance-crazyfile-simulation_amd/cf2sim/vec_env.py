@@ -127,6 +127,7 @@ class BatchedCrazyflieEnv:
         self.trunc = torch.zeros(n, dtype=torch.uint8, device=d)
         self.cost = torch.zeros(n, dtype=torch.float32, device=d)
         self.level = torch.zeros(n, dtype=torch.float32, device=d)
+        self._raw_ptrs = None                # step_raw's cached output addresses
         self.want_final_obs = want_final_obs
         self.last_collect_fused = False      # set by rollout.collect: its env-steps ran as cf2_collect_step
         self.final_obs = torch.zeros(n, self.obs_dim, dtype=torch.float32, device=d) if want_final_obs else None
@@ -399,10 +400,15 @@ class BatchedCrazyflieEnv:
         flags go to that buffer instead of self.done (the delta obs exchange packs them later)."""
         self._obs_latest = self.obs if obs_ptr is None else None
         self._state_version += 1
-        _native.check(self.lib.cf2_step(
-            self._ctx, act_ptr, None, obs_ptr or self.obs.data_ptr(), self.rew.data_ptr(), done_ptr or self.done.data_ptr(),
-            self.trunc.data_ptr() if full_info else None, self.cost.data_ptr() if full_info else None,
-            self.level.data_ptr() if full_info else None, None, self.stream), "cf2_step")
+        p = self._raw_ptrs
+        if p is None:          # the output buffers are allocated once: their addresses are cached
+            p = self._raw_ptrs = (self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(), self.trunc.data_ptr(),
+                                  self.cost.data_ptr(), self.level.data_ptr())
+        st = self.lib.cf2_step(self._ctx, act_ptr, None, obs_ptr or p[0], p[1], done_ptr or p[2],
+                               p[3] if full_info else None, p[4] if full_info else None, p[5] if full_info else None,
+                               None, torch.cuda.current_stream(self.device).cuda_stream)
+        if st != 0:
+            _native.check(st, "cf2_step")
 
     # ---- state snapshot ----
     def get_state(self):
