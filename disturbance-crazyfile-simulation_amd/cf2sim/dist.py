@@ -271,10 +271,9 @@ class PipelinedObsGather:
         cuda = self.device.type == "cuda"
         self.obs = [torch.empty(n, obs_dim, device=device) for _ in range(self.depth)]
         self.comm = torch.cuda.Stream(device=self.device) if (self.nccl and cuda) else None
-        # delta: the unpack (every rank rebuilds all rows) runs on a stream of its own, so that the
-        # all-gather of step k + 1 overlaps the rebuild of step k
-        self.ustream = torch.cuda.Stream(device=self.device) if (self.comm is not None and delta) else None
-        self.recv_free = [None] * self.depth  # events: the unpack that read recv buffer j is done
+        # the rebuild runs on the exchange stream right after the all-gather: a third stream (the
+        # rebuild of step k beside the all-gather of step k + 1) cost more host time per step than
+        # it overlapped (the eager step is host-bound at the node shard: DESIGN.md section 6)
         self.free = [None] * self.depth      # events: the exchange of the step that used buffer j read it
         self.k = 0
         self.started = not self.delta
@@ -310,11 +309,9 @@ class PipelinedObsGather:
             E = torch.cuda.Event
             self._ev_fork = [E() for _ in range(self.depth)]
             self._ev_free = [E() for _ in range(self.depth)]
-            self._ev_gath = [E() for _ in range(self.depth)]
             self._ev_unp = [E() for _ in range(self.depth)]
             self._views = {}
             self._comm_h = self.comm.cuda_stream
-            self._u_h = self.ustream.cuda_stream
             self._p_send = [t.data_ptr() for t in self.send]
             self._p_recv = [t.data_ptr() for t in self.recv]
             self._p_obs = [t.data_ptr() for t in self.obs]
@@ -353,7 +350,7 @@ class PipelinedObsGather:
     def _gather(self, out, x):
         import torch.distributed as dist
         if self.nccl:
-            dist.all_gather_into_tensor(out, x, group=self.group, async_op=True).wait()
+            dist.all_gather_into_tensor(out, x, group=self.group)
         else:
             gather_rows(x.reshape(1, -1), self.group, sizes=[1] * self.world, out=out.view(self.world, -1))
 
@@ -368,9 +365,6 @@ class PipelinedObsGather:
     def start(self, obs):
         """delta: gather the observations of a reset of every env ([n, D]) in full; every env's
         step count since its reset is 0 on every rank."""
-        if self.ustream is not None:                 # a restart: no rebuild still in flight
-            self.comm.wait_stream(self.ustream)
-        self.recv_free = [None] * self.depth
 
         def run():
             self._gather(self.slab[1], obs.contiguous())
@@ -409,9 +403,7 @@ class PipelinedObsGather:
         if not self.delta:
             def run():
                 if self.nccl:
-                    w = torch.distributed.all_gather_into_tensor(self.out[j], self.obs[j], group=self.group,
-                                                                 async_op=True)
-                    w.wait()
+                    torch.distributed.all_gather_into_tensor(self.out[j], self.obs[j], group=self.group)
                 else:
                     gather_rows(self.obs[j], self.group, sizes=[self.n] * self.world, out=self.out[j])
                 if self.comm is not None:
@@ -450,7 +442,6 @@ class PipelinedObsGather:
                 ev2 = torch.cuda.Event()
                 ev2.record(torch.cuda.current_stream(self.device))
                 self._ready = ev2
-                self.recv_free[j] = ev2
 
         def run():
             pack_obs(self.obs[j], self.done[j], cap, out=send, clear_next=self.send[(j + 1) % self.depth][:1])
@@ -458,19 +449,12 @@ class PipelinedObsGather:
                 ev = torch.cuda.Event()
                 ev.record(self.comm)
                 self.free[j] = ev
-                if self.recv_free[j] is not None:  # the unpack of step k - depth read recv[j]
-                    self.comm.wait_event(self.recv_free[j])
             if recv.is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
                 host = gather_rows(send.cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
                 recv.copy_(host.reshape(-1))
             else:
                 self._gather(recv, send)
-            if self.ustream is None:
-                unpack()
-            else:                                   # after the gather, beside the next step's gather
-                self.ustream.wait_stream(self.comm)
-                with torch.cuda.stream(self.ustream):
-                    unpack()
+            unpack()
             return cur
         out = self._run_on_comm(run)
         self.bytes_sent += 4 * words
@@ -479,9 +463,9 @@ class PipelinedObsGather:
         return out
 
     def _publish_fast(self, act, act_prev):
-        """publish() of the RCCL delta path: the same operations on the same streams as the general
-        path (pack on the exchange stream, the all-gather there, the rebuild on its own stream),
-        with pre-checked buffers, raw pointers and reused events."""
+        """publish() of the RCCL delta path: the general path's operations (pack, all-gather,
+        rebuild, all on the exchange stream) with pre-checked buffers, raw pointers and reused
+        events."""
         import torch
         import torch.distributed as dist
         k, j, D = self.k, self.k % self.depth, self.depth
@@ -499,8 +483,6 @@ class PipelinedObsGather:
         ef = self._ev_fork[j]
         ef.record(torch.cuda.current_stream(self.device))
         comm.wait_event(ef)
-        if self.recv_free[j] is not None:      # the rebuild of step k - depth read recv[j]
-            comm.wait_event(self.recv_free[j])
         st = lib.cf2_obs_pack(self._p_obs[j], self._p_done[j], self.n, self.ol, cap, self._p_send[j],
                               self._p_send[(j + 1) % D], self._comm_h)
         if st != 0:
@@ -508,31 +490,27 @@ class PipelinedObsGather:
             _native.check(st, "cf2_obs_pack")
         self._ev_free[j].record(comm)
         self.free[j] = self._ev_free[j]
-        with torch.cuda.stream(comm):
-            dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True).wait()
-        eg = self._ev_gath[j]
-        eg.record(comm)
-        self.ustream.wait_event(eg)
+        with torch.cuda.stream(comm):          # the synchronous call: 19 us of host time, async + wait 42 us
+            dist.all_gather_into_tensor(recv, send, group=self.group)
         watch = self.watch
         ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
         w = watch != NO_WATCH
         st = lib.cf2_obs_unpack(self._p_recv[j], self.world, self.n, self.ol, cap, act.data_ptr(), act_prev.data_ptr(),
                                 self.age.data_ptr(), self._p_slab[(k + 1) % 2], self._p_slab[k % 2],
                                 self.overflow.data_ptr(), int(watch) & 0xFFFFFFFF, self._p_pred[ps] if w else None,
-                                self._p_pred[pn] if w else None, self._u_h)
+                                self._p_pred[pn] if w else None, self._comm_h)
         if st != 0:
             from . import _native
             _native.check(st, "cf2_obs_unpack")
         if w:
-            with torch.cuda.stream(self.ustream):
+            with torch.cuda.stream(comm):
                 self.pred_host[ps].copy_(self.pred[ps], non_blocking=True)
                 pe = torch.cuda.Event()
-                pe.record(self.ustream)
+                pe.record(comm)
                 self.pred_ev[ps] = pe
         eu = self._ev_unp[j]
-        eu.record(self.ustream)
+        eu.record(comm)
         self._ready = eu
-        self.recv_free[j] = eu
         self.bytes_sent += 4 * words
         self.steps_sent += 1
         self.k += 1
@@ -554,11 +532,8 @@ class PipelinedObsGather:
         import torch
         if self.comm is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm)
-        if self.ustream is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.ustream)
         for j in range(self.depth):
             self.free[j] = None
-            self.recv_free[j] = None
 
 
 def shard_range(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:
