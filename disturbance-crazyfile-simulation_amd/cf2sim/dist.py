@@ -164,6 +164,7 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
 
 
 NO_WATCH = 0xFFFFFFFF
+PRED_BATCH = 4          # RCCL delta path: time-out counts copied to the host every 4 steps (< lookahead)
 
 
 def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, slab_prev, slab, overflow=None,
@@ -308,8 +309,9 @@ class PipelinedObsGather:
             self._lib = _native.load()
             E = torch.cuda.Event
             self._ev_fork = [E() for _ in range(self.depth)]
-            self._ev_free = [E() for _ in range(self.depth)]
             self._ev_unp = [E() for _ in range(self.depth)]
+            self._ev_pred = [E() for _ in range(self.L // PRED_BATCH + 3)]
+            self._pred_batch = []                # (step, event) of the count-ring copies in flight
             self._views = {}
             self._comm_h = self.comm.cuda_stream
             self._p_send = [t.data_ptr() for t in self.send]
@@ -375,6 +377,8 @@ class PipelinedObsGather:
         self._run_on_comm(run)
         self.pred_host.zero_()
         self.pred_ev = [None] * (self.L + 1)
+        if self._fast:
+            self._pred_batch = []
         self.started = True
         self.k = 0
         return self.slab[1]
@@ -386,6 +390,13 @@ class PipelinedObsGather:
             return self.n if 0 < self.max_steps else self.cap
         if k < self.L:                       # before the first prediction: every env is k + 1 old
             t = self.n if k + 1 == self.max_steps else 0
+        elif self._fast:
+            # the first batch copy issued at or after step k - L (issued after that step's rebuild;
+            # the slot is only cleared by the rebuild of step k, after this read)
+            s = (k - self.L) % (self.L + 1)
+            ev = next(e for (c, e) in self._pred_batch if c >= k - self.L)
+            ev.synchronize()
+            t = int(self.pred_host[s].max())
         else:
             s = (k - self.L) % (self.L + 1)
             ev = self.pred_ev[s]
@@ -488,8 +499,6 @@ class PipelinedObsGather:
         if st != 0:
             from . import _native
             _native.check(st, "cf2_obs_pack")
-        self._ev_free[j].record(comm)
-        self.free[j] = self._ev_free[j]
         with torch.cuda.stream(comm):          # the synchronous call: 19 us of host time, async + wait 42 us
             dist.all_gather_into_tensor(recv, send, group=self.group)
         watch = self.watch
@@ -502,15 +511,20 @@ class PipelinedObsGather:
         if st != 0:
             from . import _native
             _native.check(st, "cf2_obs_unpack")
-        if w:
+        if w and k % PRED_BATCH == 0:
+            # the whole count ring to the host every PRED_BATCH steps: step_cap(k') reads the count of
+            # step k' - L from the first batch copy at or after it (each is ~15 us of host work)
             with torch.cuda.stream(comm):
-                self.pred_host[ps].copy_(self.pred[ps], non_blocking=True)
-                pe = torch.cuda.Event()
+                self.pred_host.copy_(self.pred, non_blocking=True)
+                pe = self._ev_pred[(k // PRED_BATCH) % len(self._ev_pred)]
                 pe.record(comm)
-                self.pred_ev[ps] = pe
+            self._pred_batch.append((k, pe))
+            if len(self._pred_batch) > len(self._ev_pred) - 1:
+                self._pred_batch.pop(0)
         eu = self._ev_unp[j]
         eu.record(comm)
         self._ready = eu
+        self.free[j] = eu                      # the exchange that read obs / done buffer j ends here
         self.bytes_sent += 4 * words
         self.steps_sent += 1
         self.k += 1
