@@ -49,6 +49,8 @@ def test_small_kernel_rows_with_missing_stamps():
     for p in ph.values():
         assert 0 <= p["mean"] < 1e6 and p["max"] < 1e6
     assert res["simds_used"] == 5
+    # the two env waves sit on two different SIMDs
+    assert res["env_waves_per_simd_hist"] == {1: 2}
 
 
 def test_large_kernel_rows_and_out_of_order_stamps_are_counted():
