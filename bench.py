@@ -253,6 +253,8 @@ def parse_args(argv=None):
     ap.add_argument("--oc-steps", type=int, default=500)
     ap.add_argument("--action-ring", type=int, default=8,
                     help="action slabs cycled through in the timed region (8 x 4 MB at 262 144 envs)")
+    ap.add_argument("--two-streams", type=int, default=1,
+                    help="N = 1: also time the same envs as two half contexts on two HIP streams (two_streams key)")
     ap.add_argument("--streaming-ring", type=int, default=64,
                     help="after the timed region, 1000 env-steps with actions cycled through this many "
                          "slabs (64 x 4 MB: more than the 256 MB Infinity Cache); 0 = skip")
@@ -588,6 +590,48 @@ def main(argv=None):
                                     "time-out values"}
         cenv.close()
 
+    two_streams = None
+    if world == 1 and args.two_streams and n % 128 == 0:
+        # the same envs as two contexts of n / 2 consecutive global ids, each stepping on its own HIP
+        # stream with no per-step join: shard A's env-step k + 1 overlaps shard B's env-step k (the
+        # launch ramp and tail of one hide under the other).  Same trajectories (split invariance).
+        h = n // 2
+        tstreams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        halves = []
+        for s_i in range(2):
+            with torch.cuda.stream(tstreams[s_i]):
+                he = BatchedCrazyflieEnv(args.env_id, h, seed=args.seed, device=dev, env_id_offset=s_i * h, **env_kw)
+                bind_synthetic_tables(he, dev)
+                he.reset()
+                halves.append((he, [acts[r][s_i * h:(s_i + 1) * h].data_ptr() for r in range(ring)]))
+
+        def two_run(k0, count):
+            for k in range(k0, k0 + count):
+                for s_i, (he, ptrs) in enumerate(halves):
+                    with torch.cuda.stream(tstreams[s_i]):
+                        he.step_raw(ptrs[k % ring])
+        two_run(0, max(args.warmup, 200))
+        torch.cuda.synchronize()
+        t0_, t1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0_.record(stream)
+        for st_ in tstreams:
+            st_.wait_event(t0_)
+        two_run(0, args.steps)
+        for st_ in tstreams:
+            ev_ = torch.cuda.Event()
+            ev_.record(st_)
+            stream.wait_event(ev_)
+        t1_.record(stream)
+        torch.cuda.synchronize()
+        tus = t0_.elapsed_time(t1_) * 1e3 / args.steps
+        two_streams = {"value": n / (tus * 1e-6), "unit": "env-steps/s", "us_per_env_step": tus,
+                       "hbm_frac": bytes_per_env_step(env) * n / (tus * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                       "note": f"the same {n} envs as two contexts of {h} (consecutive global ids) on two HIP streams, "
+                               "no join per env-step (the headline keeps one context on one stream)"}
+        for he, _ in halves:
+            he.close()
+        del halves
+
     streaming = None
     if world == 1 and args.streaming_ring > 0:
         # the same env-step with the actions cycled through a ring larger than the Infinity Cache
@@ -767,6 +811,7 @@ def main(argv=None):
             "fused_rollout": fused,
             "collect": collect_line,
             "streaming_actions": streaming,
+            "two_streams": two_streams,
             "delta_exchange": exchange,
         }
         print(json.dumps(line), flush=True)
