@@ -447,6 +447,18 @@ __device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, u
 // fence needs no vmcnt wait -- but this form is explicit about what the hand-off relies on, and it
 // has no fence semantics the compiler could move memory operations around.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// A one-way hand-over between waves of a block without a block barrier: the producer's lane 0
+// sets an LDS flag after the wave's LDS writes; consumers poll it (bounded: a flag never set ends
+// the wait with stale data, which the parity tests would show, instead of a hung grid).
+__device__ __forceinline__ void lds_flag_set(uint32_t* f) {
+    __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_flag_wait(uint32_t* f) {
+    for (uint32_t it = 0; it < (1u << 22); ++it) {
+        if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
 
 // One wave's part of the small-N kernel's write-out of its 64 obs rows: the float4 chunks that touch
 // a row whose bit in mask is set (dirty: the reset observations the helper waves staged in rrow) or
@@ -2036,15 +2048,19 @@ struct SmallLds {
     // after its first sub-step (HD_* layout), handed over at an LDS barrier before sub-step 1
     static constexpr bool HD = SPEC == 1 && NOISE;
     // word offsets in a carved buffer (doubles 8-B aligned, rows 16-B aligned)
+    // (HD: wave 1 computes the reset pose once and hands it to waves 2-3: POSE_WORDS per env behind
+    // the flag word s_mask[2])
+    static constexpr uint32_t POSE_WORDS = HD ? 12 : 0;
     static constexpr uint32_t O_OBS = 0, O_RROW = 64 * OD, O_SEED = 128 * OD, O_C2 = O_SEED + SEED_SMALL * 64,
-                              O_DRAW = O_C2 + C2_WORDS * 64, O_MASK = O_DRAW + (HD ? HD_WORDS * 64 : 1),
-                              O_HJ = (O_MASK + 2 + 1) & ~1u, WORDS = O_HJ + 2 * 6 * HJ_PTS;
+                              O_DRAW = O_C2 + C2_WORDS * 64, O_POSE = O_DRAW + (HD ? HD_WORDS * 64 : 1),
+                              O_MASK = O_POSE + (HD ? POSE_WORDS * 64 : 1),
+                              O_HJ = (O_MASK + 3 + 1) & ~1u, WORDS = O_HJ + 2 * 6 * HJ_PTS;
 };
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& io, float* s_obs, float* s_seed,
                                                float* s_c2, float* s_rrow, uint32_t* s_mask, double* s_hjgrid,
-                                               float* s_draw) {
+                                               float* s_draw, float* s_pose) {
     const KParams P = shape_view<SPEC>(P0);
     using SL = SmallLds<NOISE, SPEC>;
     constexpr int OL = SL::OL;
@@ -2066,9 +2082,9 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     const bool live = i < P.N;
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     const Tile T(io.sf, P.N, i);
-    // the domain randomisation / disturbance / level draws of the reset: wave 1 in the
-    // reference-default shape (whose step draws waves 2 and 3 share), else wave 3
-    constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
+    // the domain randomisation / disturbance / level draws of the reset: wave 3 (in the
+    // reference-default shape wave 1 computes the reset pose for all three helpers meanwhile)
+    constexpr uint32_t PARAMS_WAVE = 3u;
     Env H;                         // waves 1-3: the speculative reset (kept across the barrier)
     float held1[10], ng1[9];       // wave 2: first reset sensor call
     HeldNoise hn;                  // waves 2 / 3: the noise of the first / second reset sensor call
@@ -2093,6 +2109,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
         // the env-step's draws after sub-step 0 (step tag, the env's counter), split over the
         // three helper waves; Box-Muller applied where the env-step turns words into normals
         if (live) helper_step_draws(K, ctr, gid, wave, s_draw + lane);
+        if (wave == 1 && lane == 0) s_mask[2] = 0u;     // the pose flag (set once the pose is in LDS)
         TSTAMP(10);      // helper: step draws in LDS
         lds_barrier();   // joined by the env wave before its second sub-step (step_env_body)
         TSTAMP(11);
@@ -2111,7 +2128,53 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
 #pragma unroll
             for (int k = 0; k < 4; ++k) s_seed[(6 + k) * 64 + lane] = rs.ou[k];
         }
-    } else if (P.auto_reset && live) {
+    } else if (HD && P.auto_reset && live) {
+        // the reset pose computed once, by wave 1 (its step draws are the fewest), and handed to
+        // waves 2-3 in LDS while they turn their sensor-call draws into noise (and wave 3 draws the
+        // reset's parameters)
+        __builtin_amdgcn_s_setprio(0);
+        float* row = s_rrow + lane * OD;
+        if (wave == 1) {
+            reset_kinematics<PHYS>(P, H, gr, gid);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { row[OL + k] = H.la[k]; row[2 * OL + 4 + k] = H.la[k]; }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s_pose[k * 64 + lane] = H.p[k];
+                s_pose[(3 + k) * 64 + lane] = H.v[k];
+                s_pose[(6 + k) * 64 + lane] = H.rpy[k];
+                s_pose[(9 + k) * 64 + lane] = H.wb[k];
+            }
+            if (lane == 0) lds_flag_set(s_mask + 2);
+        }
+        reset_prework();
+        if (wave >= 2) {
+            lds_flag_wait(s_mask + 2);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                H.p[k] = s_pose[k * 64 + lane];
+                H.v[k] = s_pose[(3 + k) * 64 + lane];
+                H.rpy[k] = s_pose[(6 + k) * 64 + lane];
+                H.wb[k] = s_pose[(9 + k) * 64 + lane];
+            }
+            if (wave == 2) {
+                held_combine(H, hn, held1);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) ng1[k] = ngs[k];
+#pragma unroll
+                for (int k = 0; k < 10; ++k) row[k] = held1[k];
+            } else {
+                float held2[10];
+                held_combine(H, hn, held2);
+#pragma unroll
+                for (int k = 0; k < 10; ++k) row[OL + 4 + k] = held2[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) s_c2[k * 64 + lane] = ngs[k];
+            }
+        }
+        TREADY("v"(H.p[0]), "v"(H.K[3]), "v"(H.la[3]));
+        TSTAMP(9);   // helper: speculative reset computed
+    } else if (!HD && P.auto_reset && live) {
         __builtin_amdgcn_s_setprio(0);
         reset_prework();
         if (wave == 1) {
@@ -2163,6 +2226,10 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
             // gyro-LPF triples of o_0 and o_1 complete the staged row
             Env& E = H;
             float* row = s_rrow + lane * OD;
+            if (HD) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) E.la[k] = row[OL + k];     // wave 1's, staged in the row
+            }
             if (NOISE) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) { E.lpf[k] = s_seed[k * 64 + lane]; E.bias[k] = s_seed[(3 + k) * 64 + lane]; }
@@ -2218,10 +2285,11 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     __shared__ float s_seed[SEED_SMALL * 64];              // [word][env]
     __shared__ float s_c2[C2_WORDS * 64];                  // [word][env]
     __shared__ __align__(16) float s_rrow[64 * SL::OD];    // speculative reset observation rows
-    __shared__ uint32_t s_mask[2];                         // finished envs (ballot of wave 0)
+    __shared__ uint32_t s_mask[3];                         // finished envs (ballot of wave 0), pose flag
     __shared__ double s_hjgrid[6 * HJ_PTS];
     __shared__ float s_draw[SL::HD ? HD_WORDS * 64 : 1];
-    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw);
+    __shared__ float s_pose[SL::HD ? SL::POSE_WORDS * 64 : 1];
+    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw, s_pose);
 }
 
 // The fused collect step at small N (N <= 32 768: the 8-GPU node shard, C2): step_kernel_small's
@@ -2244,7 +2312,7 @@ __global__ void __launch_bounds__(256, 2) collect_kernel_small(KParams P0, StepI
     const uint64_t mask = small_body<NOISE, DR, PHYS, SPEC>(
         P0, io, s_mem + SL::O_OBS, s_mem + SL::O_SEED, s_mem + SL::O_C2, s_mem + SL::O_RROW,
         reinterpret_cast<uint32_t*>(s_mem + SL::O_MASK), reinterpret_cast<double*>(s_mem + SL::O_HJ),
-        s_mem + SL::O_DRAW);
+        s_mem + SL::O_DRAW, s_mem + SL::O_POSE);
     // ---- policy phase: wave w takes rows 16 w .. 16 w + 15 of the block (lane l: row 16 w + (l & 15),
     // inputs 8 g .. 8 g + 7 and 32 + g), once wave 2 has completed the reset rows
     lds_barrier();

@@ -40,7 +40,7 @@ def test_small_kernel_rows_with_missing_stamps():
     ph = res["phases"]
     assert ph["env: physics"]["waves"] == 2 and ph["env: physics"]["mean"] == 7700
     assert ph["env: obs/history/stores"]["mean"] == 5300
-    assert ph["env: -> reset rows in LDS"]["mean"] == 2800
+    assert ph["env: obs row write-out"]["mean"] == 2800
     assert ph["helper: speculative reset"]["waves"] == 3 and ph["helper: speculative reset"]["mean"] == 3000
     assert ph["helper wave 2: gyro + rows + stores"]["waves"] == 1
     assert ph["helper wave 2: gyro + rows + stores"]["mean"] == 2400

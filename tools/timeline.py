@@ -11,10 +11,10 @@ Timing row per wave (16 x u64): 0 hw id (XCC << 32 | HW_ID), 1 realtime start, 2
     12 every reset chunk done, 5 end
   step_kernel_small (N <= 32 768, 64 envs per block: wave 0 steps, waves 1-3 help):
     env wave:    0 entry, 1 loads landed, 2 physics done, 3 epilogue issued, 4 barrier passed,
-                 12 reset rows in LDS, 5 end
+                 12 obs rows written, 5 end
     helper wave: 0 entry, 10 step draws in LDS, 11 draw barrier passed, 9 speculative reset done,
                  4 barrier passed, 6 / 8 (wave 2, finished envs only) reset row start / done,
-                 12 reset rows in LDS, 5 end
+                 12 obs rows written, 5 end
 A wave writes only the stamps of the code it runs; the others stay 0.  Every phase below is
 computed over the waves that wrote both of its stamps, so a stamp a kernel never writes yields no
 row (never a difference against 0).  s_memtime is per-XCD, so durations are only taken within
@@ -35,13 +35,13 @@ LARGE_PHASES = [("loads landed", 0, 1), ("physics", 1, 2), ("obs/history/stores"
                 ("block barrier wait", 3, 4), ("resets + obs copy", 4, 5), ("reset role: pose", 6, 7),
                 ("reset role 2: sensor call + history", 7, 8), ("wave lifetime", 0, 5)]
 SMALL_ENV_PHASES = [("env: loads landed", 0, 1), ("env: physics", 1, 2), ("env: obs/history/stores", 2, 3),
-                    ("env: -> barrier passed", 3, 4), ("env: -> reset rows in LDS", 4, 12),
-                    ("env: write-out", 12, 5), ("env: wave lifetime", 0, 5)]
+                    ("env: -> barrier passed", 3, 4), ("env: obs row write-out", 4, 12),
+                    ("env: -> end", 12, 5), ("env: wave lifetime", 0, 5)]
 SMALL_HELPER_PHASES = [("helper: entry -> step draws in LDS", 0, 10), ("helper: draw barrier wait", 10, 11),
                        ("helper: speculative reset", 11, 9), ("helper: wait at barrier", 9, 4),
                        ("helper wave 2: barrier -> reset row start", 4, 6),
-                       ("helper wave 2: gyro + rows + stores", 6, 8), ("helper: -> reset rows in LDS", 4, 12),
-                       ("helper: write-out", 12, 5), ("helper: wave lifetime", 0, 5)]
+                       ("helper wave 2: gyro + rows + stores", 6, 8), ("helper: reset rows + obs row write-out", 4, 12),
+                       ("helper: -> end", 12, 5), ("helper: wave lifetime", 0, 5)]
 
 
 def stamp(t: np.ndarray, k: int) -> np.ndarray:
