@@ -2541,7 +2541,7 @@ struct SmallRollLds {
     float* par;          // [RP_WORDS][64]
     float* ho;           // [RO_WORDS][64] (sensor noise only)
     float* draw;         // [HD_WORDS][64] (HD only)
-    uint32_t* mask;      // [2] the group's finished envs (ballot of its env wave)
+    uint32_t* mask;      // [3] the group's finished envs (ballot of its env wave), the pose flag
 };
 
 // The env wave's part of one step of the small-N fused rollouts: the env-step (barrier A_k inside
@@ -2637,19 +2637,34 @@ __device__ __forceinline__ void small_roll_helper_step(const KParams& P, const K
                                                        uint32_t wave, uint32_t lane, bool live, float& lvl,
                                                        int& lvl_idx, const SmallRollLds& L) {
     constexpr bool HD = SPEC == 1 && NOISE;
-    constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
+    constexpr uint32_t PARAMS_WAVE = 3u;
     if (HD) {
         if (live) helper_step_draws(Kh, ctr, gid, wave, L.draw + lane);
     }
+    if (NOISE && wave == 1 && lane == 0) L.mask[2] = 0u;     // the pose flag of step k
     lds_barrier();                               // A_k
     Env H;
     if (P.auto_reset && live) {
         const Rng gr{Kh, ctr, gid, TAG_RESET};
-        HeldNoise hn;
-        float ngs[9];
-        if (NOISE && wave >= 2) held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
-        reset_kinematics<PHYS, true>(P, H, gr, gid);
+        auto params = [&]() {
+            H.level = lvl;
+            H.level_idx = lvl_idx;
+            reset_params<DR, true>(P, H, gr);
+            float* par = L.par + lane;
+            par[RP_DT * 64] = H.dt; par[RP_M * 64] = H.m;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { par[(RP_J + c) * 64] = H.J[c]; par[(RP_DSTB + c) * 64] = H.dstb[c]; }
+            par[RP_K0 * 64] = H.k0; par[RP_K1 * 64] = H.k1;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) { par[(RP_B + c) * 64] = H.B[c]; par[(RP_K + c) * 64] = H.K[c]; }
+            par[RP_LEVEL * 64] = H.level;
+            par[RP_LEVEL_IDX * 64] = ib(H.level_idx);
+        };
+        // the reset pose once, by wave 1, into the kinematics record; with sensor noise waves 2-3
+        // read its position, velocity and attitude from there once wave 1 has set the flag (they
+        // draw their sensor-call noise, and wave 3 the reset's parameters, meanwhile)
         if (wave == 1) {
+            reset_kinematics<PHYS, true>(P, H, gr, gid);
             float* kin = L.kin + lane;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -2665,7 +2680,18 @@ __device__ __forceinline__ void small_roll_helper_step(const KParams& P, const K
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
                     if (r < P.buf_size) kin[(RK_ABUF + 4 * r + c) * 64] = H.abuf[r][c];
+            if (NOISE && lane == 0) lds_flag_set(L.mask + 2);
         } else if (NOISE) {
+            HeldNoise hn;
+            float ngs[9];
+            held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
+            if (wave == PARAMS_WAVE) params();
+            lds_flag_wait(L.mask + 2);
+            const float* kin = L.kin + lane;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                H.p[c] = kin[(RK_P + c) * 64]; H.v[c] = kin[(RK_V + c) * 64]; H.rpy[c] = kin[(RK_RPY + c) * 64];
+            }
             float held[10];
             held_combine(H, hn, held);
             float* ho = L.ho + lane;
@@ -2675,20 +2701,7 @@ __device__ __forceinline__ void small_roll_helper_step(const KParams& P, const K
 #pragma unroll
             for (int c = 0; c < 9; ++c) ho[(nb + c) * 64] = ngs[c];
         }
-        if (wave == PARAMS_WAVE) {
-            H.level = lvl;
-            H.level_idx = lvl_idx;
-            reset_params<DR, true>(P, H, gr);
-            float* par = L.par + lane;
-            par[RP_DT * 64] = H.dt; par[RP_M * 64] = H.m;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) { par[(RP_J + c) * 64] = H.J[c]; par[(RP_DSTB + c) * 64] = H.dstb[c]; }
-            par[RP_K0 * 64] = H.k0; par[RP_K1 * 64] = H.k1;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) { par[(RP_B + c) * 64] = H.B[c]; par[(RP_K + c) * 64] = H.K[c]; }
-            par[RP_LEVEL * 64] = H.level;
-            par[RP_LEVEL_IDX * 64] = ib(H.level_idx);
-        }
+        if (!NOISE && wave == PARAMS_WAVE) params();
     }
     lds_barrier();                               // B_k
     if (P.auto_reset && live && wave == PARAMS_WAVE) {
@@ -2703,13 +2716,13 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
     constexpr int OL = NOISE ? 13 : 17;
     constexpr int OD = 2 * (OL + 4);
     constexpr bool HD = SPEC == 1 && NOISE;
-    constexpr uint32_t PARAMS_WAVE = HD ? 1u : 3u;
+    constexpr uint32_t PARAMS_WAVE = 3u;          // as small_roll_helper_step's
     __shared__ __align__(16) float s_obs[64 * OD];
     __shared__ float s_kin[RK_WORDS * 64];                 // [word][env]
     __shared__ float s_par[RP_WORDS * 64];
     __shared__ float s_ho[NOISE ? RO_WORDS * 64 : 1];
     __shared__ float s_draw[HD ? HD_WORDS * 64 : 1];
-    __shared__ uint32_t s_mask[2];
+    __shared__ uint32_t s_mask[3];
     __shared__ double s_hjgrid[6 * HJ_PTS];
     const SmallRollLds L{s_obs, s_kin, s_par, s_ho, s_draw, s_mask};
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
@@ -2775,7 +2788,7 @@ __global__ void __launch_bounds__(CROLL_SMALL_BLOCK, 1) collect_rollout_kernel_s
     static_assert(NOISE && SPEC == 1, "the fused collect kernels are built for the reference-default shape with noise");
     const KParams P = shape_view<SPEC>(P0);
     constexpr int OD = 34;
-    constexpr uint32_t PARAMS_WAVE = 1u;
+    constexpr uint32_t PARAMS_WAVE = 3u;          // as small_roll_helper_step's
     using PK = Packed<OD, CF2_POLICY_BF16X3>;
     static_assert(PK::TOTAL % 4 == 0, "float4 staging");
     __shared__ __align__(16) float s_frag[PK::TOTAL];
@@ -2784,7 +2797,7 @@ __global__ void __launch_bounds__(CROLL_SMALL_BLOCK, 1) collect_rollout_kernel_s
     __shared__ float s_par[2][RP_WORDS * 64];
     __shared__ float s_ho[2][RO_WORDS * 64];
     __shared__ float s_draw[2][HD_WORDS * 64];
-    __shared__ uint32_t s_mask[2][2];
+    __shared__ uint32_t s_mask[2][3];
     __shared__ double s_hjgrid[6 * HJ_PTS];
     const uint32_t tid = threadIdx.x, wv = tid >> 6, grp = wv >> 2, wave = wv & 3u, lane = tid & 63u;
     const uint32_t base = blockIdx.x * 128u, gbase = base + 64u * grp, i = gbase + lane, gid = P.gid_off + i;
