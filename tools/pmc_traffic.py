@@ -15,17 +15,20 @@ TAIL = 30   # the timed launches: the last 30 dispatches (bench.py --steps 30 af
 
 
 def mean_counter(d, name, kern, tail=TAIL):
-    """Mean per dispatch over the last `tail` dispatches of `kern` (0 = all); a dispatch's counter
-    may come as several rows (per XCD / dimension), which are summed."""
-    per = {}
+    """Mean per dispatch over the last `tail` dispatches of `kern` (0 = all) at the largest grid
+    of the pass (the workload's launches: bench.py's other keys may launch the kernel on fewer
+    envs); a dispatch's counter may come as several rows (per XCD / dimension), which are summed."""
+    per, grid = {}, {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for i, row in enumerate(csv.DictReader(open(f))):
             if kern in row.get("Kernel_Name", "") and row["Counter_Name"] == name:
                 key = int(row.get("Dispatch_Id") or i)
                 per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+                grid[key] = int(row.get("Grid_Size") or 0)
     if not per:
         raise SystemExit(f"no {name} samples for {kern} in {d}")
-    v = [per[k] for k in sorted(per)][-tail if tail else 0:]
+    g = max(grid.values())
+    v = [per[k] for k in sorted(per) if grid[k] == g][-tail if tail else 0:]
     return sum(v) / len(v)
 
 

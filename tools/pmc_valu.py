@@ -21,15 +21,30 @@ SIMDS = 1024
 NAMES = ["SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_WAVES", "GRBM_GUI_ACTIVE"]
 
 
-def per_dispatch(kern, sub="pmc", names=NAMES):
+def per_dispatch(kern, sub="pmc", names=NAMES, grid=None):
+    """Counters per dispatch of kern (rows of one dispatch summed); grid: only dispatches of that
+    grid size."""
     per = {}
     for f in glob.glob(os.path.join(out, sub, "**", "*counter_collection.csv"), recursive=True):
         for i, row in enumerate(csv.DictReader(open(f))):
             if kern in row.get("Kernel_Name", "") and row["Counter_Name"] in names:
+                if grid is not None and int(row.get("Grid_Size") or row.get("Grid_Size_X") or 0) != grid:
+                    continue
                 key = int(row.get("Dispatch_Id") or i)
                 d = per.setdefault(key, {k: 0.0 for k in names})
                 d[row["Counter_Name"]] += float(row["Counter_Value"])
     return [per[k] for k in sorted(per)]
+
+
+def max_grid(kern, sub="pmc"):
+    """The largest grid kern was launched on in the pass: the step kernel's workload launches
+    (bench.py's two_streams key launches it on half the envs)."""
+    g = 0
+    for f in glob.glob(os.path.join(out, sub, "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kern in row.get("Kernel_Name", ""):
+                g = max(g, int(row.get("Grid_Size") or row.get("Grid_Size_X") or 0))
+    return g
 
 
 def mfma_busy(kern, sub="pmc_mfma"):
@@ -44,12 +59,12 @@ def mfma_busy(kern, sub="pmc_mfma"):
             "mfma_busy_frac": busy / SIMDS / (sum(dur) * 1e-9 * 2.4e9)}
 
 
-def durations(kern, sub="pmc"):
+def durations(kern, sub="pmc", grid=None):
     """Profiled dispatch durations (ns) of kern from the kernel trace of the same pass."""
     d = []
     for f in glob.glob(os.path.join(out, sub, "**", "*kernel_trace.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if kern in row.get("Kernel_Name", ""):
+            if kern in row.get("Kernel_Name", "") and (grid is None or int(row.get("Grid_Size") or row.get("Grid_Size_X") or 0) == grid):
                 d.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
     return [x for _, x in sorted(d)]
 
@@ -85,10 +100,11 @@ def collect_entry(kern, label, steps_per_dispatch):
     return dict(summarize(rows, label, steps_per_dispatch, durations(kern, "pmc_collect")), **(mfma_busy(kern) or {}))
 
 
-step = per_dispatch(STEP)[-30:]
+G = max_grid(STEP)
+step = per_dispatch(STEP, grid=G)[-30:]
 roll = per_dispatch(ROLL)
 res = {"workload": f"DroneHoverBulletFreeEnvWithGust-v0:N={N}", "kernel_key": key,
-       "step_kernel": summarize(step, "step_kernel", 1, durations(STEP)[-30:]),
+       "step_kernel": summarize(step, "step_kernel", 1, durations(STEP, grid=G)[-30:]),
        "rollout_kernel": summarize(roll, "rollout_kernel (K=32)", 32, durations(ROLL)),
        "collect_kernel": collect_entry(COLL, "collect_kernel (env-step + policy)", 1),
        "policy_kernel": collect_entry(POL, "policy_kernel (actor-critic forward + sampling, 34-wide obs, bf16x3)", 1),
