@@ -253,8 +253,10 @@ def parse_args(argv=None):
     ap.add_argument("--oc-steps", type=int, default=500)
     ap.add_argument("--action-ring", type=int, default=8,
                     help="action slabs cycled through in the timed region (8 x 4 MB at 262 144 envs)")
-    ap.add_argument("--two-streams", type=int, default=1,
-                    help="N = 1: also time the same envs as two half contexts on two HIP streams (two_streams key)")
+    ap.add_argument("--two-streams", type=int, default=0,
+                    help="N = 1: also time the same envs as two half contexts on two HIP streams (two_streams key; "
+                         "off by default: its half-size step_kernel launches would mix into a rocprof summary "
+                         "of the default run)")
     ap.add_argument("--streaming-ring", type=int, default=64,
                     help="after the timed region, 1000 env-steps with actions cycled through this many "
                          "slabs (64 x 4 MB: more than the 256 MB Infinity Cache); 0 = skip")
