@@ -386,8 +386,9 @@ def main(argv=None):
             pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps))
             if delta:
                 pipe.start(env.obs)
-                gather_mode = (f"pipelined delta all_gather_into_tensor (o_k + reset bitmap + side slab of "
-                               f"{pipe.cap} resets per rank, rows rebuilt on every rank; side stream)")
+                gather_mode = (f"pipelined delta all-gather (o_k + reset bitmap + side slab of "
+                               f"{pipe.cap} resets per rank, rows rebuilt on every rank; side stream; "
+                               f"{pipe.exchange} exchange)")
             else:
                 gather_mode = "pipelined all_gather_into_tensor of the rows (2 obs buffers, side stream)"
         else:
@@ -768,7 +769,11 @@ def main(argv=None):
                        "overflows": pipe.overflows() if pipe is not None else 0,
                        "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
                        "rx_frac_of_xgmi": rx / (elapsed / args.steps) / 1e9 / XGMI_PEAK_GBS,
-                       "launch": "eager per-step launches"}
+                       "launch": "eager per-step launches",
+                       "exchange": pipe.exchange if pipe is not None else "padded all_gather"}
+        if pipe is not None:
+            pipe.drain()
+            pipe.close()
 
     if rank == 0:
         cpu = None

@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
     "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
     "cf2_hbm_probe", "cf2_obs_packed_words", "cf2_obs_pack", "cf2_obs_unpack",
+    "cf2_xchg_bind", "cf2_xchg_unique_id", "cf2_xchg_create", "cf2_xchg_destroy", "cf2_xchg_step", "cf2_xchg_wait",
 )
 
 
@@ -96,6 +97,13 @@ def load() -> ctypes.CDLL:
     lib.cf2_obs_packed_words.argtypes = [u32, u32, u32]
     lib.cf2_obs_pack.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
     lib.cf2_obs_unpack.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
+    lib.cf2_xchg_bind.argtypes = [ctypes.c_char_p]
+    lib.cf2_xchg_unique_id.argtypes = [vp, ctypes.c_size_t]
+    lib.cf2_xchg_create.argtypes = [vp, ctypes.c_size_t, u32, u32, u32, P(vp)]
+    lib.cf2_xchg_destroy.argtypes = [vp]
+    lib.cf2_xchg_step.argtypes = [vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp,
+                                  vp, vp]
+    lib.cf2_xchg_wait.argtypes = [vp, u32, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
                         "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_obs_packed_words"):

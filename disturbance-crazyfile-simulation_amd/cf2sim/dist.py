@@ -166,6 +166,34 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
 NO_WATCH = 0xFFFFFFFF
 PRED_BATCH = 4          # RCCL delta path: time-out counts copied to the host every 4 steps (< lookahead)
 
+_LIVE_XCHG = set()      # native exchanges not closed yet: destroyed at exit, before the runtime unloads
+
+
+def _close_live_exchanges():
+    for g in list(_LIVE_XCHG):
+        g.close()
+
+
+def _native_exchange(lib, group, world: int, depth: int, device):
+    """The RCCL communicator of cf2_xchg_* for this group (collective: every rank calls it): rank
+    0's id broadcast over the process group; PyTorch's own RCCL instance where it ships one."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from . import _native
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    _native.check(lib.cf2_xchg_bind(path.encode() if os.path.exists(path) else None), "cf2_xchg_bind")
+    idb = (ctypes.c_uint8 * 128)()
+    rank = dist.get_rank(group)
+    if rank == 0:
+        _native.check(lib.cf2_xchg_unique_id(idb, 128), "cf2_xchg_unique_id")
+    t = torch.tensor(list(bytes(idb)), dtype=torch.uint8, device=device)
+    dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    idb = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(t.cpu().tolist()))
+    h = ctypes.c_void_p()
+    _native.check(lib.cf2_xchg_create(idb, 128, world, rank, depth, ctypes.byref(h)), "cf2_xchg_create")
+    return h
+
 
 def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, slab_prev, slab, overflow=None,
                watch_age: int = NO_WATCH, pred=None, pred_next=None):
@@ -304,6 +332,7 @@ class PipelinedObsGather:
         # the node shard otherwise): buffers checked once here, raw pointers, reused events, views
         # cached per side capacity
         self._fast = self.delta and self.comm is not None
+        self._xchg = None
         if self._fast:
             from . import _native
             self._lib = _native.load()
@@ -320,6 +349,39 @@ class PipelinedObsGather:
             self._p_done = [t.data_ptr() for t in self.done]
             self._p_slab = [t.data_ptr() for t in self.slab]
             self._p_pred = [self.pred[r].data_ptr() for r in range(self.L + 1)]
+            # the whole step as one C call on our own RCCL communicator (cf2_xchg_step), unless
+            # CF2SIM_EXCHANGE=torch asks for the process group's all-gather between the launches
+            self._xchg = None
+            if os.environ.get("CF2SIM_EXCHANGE", "native") == "native":
+                if self.depth > 8:
+                    raise ValueError("the native exchange keeps at most 8 buffers in flight")
+                self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
+                self._p_age, self._p_ovf = self.age.data_ptr(), self.overflow.data_ptr()
+                _LIVE_XCHG.add(self)
+                if len(_LIVE_XCHG) == 1:
+                    import atexit
+                    atexit.register(_close_live_exchanges)
+
+    @property
+    def exchange(self) -> str:
+        """How a step's exchange runs: 'native' (one cf2_xchg_step call), 'torch' (launches and the
+        process group's all-gather from Python), 'gloo' or 'full'."""
+        if not self.delta:
+            return "full"
+        if not self._fast:
+            return "gloo"
+        return "native" if self._xchg is not None else "torch"
+
+    def close(self):
+        """Release the native exchange's communicator (after drain(); also run at exit)."""
+        x = getattr(self, "_xchg", None)
+        if x is not None:
+            import torch
+            torch.cuda.synchronize(self.device)
+            self._xchg = None
+            _LIVE_XCHG.discard(self)
+            from . import _native
+            _native.check(self._lib.cf2_xchg_destroy(x), "cf2_xchg_destroy")
 
     @property
     def bytes_per_rank_per_step(self) -> int:
@@ -333,9 +395,12 @@ class PipelinedObsGather:
 
     def _wait_free(self, j):
         import torch
-        if self.free[j] is not None:
-            if isinstance(self.free[j], torch.cuda.Event):
-                torch.cuda.current_stream(self.device).wait_event(self.free[j])
+        f = self.free[j]
+        if f is not None:
+            if isinstance(f, torch.cuda.Event):
+                torch.cuda.current_stream(self.device).wait_event(f)
+            elif isinstance(f, int) and self._xchg is not None:     # native: the end event of slot f
+                self._lib.cf2_xchg_wait(self._xchg, f, torch.cuda.current_stream(self.device).cuda_stream)
             self.free[j] = None
 
     def buffer(self):
@@ -491,26 +556,38 @@ class PipelinedObsGather:
             v = self._views[key] = (words, self.send[j][:words], self.recv[j][:self.world * words])
         words, send, recv = v
         lib, comm = self._lib, self.comm
-        ef = self._ev_fork[j]
-        ef.record(torch.cuda.current_stream(self.device))
-        comm.wait_event(ef)
-        st = lib.cf2_obs_pack(self._p_obs[j], self._p_done[j], self.n, self.ol, cap, self._p_send[j],
-                              self._p_send[(j + 1) % D], self._comm_h)
-        if st != 0:
-            from . import _native
-            _native.check(st, "cf2_obs_pack")
-        with torch.cuda.stream(comm):          # the synchronous call: 19 us of host time, async + wait 42 us
-            dist.all_gather_into_tensor(recv, send, group=self.group)
         watch = self.watch
         ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
         w = watch != NO_WATCH
-        st = lib.cf2_obs_unpack(self._p_recv[j], self.world, self.n, self.ol, cap, act.data_ptr(), act_prev.data_ptr(),
-                                self.age.data_ptr(), self._p_slab[(k + 1) % 2], self._p_slab[k % 2],
-                                self.overflow.data_ptr(), int(watch) & 0xFFFFFFFF, self._p_pred[ps] if w else None,
-                                self._p_pred[pn] if w else None, self._comm_h)
-        if st != 0:
-            from . import _native
-            _native.check(st, "cf2_obs_unpack")
+        if self._xchg is not None:
+            # fork, pack, RCCL all-gather, rebuild and the end event of slot j: one C call
+            st = lib.cf2_xchg_step(self._xchg, j, self._p_obs[j], self._p_done[j], self.n, self.ol, cap,
+                                   self._p_send[j], self._p_send[(j + 1) % D], self._p_recv[j], act.data_ptr(),
+                                   act_prev.data_ptr(), self._p_age, self._p_slab[(k + 1) % 2], self._p_slab[k % 2],
+                                   self._p_ovf, int(watch) & 0xFFFFFFFF, self._p_pred[ps] if w else None,
+                                   self._p_pred[pn] if w else None, torch.cuda.current_stream(self.device).cuda_stream,
+                                   self._comm_h)
+            if st != 0:
+                from . import _native
+                _native.check(st, "cf2_xchg_step")
+        else:
+            ef = self._ev_fork[j]
+            ef.record(torch.cuda.current_stream(self.device))
+            comm.wait_event(ef)
+            st = lib.cf2_obs_pack(self._p_obs[j], self._p_done[j], self.n, self.ol, cap, self._p_send[j],
+                                  self._p_send[(j + 1) % D], self._comm_h)
+            if st != 0:
+                from . import _native
+                _native.check(st, "cf2_obs_pack")
+            with torch.cuda.stream(comm):          # the synchronous call: 19 us of host time, async + wait 42 us
+                dist.all_gather_into_tensor(recv, send, group=self.group)
+            st = lib.cf2_obs_unpack(self._p_recv[j], self.world, self.n, self.ol, cap, act.data_ptr(),
+                                    act_prev.data_ptr(), self.age.data_ptr(), self._p_slab[(k + 1) % 2],
+                                    self._p_slab[k % 2], self.overflow.data_ptr(), int(watch) & 0xFFFFFFFF,
+                                    self._p_pred[ps] if w else None, self._p_pred[pn] if w else None, self._comm_h)
+            if st != 0:
+                from . import _native
+                _native.check(st, "cf2_obs_unpack")
         if w and k % PRED_BATCH == 0:
             # the whole count ring to the host every PRED_BATCH steps: step_cap(k') reads the count of
             # step k' - L from the first batch copy at or after it (each is ~15 us of host work)
@@ -521,10 +598,14 @@ class PipelinedObsGather:
             self._pred_batch.append((k, pe))
             if len(self._pred_batch) > len(self._ev_pred) - 1:
                 self._pred_batch.pop(0)
-        eu = self._ev_unp[j]
-        eu.record(comm)
-        self._ready = eu
-        self.free[j] = eu                      # the exchange that read obs / done buffer j ends here
+        if self._xchg is not None:
+            self._ready = j                    # the exchange that read obs / done buffer j ends at slot j
+            self.free[j] = j
+        else:
+            eu = self._ev_unp[j]
+            eu.record(comm)
+            self._ready = eu
+            self.free[j] = eu                  # the exchange that read obs / done buffer j ends here
         self.bytes_sent += 4 * words
         self.steps_sent += 1
         self.k += 1
@@ -534,7 +615,9 @@ class PipelinedObsGather:
         """Make the current stream wait for the latest published slab."""
         import torch
         ev = getattr(self, "_ready", None)
-        if ev is not None:
+        if isinstance(ev, int) and self._xchg is not None:
+            self._lib.cf2_xchg_wait(self._xchg, ev, torch.cuda.current_stream(self.device).cuda_stream)
+        elif ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
 
     def overflows(self) -> int:

@@ -36,8 +36,12 @@
 //                                       (a block's resets hold consecutive slots, in env order)
 //   [.., + cap (OL + 5))                side entries: local env index, o_0[OL], A[4]
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 #include <stdint.h>
+#include <string.h>
 #include <math.h>
+#include <mutex>
 #include "../../include/cf2sim.h"
 #include "cf2sim_internal.h"
 
@@ -280,5 +284,119 @@ extern "C" int cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, ui
                            packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
                            overflow_dev, watch_age, pred_dev, pred_next_dev);
     const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+// ---- the exchange driven natively (cf2_xchg_*): RCCL bound at run time (dlopen), so the library
+// needs no link-time RCCL and shares the instance a host framework already loaded
+namespace {
+struct RcclApi {
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+};
+RcclApi g_rccl;
+std::mutex g_rccl_mu;
+constexpr uint32_t XCHG_MAX_DEPTH = 8;
+}  // namespace
+
+struct cf2_xchg {
+    ncclComm_t comm;
+    uint32_t world, rank, depth;
+    hipEvent_t fork;
+    hipEvent_t end[XCHG_MAX_DEPTH];
+};
+
+extern "C" int cf2_xchg_bind(const char* rccl_path) {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (g_rccl.all_gather) return CF2_OK;
+    const char* path = rccl_path ? rccl_path : "librccl.so.1";
+    void* h = dlopen(path, RTLD_NOW | RTLD_NOLOAD);       // already in the process: that instance
+    if (!h) h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+    if (!h) return CF2_ERR_UNSUPPORTED;
+    RcclApi a;
+    a.get_id = reinterpret_cast<decltype(a.get_id)>(dlsym(h, "ncclGetUniqueId"));
+    a.init = reinterpret_cast<decltype(a.init)>(dlsym(h, "ncclCommInitRank"));
+    a.all_gather = reinterpret_cast<decltype(a.all_gather)>(dlsym(h, "ncclAllGather"));
+    a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
+    if (!a.get_id || !a.init || !a.all_gather || !a.destroy) return CF2_ERR_UNSUPPORTED;
+    g_rccl = a;
+    return CF2_OK;
+}
+
+extern "C" int cf2_xchg_unique_id(uint8_t* id_out, size_t id_len) {
+    if (!id_out || id_len < sizeof(ncclUniqueId)) return CF2_ERR_INVALID_ARG;
+    if (!g_rccl.get_id) return CF2_ERR_UNSUPPORTED;
+    ncclUniqueId id;
+    if (g_rccl.get_id(&id) != ncclSuccess) return CF2_ERR_HIP;
+    memcpy(id_out, &id, sizeof(id));
+    return CF2_OK;
+}
+
+extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world, uint32_t rank, uint32_t depth,
+                               cf2_xchg** out) {
+    if (!id || id_len < sizeof(ncclUniqueId) || !out || world == 0 || rank >= world || depth == 0 ||
+        depth > XCHG_MAX_DEPTH)
+        return CF2_ERR_INVALID_ARG;
+    if (!g_rccl.init) return CF2_ERR_UNSUPPORTED;
+    *out = nullptr;
+    cf2_xchg* x = new cf2_xchg();
+    x->world = world; x->rank = rank; x->depth = depth;
+    hipError_t e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
+    uint32_t made = 0;
+    for (; e == hipSuccess && made < depth; ++made) e = hipEventCreateWithFlags(&x->end[made], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        for (uint32_t k = 0; k + 1 < made; ++k) (void)hipEventDestroy(x->end[k]);
+        if (made) (void)hipEventDestroy(x->fork);
+        delete x;
+        return hip_fail(e);
+    }
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    if (g_rccl.init(&x->comm, (int)world, uid, (int)rank) != ncclSuccess) {
+        for (uint32_t k = 0; k < depth; ++k) (void)hipEventDestroy(x->end[k]);
+        (void)hipEventDestroy(x->fork);
+        delete x;
+        return CF2_ERR_HIP;
+    }
+    *out = x;
+    return CF2_OK;
+}
+
+extern "C" int cf2_xchg_destroy(cf2_xchg* x) {
+    if (!x) return CF2_OK;
+    int st = CF2_OK;
+    if (g_rccl.destroy && g_rccl.destroy(x->comm) != ncclSuccess) st = CF2_ERR_HIP;
+    for (uint32_t k = 0; k < x->depth; ++k) (void)hipEventDestroy(x->end[k]);
+    (void)hipEventDestroy(x->fork);
+    delete x;
+    return st;
+}
+
+extern "C" int cf2_xchg_step(cf2_xchg* x, uint32_t slot, const float* obs_dev, const uint8_t* reset_dev, uint32_t n,
+                             uint32_t obs_len, uint32_t cap, uint32_t* send_dev, uint32_t* send_next_dev,
+                             uint32_t* recv_dev, const float* act_dev, const float* act_prev_dev, uint16_t* age_dev,
+                             const float* slab_prev_dev, float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age,
+                             uint32_t* pred_dev, uint32_t* pred_next_dev, void* env_stream, void* comm_stream) {
+    if (!x || slot >= x->depth || !recv_dev || !layout_ok(n, obs_len, cap)) return CF2_ERR_INVALID_ARG;
+    const hipStream_t cs = (hipStream_t)comm_stream;
+    hipError_t e = hipEventRecord(x->fork, (hipStream_t)env_stream);     // the env-step that wrote obs / done
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs, x->fork, 0);
+    if (e != hipSuccess) return hip_fail(e);
+    int st = cf2_obs_pack(obs_dev, reset_dev, n, obs_len, cap, send_dev, send_next_dev, comm_stream);
+    if (st != CF2_OK) return st;
+    const size_t words = PackLayout{n, obs_len, cap}.words();
+    if (g_rccl.all_gather(send_dev, recv_dev, words, ncclUint32, x->comm, cs) != ncclSuccess) return CF2_ERR_HIP;
+    st = cf2_obs_unpack(recv_dev, x->world, n, obs_len, cap, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
+                        overflow_dev, watch_age, pred_dev, pred_next_dev, comm_stream);
+    if (st != CF2_OK) return st;
+    e = hipEventRecord(x->end[slot], cs);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream) {
+    if (!x || slot >= x->depth) return CF2_ERR_INVALID_ARG;
+    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->end[slot], 0);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }

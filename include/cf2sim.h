@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 6
+#define CF2SIM_ABI_VERSION 7
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -360,6 +360,30 @@ int  cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, 
                     const float* act_dev, const float* act_prev_dev, uint16_t* age_dev, const float* slab_prev_dev,
                     float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
                     uint32_t* pred_next_dev, void* stream);
+
+/* The same exchange driven natively, one call per env-step: an RCCL communicator of this library's
+ * own (one rank per GPU, created on the current device) and, per step, pack -> ncclAllGather of the
+ * packed words -> rebuild, on comm_stream after env_stream's work so far (an event fork), ending
+ * with an event of slot `slot` (< depth) that cf2_xchg_wait makes a stream wait for.  What the
+ * host would otherwise do per step with three launches, a process-group all-gather and stream /
+ * event calls (~65 us of host time at the node shard) is one C call.
+ * cf2_xchg_bind: the RCCL library to use (NULL: "librccl.so.1"); an instance the process has
+ * already loaded (e.g. PyTorch's) is reused.  cf2_xchg_unique_id: on one rank, the 128-byte id
+ * every rank passes to cf2_xchg_create (collective: all ranks call it together).  The arguments of
+ * cf2_xchg_step are those of cf2_obs_pack and cf2_obs_unpack; recv_dev holds world x
+ * cf2_obs_packed_words(n, obs_len, cap) words.  RCCL failures return CF2_ERR_HIP. */
+typedef struct cf2_xchg cf2_xchg;
+int  cf2_xchg_bind(const char* rccl_path);
+int  cf2_xchg_unique_id(uint8_t* id_out, size_t id_len);
+int  cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world, uint32_t rank, uint32_t depth,
+                     cf2_xchg** out);
+int  cf2_xchg_destroy(cf2_xchg* x);
+int  cf2_xchg_step(cf2_xchg* x, uint32_t slot, const float* obs_dev, const uint8_t* reset_dev, uint32_t n,
+                   uint32_t obs_len, uint32_t cap, uint32_t* send_dev, uint32_t* send_next_dev, uint32_t* recv_dev,
+                   const float* act_dev, const float* act_prev_dev, uint16_t* age_dev, const float* slab_prev_dev,
+                   float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
+                   uint32_t* pred_next_dev, void* env_stream, void* comm_stream);
+int  cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream);
 
 /* Measurement support (no reference counterpart): streaming kernels over `bytes` (a multiple of
  * 16, both pointers 16-B aligned) with non-temporal accesses.  mode 0: copy src -> dst; mode 1:

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_config_struct_matches(lib):
     from cf2sim.config import CF2Config
     assert lib.cf2_config_sizeof() == ctypes.sizeof(CF2Config)
-    assert lib.cf2_abi_version() == 6
+    assert lib.cf2_abi_version() == 7
 
 
 def test_status_strings_and_invalid_args(lib):

@@ -75,8 +75,9 @@ def test_kernels_equal_torch_ops(gpu, world, n, ol, cap):
         assert int(ovf_g.item()) > 0
 
 
-def _run_env(rank, world, port, out, backend, n, T):
+def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
     sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+    os.environ["CF2SIM_EXCHANGE"] = exchange
     import torch.distributed as dist
     from cf2sim.dist import PipelinedObsGather, gather_rows
     from cf2sim.vec_env import BatchedCrazyflieEnv
@@ -115,28 +116,39 @@ def _run_env(rank, world, port, out, backend, n, T):
         if not torch.equal(slab, full):
             bad.append(k)
     torch.cuda.synchronize()
+    how = pipe.exchange
+    pipe.close()
     if rank == 0:
         with open(out, "w") as f:
-            f.write(f"{len(bad)} {resets} {pipe.overflows()} {bad[:3]}")
+            f.write(f"{len(bad)} {resets} {pipe.overflows()} {how} {bad[:3]}")
     dist.destroy_process_group()
 
 
-def _check(out, T):
-    nbad, resets, ovf = open(out).read().split()[:3]
+def _check(out, T, how):
+    nbad, resets, ovf, got = open(out).read().split()[:4]
     assert int(nbad) == 0, open(out).read()
     assert int(resets) > 0 and int(ovf) == 0
+    assert got == how
 
 
 def test_delta_exchange_one_rccl_rank(gpu, tmp_path):
+    """The native exchange (cf2_xchg_step: pack, our own RCCL communicator's all-gather, rebuild)."""
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240), nprocs=1, join=True)
-    _check(out, 240)
+    _check(out, 240, "native")
+
+
+def test_delta_exchange_one_rccl_rank_torch_path(gpu, tmp_path):
+    """The same exchange with the process group's all-gather between the launches from Python."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "torch"), nprocs=1, join=True)
+    _check(out, 240, "torch")
 
 
 def test_delta_exchange_two_gloo_ranks_on_one_gpu(gpu, tmp_path):
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 240), nprocs=2, join=True)
-    _check(out, 240)
+    _check(out, 240, "gloo")
 
 
 def test_unpack_rejects_operands_the_kernel_would_overrun(gpu):
