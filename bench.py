@@ -401,12 +401,17 @@ def main(argv=None):
     pipe_p = None
     if pipe is not None:
         pipe_p = ([b.data_ptr() for b in pipe.obs], [b.data_ptr() for b in pipe.done] if delta else None)
+    # the native exchange: env-step and exchange in one C call per step (cf2_xchg_env_step)
+    native_x = pipe is not None and delta and pipe.exchange == "native"
+    act_gp = [a.data_ptr() for a in act_g] if native_x else None
 
     def one_step(k, with_gather):
         j = kk[0]
         kk[0] += 1
         r = j % ring
-        if with_gather and pipe is not None:
+        if with_gather and native_x:
+            pipe.step_and_publish(env, act_p[r], act_gp[r], act_gp[(j - 1) % ring])
+        elif with_gather and pipe is not None:
             b = pipe.k % pipe.depth
             pipe.buffer()                  # waits (on the device) until the exchange that read it is done
             if delta:

@@ -357,6 +357,14 @@ class PipelinedObsGather:
                     raise ValueError("the native exchange keeps at most 8 buffers in flight")
                 self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
                 self._p_age, self._p_ovf = self.age.data_ptr(), self.overflow.data_ptr()
+                import ctypes
+                arr = lambda ptrs: (ctypes.c_void_p * len(ptrs))(*ptrs)     # noqa: E731
+                self._reg = [arr(self._p_obs), arr(self._p_done), arr(self._p_send), arr(self._p_recv),
+                             arr(self._p_pred)]
+                _native.check(self._lib.cf2_xchg_register(
+                    self._xchg, self.n, self.ol, int(self.watch) & 0xFFFFFFFF, *self._reg[:4], self._p_slab[0],
+                    self._p_slab[1], self._p_age, self._p_ovf, self._reg[4], self.L + 1, self._comm_h),
+                    "cf2_xchg_register")
                 _LIVE_XCHG.add(self)
                 if len(_LIVE_XCHG) == 1:
                     import atexit
@@ -588,6 +596,38 @@ class PipelinedObsGather:
             if st != 0:
                 from . import _native
                 _native.check(st, "cf2_obs_unpack")
+        return self._published(k, j, words, w)
+
+    def step_and_publish(self, env, act_ptr: int, act_all_ptr: int, act_prev_all_ptr: int):
+        """Native exchange: env-step k of `env` (this rank's shard; act_ptr its [n, 4] actions) into
+        the exchange's buffers, then that step's exchange, in one C call (cf2_xchg_env_step: what
+        buffer() + env.step_raw(...) + publish(act_all, act_prev_all) do).  Raw device pointers,
+        not checked (act_all / act_prev_all: [world * n, 4] float32, as publish() takes them).
+        Returns the slab of step k."""
+        import torch
+        if self._xchg is None:
+            raise RuntimeError("step_and_publish needs the native exchange (RCCL, delta=True)")
+        if not self.started:
+            raise RuntimeError("delta exchange: call start(reset observations) first")
+        if env.num_envs != self.n or env.obs_dim != self.od:
+            raise ValueError("step_and_publish: the env's shard does not match the exchange's layout")
+        k, j = self.k, self.k % self.depth
+        cap = self.step_cap(k)
+        rew, trunc, cost, level = env._raw_step_outputs()
+        st = self._lib.cf2_xchg_env_step(self._xchg, env._ctx, k, cap, act_ptr, act_all_ptr, act_prev_all_ptr, rew,
+                                         trunc, cost, level, torch.cuda.current_stream(self.device).cuda_stream)
+        if st != 0:
+            from . import _native
+            _native.check(st, "cf2_xchg_env_step")
+        words = self._views.get(("w", cap))
+        if words is None:
+            words = self._views[("w", cap)] = packed_words(self.n, self.ol, cap)
+        return self._published(k, j, words, self.watch != NO_WATCH)
+
+    def _published(self, k, j, words, w):
+        """publish()'s bookkeeping after the exchange of step k (buffer slot j) was issued."""
+        import torch
+        comm = self.comm
         if w and k % PRED_BATCH == 0:
             # the whole count ring to the host every PRED_BATCH steps: step_cap(k') reads the count of
             # step k' - L from the first batch copy at or after it (each is ~15 us of host work)

@@ -410,6 +410,18 @@ class BatchedCrazyflieEnv:
         if st != 0:
             _native.check(st, "cf2_step")
 
+    def _raw_step_outputs(self):
+        """For an env-step launched outside step_raw (the native exchange's cf2_xchg_env_step, whose
+        observations go to the exchange's buffers): the reward / truncation / cost / level output
+        addresses; the step is recorded as step_raw records one."""
+        self._obs_latest = None
+        self._state_version += 1
+        p = self._raw_ptrs
+        if p is None:
+            p = self._raw_ptrs = (self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(), self.trunc.data_ptr(),
+                                  self.cost.data_ptr(), self.level.data_ptr())
+        return p[1], p[3], p[4], p[5]
+
     # ---- state snapshot ----
     def get_state(self):
         sf = torch.empty(self.layout.num_float_fields, self.num_envs, dtype=torch.float32, device=self.device)

@@ -301,11 +301,27 @@ std::mutex g_rccl_mu;
 constexpr uint32_t XCHG_MAX_DEPTH = 8;
 }  // namespace
 
+constexpr uint32_t XCHG_MAX_PRED = 64;
+
 struct cf2_xchg {
     ncclComm_t comm;
     uint32_t world, rank, depth;
     hipEvent_t fork;
     hipEvent_t end[XCHG_MAX_DEPTH];
+    bool pending[XCHG_MAX_DEPTH];      // slot's exchange issued: the next env-step into it waits for end[slot]
+    bool recorded[XCHG_MAX_DEPTH];     // end[slot] has been recorded at least once
+    // registered buffers (cf2_xchg_register) for cf2_xchg_env_step
+    bool registered;
+    uint32_t n, ol, watch, npred;
+    float* obs[XCHG_MAX_DEPTH];
+    uint8_t* done[XCHG_MAX_DEPTH];
+    uint32_t* send[XCHG_MAX_DEPTH];
+    uint32_t* recv[XCHG_MAX_DEPTH];
+    float* slab[2];
+    uint16_t* age;
+    uint32_t* overflow;
+    uint32_t* pred[XCHG_MAX_PRED];
+    hipStream_t comm_stream;
 };
 
 extern "C" int cf2_xchg_bind(const char* rccl_path) {
@@ -392,11 +408,55 @@ extern "C" int cf2_xchg_step(cf2_xchg* x, uint32_t slot, const float* obs_dev, c
                         overflow_dev, watch_age, pred_dev, pred_next_dev, comm_stream);
     if (st != CF2_OK) return st;
     e = hipEventRecord(x->end[slot], cs);
-    return e == hipSuccess ? CF2_OK : hip_fail(e);
+    if (e != hipSuccess) return hip_fail(e);
+    x->pending[slot] = x->recorded[slot] = true;
+    return CF2_OK;
 }
 
 extern "C" int cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream) {
     if (!x || slot >= x->depth) return CF2_ERR_INVALID_ARG;
+    if (!x->recorded[slot]) return CF2_OK;
     const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->end[slot], 0);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, float* const* obs_dev,
+                                 uint8_t* const* reset_dev, uint32_t* const* send_dev, uint32_t* const* recv_dev,
+                                 float* slab0_dev, float* slab1_dev, uint16_t* age_dev, uint32_t* overflow_dev,
+                                 uint32_t* const* pred_dev, uint32_t npred, void* comm_stream) {
+    if (!x || !obs_dev || !reset_dev || !send_dev || !recv_dev || !slab0_dev || !slab1_dev || !age_dev ||
+        !layout_ok(n, obs_len, n) || npred > XCHG_MAX_PRED || (watch_age != 0xFFFFFFFFu && (npred < 2 || !pred_dev)))
+        return CF2_ERR_INVALID_ARG;
+    for (uint32_t j = 0; j < x->depth; ++j) {
+        if (!obs_dev[j] || !reset_dev[j] || !send_dev[j] || !recv_dev[j]) return CF2_ERR_INVALID_ARG;
+        x->obs[j] = obs_dev[j]; x->done[j] = reset_dev[j]; x->send[j] = send_dev[j]; x->recv[j] = recv_dev[j];
+    }
+    for (uint32_t r = 0; r < npred; ++r) x->pred[r] = pred_dev[r];
+    x->n = n; x->ol = obs_len; x->watch = watch_age; x->npred = npred;
+    x->slab[0] = slab0_dev; x->slab[1] = slab1_dev;
+    x->age = age_dev; x->overflow = overflow_dev;
+    x->comm_stream = (hipStream_t)comm_stream;
+    x->registered = true;
+    return CF2_OK;
+}
+
+extern "C" int cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, const float* act_dev,
+                                 const float* act_all_dev, const float* act_prev_all_dev, float* rew_dev,
+                                 uint8_t* trunc_dev, float* cost_dev, float* level_dev, void* env_stream) {
+    if (!x || !x->registered || !ctx) return CF2_ERR_INVALID_ARG;
+    const uint32_t j = (uint32_t)(k % x->depth);
+    const hipStream_t es = (hipStream_t)env_stream;
+    if (x->pending[j]) {                 // the exchange that last read buffer j
+        const hipError_t e = hipStreamWaitEvent(es, x->end[j], 0);
+        if (e != hipSuccess) return hip_fail(e);
+        x->pending[j] = false;
+    }
+    int st = cf2_step(ctx, act_dev, nullptr, x->obs[j], rew_dev, x->done[j], trunc_dev, cost_dev, level_dev, nullptr,
+                      env_stream);
+    if (st != CF2_OK) return st;
+    const bool w = x->watch != 0xFFFFFFFFu;
+    return cf2_xchg_step(x, j, x->obs[j], x->done[j], x->n, x->ol, cap, x->send[j], x->send[(j + 1) % x->depth],
+                         x->recv[j], act_all_dev, act_prev_all_dev, x->age, x->slab[(k + 1) % 2], x->slab[k % 2],
+                         x->overflow, x->watch, w ? x->pred[k % x->npred] : nullptr,
+                         w ? x->pred[(k + 1) % x->npred] : nullptr, env_stream, x->comm_stream);
 }

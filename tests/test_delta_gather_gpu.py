@@ -77,7 +77,7 @@ def test_kernels_equal_torch_ops(gpu, world, n, ol, cap):
 
 def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
     sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
-    os.environ["CF2SIM_EXCHANGE"] = exchange
+    os.environ["CF2SIM_EXCHANGE"] = "native" if exchange == "native_env" else exchange
     import torch.distributed as dist
     from cf2sim.dist import PipelinedObsGather, gather_rows
     from cf2sim.vec_env import BatchedCrazyflieEnv
@@ -104,13 +104,20 @@ def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
         bad.append(-1)
     for k in range(T):
         a = acts[k]
-        buf = pipe.buffer()
-        done = pipe.done_buffer()
-        env.step_raw(a[rank * n:(rank + 1) * n].data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=done.data_ptr())
-        ref_obs = buf.clone()
-        ref_done = done.clone()
-        slab = pipe.publish(a, acts[k - 1] if k > 0 else a)
-        pipe.drain()
+        a_prev = acts[k - 1] if k > 0 else a
+        if exchange == "native_env":       # env-step + exchange in one C call
+            j = pipe.k % pipe.depth
+            slab = pipe.step_and_publish(env, a[rank * n:(rank + 1) * n].data_ptr(), a.data_ptr(), a_prev.data_ptr())
+            pipe.drain()
+            ref_obs, ref_done = pipe.obs[j].clone(), pipe.done[j].clone()
+        else:
+            buf = pipe.buffer()
+            done = pipe.done_buffer()
+            env.step_raw(a[rank * n:(rank + 1) * n].data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=done.data_ptr())
+            ref_obs = buf.clone()
+            ref_done = done.clone()
+            slab = pipe.publish(a, a_prev)
+            pipe.drain()
         full = gather_rows(ref_obs, sizes=[n] * world)
         resets += int(gather_rows(ref_done, sizes=[n] * world).sum())
         if not torch.equal(slab, full):
@@ -135,6 +142,13 @@ def test_delta_exchange_one_rccl_rank(gpu, tmp_path):
     """The native exchange (cf2_xchg_step: pack, our own RCCL communicator's all-gather, rebuild)."""
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240), nprocs=1, join=True)
+    _check(out, 240, "native")
+
+
+def test_delta_exchange_one_rccl_rank_env_step_in_one_call(gpu, tmp_path):
+    """The native exchange's registered form: env-step + exchange per cf2_xchg_env_step call."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "native_env"), nprocs=1, join=True)
     _check(out, 240, "native")
 
 

@@ -80,6 +80,11 @@ def main():
         pipe.publish(ag_[1], ag_[0])
     t("delta_step_eager_total", full_step)
     pipe.drain()
+    if pipe.exchange == "native":         # the env-step and its exchange as one C call
+        ap, a1, a0 = acts[0].data_ptr(), ag_[1].data_ptr(), ag_[0].data_ptr()
+        t("delta_step_one_call", lambda: pipe.step_and_publish(env, ap, a1, a0))
+        pipe.drain()
+    pipe.close()
     print(json.dumps({k: round(v, 2) for k, v in out.items()}))
     dist.destroy_process_group()
 
