@@ -355,7 +355,12 @@ class PipelinedObsGather:
             if os.environ.get("CF2SIM_EXCHANGE", "native") == "native":
                 if self.depth > 8:
                     raise ValueError("the native exchange keeps at most 8 buffers in flight")
-                self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
+                try:
+                    self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
+                except _native.CF2Error as e:      # e.g. no RCCL library to bind: the torch path, said so
+                    import warnings
+                    warnings.warn(f"native exchange unavailable ({e}); using the process group's all-gather")
+            if self._xchg is not None:
                 self._p_age, self._p_ovf = self.age.data_ptr(), self.overflow.data_ptr()
                 import ctypes
                 arr = lambda ptrs: (ctypes.c_void_p * len(ptrs))(*ptrs)     # noqa: E731
