@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
     "cf2_hbm_probe", "cf2_obs_packed_words", "cf2_obs_pack", "cf2_obs_unpack",
     "cf2_xchg_bind", "cf2_xchg_unique_id", "cf2_xchg_create", "cf2_xchg_destroy", "cf2_xchg_step", "cf2_xchg_wait",
-    "cf2_xchg_register", "cf2_xchg_env_step",
+    "cf2_xchg_register", "cf2_xchg_env_step", "cf2_xchg_pred_sync",
 )
 
 
@@ -105,7 +105,8 @@ def load() -> ctypes.CDLL:
     lib.cf2_xchg_step.argtypes = [vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp,
                                   vp, vp]
     lib.cf2_xchg_wait.argtypes = [vp, u32, vp]
-    lib.cf2_xchg_register.argtypes = [vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]
+    lib.cf2_xchg_register.argtypes = [vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, u32, u32, vp]
+    lib.cf2_xchg_pred_sync.argtypes = [vp, ctypes.c_uint64]
     lib.cf2_xchg_env_step.argtypes = [vp, vp, ctypes.c_uint64, u32, vp, vp, vp, vp, vp, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",

@@ -368,8 +368,9 @@ class PipelinedObsGather:
                              arr(self._p_pred)]
                 _native.check(self._lib.cf2_xchg_register(
                     self._xchg, self.n, self.ol, int(self.watch) & 0xFFFFFFFF, *self._reg[:4], self._p_slab[0],
-                    self._p_slab[1], self._p_age, self._p_ovf, self._reg[4], self.L + 1, self._comm_h),
-                    "cf2_xchg_register")
+                    self._p_slab[1], self._p_age, self._p_ovf, self._reg[4], self.L + 1,
+                    self.pred_host.data_ptr() if self.watch != NO_WATCH else None, PRED_BATCH, len(self._ev_pred),
+                    self._comm_h), "cf2_xchg_register")
                 _LIVE_XCHG.add(self)
                 if len(_LIVE_XCHG) == 1:
                     import atexit
@@ -472,8 +473,11 @@ class PipelinedObsGather:
             # the first batch copy issued at or after step k - L (issued after that step's rebuild;
             # the slot is only cleared by the rebuild of step k, after this read)
             s = (k - self.L) % (self.L + 1)
-            ev = next(e for (c, e) in self._pred_batch if c >= k - self.L)
-            ev.synchronize()
+            c, ev = next((c, e) for (c, e) in self._pred_batch if c >= k - self.L)
+            if ev is None:                   # copied by cf2_xchg_env_step
+                self._lib.cf2_xchg_pred_sync(self._xchg, c)
+            else:
+                ev.synchronize()
             t = int(self.pred_host[s].max())
         else:
             s = (k - self.L) % (self.L + 1)
@@ -627,10 +631,15 @@ class PipelinedObsGather:
         words = self._views.get(("w", cap))
         if words is None:
             words = self._views[("w", cap)] = packed_words(self.n, self.ol, cap)
-        return self._published(k, j, words, self.watch != NO_WATCH)
+        if self.watch != NO_WATCH and k % PRED_BATCH == 0:      # the C call copied the count ring
+            self._pred_batch.append((k, None))
+            if len(self._pred_batch) > len(self._ev_pred) - 1:
+                self._pred_batch.pop(0)
+        return self._published(k, j, words, False)
 
     def _published(self, k, j, words, w):
-        """publish()'s bookkeeping after the exchange of step k (buffer slot j) was issued."""
+        """publish()'s bookkeeping after the exchange of step k (buffer slot j) was issued (w: copy
+        the time-out count ring to the host at this step's batch boundary)."""
         import torch
         comm = self.comm
         if w and k % PRED_BATCH == 0:

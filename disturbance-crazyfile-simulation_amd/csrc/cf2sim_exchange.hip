@@ -301,7 +301,7 @@ std::mutex g_rccl_mu;
 constexpr uint32_t XCHG_MAX_DEPTH = 8;
 }  // namespace
 
-constexpr uint32_t XCHG_MAX_PRED = 64;
+constexpr uint32_t XCHG_MAX_PRED = 64, XCHG_MAX_PRED_EV = 16;
 
 struct cf2_xchg {
     ncclComm_t comm;
@@ -321,6 +321,11 @@ struct cf2_xchg {
     uint16_t* age;
     uint32_t* overflow;
     uint32_t* pred[XCHG_MAX_PRED];
+    // the look-ahead ring copied to pinned host memory every pred_batch env-steps, each copy
+    // followed by an event of a ring of npev (cf2_xchg_pred_sync)
+    uint32_t* pred_host;
+    uint32_t pred_batch, npev;
+    hipEvent_t pev[XCHG_MAX_PRED_EV];
     hipStream_t comm_stream;
 };
 
@@ -383,6 +388,7 @@ extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world,
 extern "C" int cf2_xchg_destroy(cf2_xchg* x) {
     if (!x) return CF2_OK;
     int st = CF2_OK;
+    for (uint32_t k = 0; k < x->npev; ++k) (void)hipEventDestroy(x->pev[k]);
     if (g_rccl.destroy && g_rccl.destroy(x->comm) != ncclSuccess) st = CF2_ERR_HIP;
     for (uint32_t k = 0; k < x->depth; ++k) (void)hipEventDestroy(x->end[k]);
     (void)hipEventDestroy(x->fork);
@@ -423,10 +429,28 @@ extern "C" int cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream) {
 extern "C" int cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, float* const* obs_dev,
                                  uint8_t* const* reset_dev, uint32_t* const* send_dev, uint32_t* const* recv_dev,
                                  float* slab0_dev, float* slab1_dev, uint16_t* age_dev, uint32_t* overflow_dev,
-                                 uint32_t* const* pred_dev, uint32_t npred, void* comm_stream) {
-    if (!x || !obs_dev || !reset_dev || !send_dev || !recv_dev || !slab0_dev || !slab1_dev || !age_dev ||
-        !layout_ok(n, obs_len, n) || npred > XCHG_MAX_PRED || (watch_age != 0xFFFFFFFFu && (npred < 2 || !pred_dev)))
+                                 uint32_t* const* pred_dev, uint32_t npred, uint32_t* pred_host, uint32_t pred_batch,
+                                 uint32_t pred_events, void* comm_stream) {
+    if (!x || x->registered || !obs_dev || !reset_dev || !send_dev || !recv_dev || !slab0_dev || !slab1_dev ||
+        !age_dev || !layout_ok(n, obs_len, n) || npred > XCHG_MAX_PRED || pred_events > XCHG_MAX_PRED_EV ||
+        (watch_age != 0xFFFFFFFFu && (npred < 2 || !pred_dev)) ||
+        (pred_host && (watch_age == 0xFFFFFFFFu || pred_batch == 0 || pred_events == 0)))
         return CF2_ERR_INVALID_ARG;
+    for (uint32_t r = 1; r < npred; ++r)           // one [npred][world] array
+        if (pred_dev[r] != pred_dev[0] + (size_t)r * x->world) return CF2_ERR_INVALID_ARG;
+    if (pred_host) {
+        hipError_t e = hipSuccess;
+        for (; e == hipSuccess && x->npev < pred_events; ++x->npev)
+            e = hipEventCreateWithFlags(&x->pev[x->npev], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            --x->npev;
+            for (uint32_t k = 0; k < x->npev; ++k) (void)hipEventDestroy(x->pev[k]);
+            x->npev = 0;
+            return hip_fail(e);
+        }
+    }
+    x->pred_host = pred_host;
+    x->pred_batch = pred_batch;
     for (uint32_t j = 0; j < x->depth; ++j) {
         if (!obs_dev[j] || !reset_dev[j] || !send_dev[j] || !recv_dev[j]) return CF2_ERR_INVALID_ARG;
         x->obs[j] = obs_dev[j]; x->done[j] = reset_dev[j]; x->send[j] = send_dev[j]; x->recv[j] = recv_dev[j];
@@ -455,8 +479,19 @@ extern "C" int cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t
                       env_stream);
     if (st != CF2_OK) return st;
     const bool w = x->watch != 0xFFFFFFFFu;
-    return cf2_xchg_step(x, j, x->obs[j], x->done[j], x->n, x->ol, cap, x->send[j], x->send[(j + 1) % x->depth],
-                         x->recv[j], act_all_dev, act_prev_all_dev, x->age, x->slab[(k + 1) % 2], x->slab[k % 2],
-                         x->overflow, x->watch, w ? x->pred[k % x->npred] : nullptr,
-                         w ? x->pred[(k + 1) % x->npred] : nullptr, env_stream, x->comm_stream);
+    st = cf2_xchg_step(x, j, x->obs[j], x->done[j], x->n, x->ol, cap, x->send[j], x->send[(j + 1) % x->depth],
+                       x->recv[j], act_all_dev, act_prev_all_dev, x->age, x->slab[(k + 1) % 2], x->slab[k % 2],
+                       x->overflow, x->watch, w ? x->pred[k % x->npred] : nullptr,
+                       w ? x->pred[(k + 1) % x->npred] : nullptr, env_stream, x->comm_stream);
+    if (st != CF2_OK || !x->pred_host || k % x->pred_batch) return st;
+    hipError_t e = hipMemcpyAsync(x->pred_host, x->pred[0], (size_t)x->npred * x->world * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, x->comm_stream);
+    if (e == hipSuccess) e = hipEventRecord(x->pev[(k / x->pred_batch) % x->npev], x->comm_stream);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_xchg_pred_sync(cf2_xchg* x, uint64_t k) {
+    if (!x || !x->pred_host || k % x->pred_batch) return CF2_ERR_INVALID_ARG;
+    const hipError_t e = hipEventSynchronize(x->pev[(k / x->pred_batch) % x->npev]);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
 }

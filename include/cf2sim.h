@@ -385,14 +385,19 @@ int  cf2_xchg_step(cf2_xchg* x, uint32_t slot, const float* obs_dev, const uint8
                    uint32_t* pred_next_dev, void* env_stream, void* comm_stream);
 int  cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream);
 /* Registered form: the exchange's buffers set once (obs / reset / send / recv: depth each; slab0,
- * slab1; pred: npred rows of world counters, the look-ahead ring, when watch_age is on), then one
- * call per env-step k runs the env-step of ctx into obs[k % depth] / reset[k % depth] (cf2_step
- * with the given reward / truncation / cost / level outputs; it first waits for the exchange that
- * last read that buffer) and that step's exchange into slab[k % 2] from slab[(k + 1) % 2]. */
+ * slab1; pred: npred rows of world counters, one [npred][world] array, the look-ahead ring, when
+ * watch_age is on), then one call per env-step k runs the env-step of ctx into obs[k % depth] /
+ * reset[k % depth] (cf2_step with the given reward / truncation / cost / level outputs; it first
+ * waits for the exchange that last read that buffer) and that step's exchange into slab[k % 2]
+ * from slab[(k + 1) % 2].  pred_host (pinned, npred x world words; or NULL): every pred_batch
+ * env-steps the call also copies the whole ring there, followed by an event of a ring of
+ * pred_events; cf2_xchg_pred_sync(x, k) waits on the host for the copy made at step k. */
 int  cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, float* const* obs_dev,
                        uint8_t* const* reset_dev, uint32_t* const* send_dev, uint32_t* const* recv_dev,
                        float* slab0_dev, float* slab1_dev, uint16_t* age_dev, uint32_t* overflow_dev,
-                       uint32_t* const* pred_dev, uint32_t npred, void* comm_stream);
+                       uint32_t* const* pred_dev, uint32_t npred, uint32_t* pred_host, uint32_t pred_batch,
+                       uint32_t pred_events, void* comm_stream);
+int  cf2_xchg_pred_sync(cf2_xchg* x, uint64_t k);
 int  cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, const float* act_dev,
                        const float* act_all_dev, const float* act_prev_all_dev, float* rew_dev, uint8_t* trunc_dev,
                        float* cost_dev, float* level_dev, void* env_stream);
