@@ -23,9 +23,12 @@ rank stepping its contiguous global-id shard (32 768 envs per GPU at N = 8; "sca
 is the north-star variant with the per-step RCCL all-gather of the observation slab over xGMI
 (--gather-obs, default on at N > 1), pipelined with the next env-step.  By default the exchange
 moves deltas (--gather-mode delta, cf2sim.dist: o_k of every env, a reset bitmap and the reset
-rows' first halves; every rank rebuilds the full [262144, 34] slab bit-identically from the
-previous one and the actions, which every rank holds), 2.36x fewer xGMI bytes than the full rows
-(--gather-mode full).  The same shards without the gather ("no_gather") and 262 144 envs per GPU
+rows' first halves; every rank keeps what it gathered and advances the envs' ages, and any row of
+the [262144, 34] slab is materialised bit-identically on request from those buffers and the
+actions, which every rank holds), 2.36x fewer xGMI bytes than the full rows (--gather-mode full).
+Over RCCL the timed env-steps run back to back with the exchange's pack fused into the env-step
+kernel, and each batch of 16 steps is all-gathered and consumed on the exchange stream while the
+next batch steps (PipelinedObsGather.run / cf2_xchg_run).  The same shards without the gather ("no_gather") and 262 144 envs per GPU
 ("weak_scaling") are extra keys of the line.
 """
 from __future__ import annotations
@@ -243,7 +246,7 @@ def parse_args(argv=None):
                     help="per-step RCCL all-gather of the obs slab (default: on at N > 1)")
     ap.add_argument("--no-gather-obs", dest="gather_obs", action="store_false")
     ap.add_argument("--gather-mode", choices=("delta", "full"), default="delta",
-                    help="delta: o_k + reset side slab, every rank rebuilds the rows (default); full: the rows")
+                    help="delta: o_k + reset side slab, rows materialised on request (default); full: the rows")
     ap.add_argument("--weak-envs", type=int, default=262144,
                     help="N > 1: the weak_scaling key times this many envs per rank; 0 = skip")
     ap.add_argument("--weak-steps", type=int, default=1000)
@@ -387,8 +390,8 @@ def main(argv=None):
             if delta:
                 pipe.start(env.obs)
                 gather_mode = (f"pipelined delta all-gather (o_k + reset bitmap + side slab of "
-                               f"{pipe.cap} resets per rank, rows rebuilt on every rank; side stream; "
-                               f"{pipe.exchange} exchange)")
+                               f"{pipe.cap} resets per rank + predicted time-outs; every rank advances the ages, "
+                               f"rows on request; side stream; {pipe.exchange} exchange)")
             else:
                 gather_mode = "pipelined all_gather_into_tensor of the rows (2 obs buffers, side stream)"
         else:
@@ -401,29 +404,34 @@ def main(argv=None):
     pipe_p = None
     if pipe is not None:
         pipe_p = ([b.data_ptr() for b in pipe.obs], [b.data_ptr() for b in pipe.done] if delta else None)
-    # the native exchange: env-step and exchange in one C call per step (cf2_xchg_env_step)
+    # the native exchange: env-steps back to back (the pack fused in), one all-gather + consume per
+    # batch of 16 (cf2_xchg_run); the actions of step k are slab k % ring, as in the eager loop
     native_x = pipe is not None and delta and pipe.exchange == "native"
-    act_gp = [a.data_ptr() for a in act_g] if native_x else None
 
     def one_step(k, with_gather):
         j = kk[0]
         kk[0] += 1
         r = j % ring
-        if with_gather and native_x:
-            pipe.step_and_publish(env, act_p[r], act_gp[r], act_gp[(j - 1) % ring])
-        elif with_gather and pipe is not None:
+        if with_gather and pipe is not None:
             b = pipe.k % pipe.depth
             pipe.buffer()                  # waits (on the device) until the exchange that read it is done
             if delta:
                 env.step_raw(act_p[r], obs_ptr=pipe_p[0][b], done_ptr=pipe_p[1][b])
-                pipe.publish(act_g[r], act_g[(j - 1) % ring])
             else:
                 env.step_raw(act_p[r], obs_ptr=pipe_p[0][b])
-                pipe.publish()
+            pipe.publish()
         else:
             env.step_raw(act_p[r])
             if with_gather:
                 env.gather_observations()
+
+    def steps_of(steps, with_gather):
+        if with_gather and native_x:
+            pipe.run(env, act_p, steps)
+            kk[0] += steps
+        else:
+            for k in range(steps):
+                one_step(k, with_gather)
 
     def run(steps, with_gather, graph=None):
         """exactly `steps` env-steps between barrier + synchronize; returns the max-over-ranks wall
@@ -436,8 +444,7 @@ def main(argv=None):
             for g_ in graph:
                 g_.replay()
         else:
-            for k in range(steps):
-                one_step(k, with_gather)
+            steps_of(steps, with_gather)
         if with_gather and pipe is not None:
             pipe.drain()
         e1.record(stream)
@@ -446,8 +453,7 @@ def main(argv=None):
             dist.barrier()
         return max_over_ranks(time.perf_counter() - t0), e0.elapsed_time(e1)
 
-    for k in range(args.warmup):
-        one_step(k, gather)
+    steps_of(args.warmup, gather)
     if pipe is not None:
         pipe.drain()
     torch.cuda.synchronize()
@@ -473,6 +479,28 @@ def main(argv=None):
     # ---- timed region: exactly K steps between barrier + synchronize, max over ranks ----
     elapsed, ev_ms = run(args.steps, gather, graph)
     kern_ms = ev_ms / args.steps
+    rows_check = None
+    if gather and delta and pipe is not None:
+        # rows on request: the whole [global_envs, D] slab of the last timed step, materialised from
+        # the gathered buffers and the actions, must equal a full all-gather of that step's rows
+        from cf2sim.dist import gather_rows
+        kl = pipe.k - 1
+        a3 = [acts_g[max(kl - d, 0) % ring] for d in range(3)]
+        full = gather_rows(pipe.obs[kl % pipe.depth], sizes=shards)
+        rows = pipe.rows(*a3)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(rows, full))
+        r0_, r1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0_.record(stream)
+        for _ in range(10):
+            pipe.rows(*a3, out=rows)
+        r1_.record(stream)
+        torch.cuda.synchronize()
+        rows_check = {"step": kl, "rows": global_envs, "equal_to_full_gather": same,
+                      "us_all_rows": r0_.elapsed_time(r1_) * 1e3 / 10}
+        if not same:
+            raise SystemExit("bench.py: the exchanged rows differ from the full all-gather")
+        del full, rows
     if gather:
         # the timed region also holds the all-gathers: time the step kernel alone here
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
@@ -665,45 +693,58 @@ def main(argv=None):
     exchange = None
     if world == 1 and args.exchange_probe and n == METRIC_GLOBAL_ENVS and delta_supported(env.cfg):
         # the delta obs exchange of the 8-GPU shape on one GPU: 8 shards of this step's real rows
-        # and done flags packed as the ranks would (cf2_obs_pack, 32 768 rows each), then every
-        # rank's rebuild of all 262 144 rows (cf2_obs_unpack), timed with HIP events on this stream
-        from cf2sim.dist import default_cap, pack_obs, packed_words, unpack_obs
+        # and done flags packed as the ranks would (cf2_obs_pack, 32 768 rows each), then a rank's
+        # per-step consume of all 262 144 envs (cf2_obs_consume: the ages) and, on request, the
+        # materialisation of all 262 144 rows (cf2_obs_rows), timed with HIP events on this stream
+        from cf2sim.dist import consume_obs, default_cap, obs_rows, pack_obs, packed_words
         W8, n8, ol = 8, n // 8, env.obs_dim // 2 - 4
         cap = default_cap(n8)
         words = packed_words(n8, ol, cap)
         send = torch.zeros(W8 * words, dtype=torch.int32, device=dev)
+        prev_pk = torch.zeros(W8 * words, dtype=torch.int32, device=dev)
         rows, dn = env.obs.clone(), env.done.clone()
-        prev = rows.clone()
-        cur = torch.empty_like(rows)
+        out_rows = torch.empty_like(rows)
         age = torch.full((n,), 3, dtype=torch.int16, device=dev)          # uint16 storage, as the exchange keeps it
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         reps = 20
+
+        scr = torch.zeros(W8 + 1, 288, dtype=torch.int32, device=dev)
+
+        def pack_all(dst):
+            for r in range(W8):
+                # each pack zeroes the side-slot counters of the next one, as the ranks' packs do
+                pack_obs(rows[r * n8:(r + 1) * n8], dn[r * n8:(r + 1) * n8], cap, out=dst[r * words:(r + 1) * words],
+                         scratch=scr[r], next_scratch=scr[r + 1])
+            scr[0].zero_()
+        pack_all(prev_pk)
         torch.cuda.synchronize()
         ev[0].record(stream)
         for _ in range(reps):
-            for r in range(W8):
-                # each pack zeroes the next buffer's count word (clear_next), as the ranks' packs do
-                nx = (r + 1) % W8
-                pack_obs(rows[r * n8:(r + 1) * n8], dn[r * n8:(r + 1) * n8], cap, out=send[r * words:(r + 1) * words],
-                         clear_next=send[nx * words:nx * words + 1])
+            pack_all(send)
         ev[1].record(stream)
         for _ in range(reps):
-            unpack_obs(send, W8, n8, ol, cap, acts_g[1], acts_g[0], age, prev, cur)
+            consume_obs(send, W8, n8, ol, cap, age)
         ev[2].record(stream)
+        for _ in range(reps):
+            obs_rows(send, cap, prev_pk, cap, W8, n8, ol, age, acts_g[2], acts_g[1], acts_g[0], out=out_rows)
+        ev[3].record(stream)
         torch.cuda.synchronize()
         pack_us = ev[0].elapsed_time(ev[1]) * 1e3 / (reps * W8)
-        unpack_us = ev[1].elapsed_time(ev[2]) * 1e3 / reps
+        consume_us = ev[1].elapsed_time(ev[2]) * 1e3 / reps
+        rows_us = ev[2].elapsed_time(ev[3]) * 1e3 / reps
         full_b, delta_b = n8 * env.obs_dim * 4, words * 4
+        rows_b = n * (4 * env.obs_dim + 4 * ol + 12 * 4 + 2) + W8 * delta_b
         exchange = {"shape": f"8 ranks x {n8} envs", "cap_per_rank": cap, "bytes_per_rank_per_step": delta_b,
                     "full_rows_bytes_per_rank_per_step": full_b, "reduction": full_b / delta_b,
                     "link_bound_us_8gpu": delta_b / 153e9 * 1e6, "link_bound_us_8gpu_full_rows": full_b / 153e9 * 1e6,
-                    "pack_us_per_rank": pack_us, "unpack_us_all_rows": unpack_us,
-                    "unpack_algorithmic_bytes": n * (4 * env.obs_dim + 4 * (ol + 4) + 4 * ol + 32 + 2),
+                    "pack_us_per_rank": pack_us, "consume_us_all_envs": consume_us,
+                    "consume_algorithmic_bytes": n * 4 + W8 * ((n8 + 31) // 32) * 4,
+                    "rows_on_request_us_all_rows": rows_us, "rows_algorithmic_bytes": rows_b,
+                    "rows_GBs": rows_b / (rows_us * 1e-6) / 1e9,
                     "note": "link bound: each GPU receives one packed buffer from each of 7 peers over its 7 xGMI links "
-                            "(~153 GB/s each) in parallel; the unpack (every rank rebuilds all rows from the previous "
-                            "slab) runs on the exchange's side stream, beside the next env-step"}
-        exchange["unpack_GBs"] = exchange["unpack_algorithmic_bytes"] / (unpack_us * 1e-6) / 1e9
-        del send, rows, prev, cur
+                            "(~153 GB/s each) in parallel; per step a receiver only advances the envs' ages (consume); "
+                            "rows are materialised on request"}
+        del send, prev_pk, rows, out_rows
 
     bytes_per = bytes_per_env_step(env)
     out_of_cache = None
@@ -774,8 +815,10 @@ def main(argv=None):
                        "overflows": pipe.overflows() if pipe is not None else 0,
                        "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
                        "rx_frac_of_xgmi": rx / (elapsed / args.steps) / 1e9 / XGMI_PEAK_GBS,
-                       "launch": "eager per-step launches",
-                       "exchange": pipe.exchange if pipe is not None else "padded all_gather"}
+                       "launch": (f"env-steps back to back with the pack fused in, one all-gather + consume per "
+                                  f"batch of {pipe.unit} (cf2_xchg_run)" if native_x else "eager per-step launches"),
+                       "exchange": pipe.exchange if pipe is not None else "padded all_gather",
+                       "rows_on_request": rows_check}
         if pipe is not None:
             pipe.drain()
             pipe.close()

@@ -27,9 +27,10 @@ EXPORTED_SYMBOLS = (
     "cf2_set_ground_effect",
     "cf2_rollout", "cf2_get_state", "cf2_set_state", "cf2_hj_disturbance",
     "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_policy_pack", "cf2_policy_forward", "cf2_value_forward_masked", "cf2_gae",
-    "cf2_hbm_probe", "cf2_obs_packed_words", "cf2_obs_pack", "cf2_obs_unpack",
-    "cf2_xchg_bind", "cf2_xchg_unique_id", "cf2_xchg_create", "cf2_xchg_destroy", "cf2_xchg_step", "cf2_xchg_wait",
-    "cf2_xchg_register", "cf2_xchg_env_step", "cf2_xchg_pred_sync",
+    "cf2_hbm_probe", "cf2_step_packed", "cf2_obs_packed_words", "cf2_xchg_send_words", "cf2_obs_pack", "cf2_obs_consume", "cf2_obs_rows",
+    "cf2_xchg_bind", "cf2_xchg_unique_id", "cf2_xchg_create", "cf2_xchg_destroy", "cf2_xchg_register",
+    "cf2_xchg_publish", "cf2_xchg_wait_free", "cf2_xchg_wait", "cf2_xchg_env_step", "cf2_xchg_run",
+    "cf2_xchg_recv_words",
 )
 
 
@@ -96,21 +97,28 @@ def load() -> ctypes.CDLL:
     lib.cf2_hbm_probe.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
     lib.cf2_obs_packed_words.restype = ctypes.c_size_t
     lib.cf2_obs_packed_words.argtypes = [u32, u32, u32]
-    lib.cf2_obs_pack.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp]
-    lib.cf2_obs_unpack.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp]
+    lib.cf2_obs_pack.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
+    lib.cf2_step_packed.argtypes = [vp] * 11 + [u32, vp]
+    lib.cf2_xchg_send_words.restype = ctypes.c_size_t
+    lib.cf2_xchg_send_words.argtypes = [u32, u32, u32, u32]
+    lib.cf2_xchg_recv_words.restype = ctypes.c_size_t
+    lib.cf2_xchg_recv_words.argtypes = [u32, u32, u32, u32, u32]
+    lib.cf2_obs_consume.argtypes = [vp, u32, u32, u32, u32, vp, vp, u32, vp, vp, vp]
+    lib.cf2_obs_rows.argtypes = [vp, u32, u32, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp, u32, u32, vp, vp]
     lib.cf2_xchg_bind.argtypes = [ctypes.c_char_p]
     lib.cf2_xchg_unique_id.argtypes = [vp, ctypes.c_size_t]
     lib.cf2_xchg_create.argtypes = [vp, ctypes.c_size_t, u32, u32, u32, P(vp)]
     lib.cf2_xchg_destroy.argtypes = [vp]
-    lib.cf2_xchg_step.argtypes = [vp, u32, vp, vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp,
-                                  vp, vp]
-    lib.cf2_xchg_wait.argtypes = [vp, u32, vp]
-    lib.cf2_xchg_register.argtypes = [vp, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, u32, u32, vp]
-    lib.cf2_xchg_pred_sync.argtypes = [vp, ctypes.c_uint64]
-    lib.cf2_xchg_env_step.argtypes = [vp, vp, ctypes.c_uint64, u32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.cf2_xchg_register.argtypes = [vp, u32, u32, u32, u32, vp, vp, vp, vp, vp, vp, vp, u32]
+    lib.cf2_xchg_publish.argtypes = [vp, ctypes.c_uint64, u32, u32, vp]
+    lib.cf2_xchg_wait_free.argtypes = [vp, u32, vp]
+    lib.cf2_xchg_wait.argtypes = [vp, vp]
+    lib.cf2_xchg_env_step.argtypes = [vp, vp, ctypes.c_uint64, u32, u32, vp, vp, vp, vp, vp, vp]
+    lib.cf2_xchg_run.argtypes = [vp, vp, ctypes.c_uint64, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
-                        "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_obs_packed_words"):
+                        "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_obs_packed_words",
+                        "cf2_xchg_send_words", "cf2_xchg_recv_words"):
             getattr(lib, name).restype = ctypes.c_int
     if lib.cf2_config_sizeof() != ctypes.sizeof(CF2Config):
         raise CF2Error(f"cf2_config size mismatch: C {lib.cf2_config_sizeof()} vs Python {ctypes.sizeof(CF2Config)}")

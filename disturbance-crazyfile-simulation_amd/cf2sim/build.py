@@ -11,7 +11,7 @@ SRC_DIR = os.path.abspath(os.path.join(PKG_DIR, "..", "csrc"))
 INC_DIR = os.path.abspath(os.path.join(PKG_DIR, "..", "..", "include"))
 LIB = os.path.join(PKG_DIR, "libcf2sim.so")
 SOURCES = ["cf2sim_kernels.hip", "cf2sim_policy.hip", "cf2sim_util.hip", "cf2sim_exchange.hip", "cf2sim_api.cpp"]
-HEADERS = ["cf2sim_internal.h", "cf2sim_rng.h", "cf2sim_policy.h"]
+HEADERS = ["cf2sim_internal.h", "cf2sim_rng.h", "cf2sim_policy.h", "cf2sim_pack.h"]
 # The env-step is fp32 throughout.  FMA contraction, approximate division/sqrt (v_rcp / v_sqrt,
 # ~1 ulp) and the hardware sin/cos/log are allowed: the kernel is compared against the fp32 and
 # fp64 CPU restatements with stated tolerances (tests/test_gpu_parity.py), not bitwise.

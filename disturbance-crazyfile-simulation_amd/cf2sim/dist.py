@@ -14,6 +14,7 @@ stays out of scope.
 from __future__ import annotations
 
 import os
+import weakref as _weakref
 
 
 def launch_plan(world: int, port: int, script: str, argv: list[str], base_env: dict | None = None,
@@ -70,10 +71,16 @@ def run_ranks(plan, timeout: float | None = None) -> int:
 
 
 # ---- delta observation exchange (csrc/cf2sim_exchange.hip has the protocol; cf2_obs_pack /
-# cf2_obs_unpack run it on GPU tensors, the torch-op versions below on CPU tensors for the gloo
-# rehearsal of the multi-rank path; both produce the same rows bit for bit) ----
+# cf2_obs_consume / cf2_obs_rows run it on GPU tensors, the torch-op versions below on CPU tensors
+# for the gloo rehearsal of the multi-rank path; both produce the same rows bit for bit) ----
 
-PACK_BLOCK = 256      # envs per pack block: one block-table word each (the block's first side slot)
+PACK_BLOCK = 64       # envs per pack block: one block-table word each (the side slot of the block's first reset)
+PACK_DROPPED = -1     # block-table word (int32 view of 0xFFFFFFFF): the block's resets got no side slot
+PACK_SCRATCH_WORDS = 288   # side-slot counters of a pack (csrc/cf2sim_pack.h), past the largest packed buffer
+ZERO_AHEAD = 8        # a consume zeroes the look-ahead rows of the 8 steps after its own
+NO_WATCH = 0xFFFFFFFF
+PRED_BATCH = 4        # eager exchange: the time-out count ring is copied to the host every 4 env-steps
+RUN_UNIT = 16         # native exchange: env-steps per batch of PipelinedObsGather.run (one all-gather each)
 
 
 def _side(n: int, ol: int) -> int:
@@ -89,7 +96,8 @@ def packed_words(n: int, ol: int, cap: int) -> int:
 def default_cap(n: int) -> int:
     """Side-slab capacity: 7.5 % of the shard.  The bench workload ends 4.1 % of its episodes per
     env-step in steady state and 5.7 % at the synchronised-start peak (profiles/r02_reset_rate.json);
-    a step that exceeds it marks the rows it could not send (NaN) and counts an overflow."""
+    a step that exceeds it NaNs the o_0 / action parts of the reset rows of the 64-env blocks that
+    found no room and counts those blocks as overflows."""
     return min(int(n), max(64, (3 * n + 39) // 40))
 
 
@@ -112,9 +120,11 @@ def _need(ok: bool, what: str):
         raise ValueError(f"delta exchange: {what}")
 
 
-def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
+def pack_obs(obs, reset, cap: int, out=None, scratch=None, next_scratch=None):
     """One rank's packed buffer (int32 [packed_words]) from its step's obs rows [n, OD] and
-    auto-reset flags [n] (uint8 or bool)."""
+    auto-reset flags [n] (uint8 or bool).  GPU: scratch = this pack's side-slot counters
+    (PACK_SCRATCH_WORDS int32, zeroed; a fresh zeroed one if None), next_scratch = the counters the
+    next pack uses (zeroed by this one; or None).  CPU: slots are handed out in block order."""
     import numpy as np
     import torch
     n, od = obs.shape
@@ -125,16 +135,21 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
     if obs.is_cuda:
         from . import _native
         lib = _native.load()
+        if scratch is None:
+            scratch = torch.zeros(PACK_SCRATCH_WORDS, dtype=torch.int32, device=obs.device)
         # the kernel indexes by these sizes: check them on the host before the launch
         _need(obs.is_contiguous() and obs.dtype == torch.float32, "obs must be contiguous float32 [n, OD]")
         _need(reset.numel() >= n and reset.is_cuda, "reset needs n flags on the GPU")
         _need(out.dtype == torch.int32 and out.is_contiguous() and out.numel() >= words and out.is_cuda,
               f"out needs {words} int32 words on the GPU")
-        _need(clear_next is None or (clear_next.is_cuda and clear_next.numel() >= 1), "clear_next needs 1 word")
+        for name, t in (("scratch", scratch), ("next_scratch", next_scratch)):
+            _need(t is None or (t.is_cuda and t.dtype == torch.int32 and t.is_contiguous()
+                                and t.numel() >= PACK_SCRATCH_WORDS), f"{name} needs {PACK_SCRATCH_WORDS} int32")
+        _need(next_scratch is None or next_scratch.data_ptr() != scratch.data_ptr(), "next_scratch must not be scratch")
         r8 = reset if reset.dtype == torch.uint8 else reset.to(torch.uint8)
         _native.check(lib.cf2_obs_pack(obs.data_ptr(), r8.contiguous().data_ptr(), n, ol, cap, out.data_ptr(),
-                                       _native.ptr(clear_next), torch.cuda.current_stream(obs.device).cuda_stream),
-                      "cf2_obs_pack")
+                                       scratch.data_ptr(), _native.ptr(next_scratch),
+                                       torch.cuda.current_stream(obs.device).cuda_stream), "cf2_obs_pack")
         return out
     r = reset.bool().cpu()
     out.zero_()
@@ -145,28 +160,156 @@ def pack_obs(obs, reset, cap: int, out=None, clear_next=None):
     pb = np.packbits(r.numpy(), bitorder="little")
     bits[:pb.size] = pb
     out[4 + n * ol:4 + n * ol + nb] = torch.from_numpy(bits.view(np.int32))
-    idx = torch.nonzero(r).flatten()
-    out[0], out[1], out[2], out[3] = int(idx.numel()), n, ol, cap
-    # block table: the first side slot of each pack block's resets (blocks in env order here; the
-    # GPU kernel hands slots out per block in any order, so only the slots differ, not the rows)
+    out[1], out[2], out[3] = n, ol, cap
+    # block table: each 64-env block's resets take consecutive slots (blocks in order here; the GPU
+    # hands slots out per XCD region, so only the slots differ, not the rows); a block that does not
+    # fit is dropped
     nblk = (n + PACK_BLOCK - 1) // PACK_BLOCK
-    per_blk = torch.zeros(nblk, dtype=torch.int64)
-    per_blk.index_add_(0, idx // PACK_BLOCK, torch.ones_like(idx))
-    out[4 + n * ol + nb:4 + n * ol + nb + nblk] = (torch.cumsum(per_blk, 0) - per_blk).to(torch.int32)
-    side = _side(n, ol)
-    for s, i in enumerate(idx[:cap].tolist()):
-        e = side + s * (ol + 5)
-        out[e] = i
-        f[e + 1:e + 1 + ol + 4] = obs[i, :ol + 4]
-    if clear_next is not None:
-        clear_next.zero_()
+    cnt = torch.zeros(nblk, dtype=torch.int64)
+    idx = torch.nonzero(r).flatten()
+    cnt.index_add_(0, idx // PACK_BLOCK, torch.ones_like(idx))
+    btab = torch.zeros(nblk, dtype=torch.int64)
+    side, used = _side(n, ol), 0
+    for b in torch.nonzero(cnt).flatten().tolist():
+        c = int(cnt[b])
+        if used + c > cap:
+            btab[b] = PACK_DROPPED
+            continue
+        btab[b] = used
+        for s_, i in enumerate(idx[(idx // PACK_BLOCK) == b].tolist()):
+            e = side + (used + s_) * (ol + 5)
+            out[e] = i
+            f[e + 1:e + 1 + ol + 4] = obs[i, :ol + 4]
+        used += c
+    out[4 + n * ol + nb:4 + n * ol + nb + nblk] = btab.to(torch.int32)
     return out
 
 
-NO_WATCH = 0xFFFFFFFF
-PRED_BATCH = 4          # RCCL delta path: time-out counts copied to the host every 4 steps (< lookahead)
+def _slots(pk, n: int, ol: int, rs):
+    """Side slot of every env (valid where rs; PACK_DROPPED where its block got none) from the block
+    table and the bitmap (cf2sim_pack.h pack_slot)."""
+    import torch
+    nb = (n + 31) // 32
+    nblk = (n + PACK_BLOCK - 1) // PACK_BLOCK
+    btab = pk[4 + n * ol + nb:4 + n * ol + nb + nblk].to(torch.int64)
+    blk = torch.arange(n) // PACK_BLOCK
+    c = torch.cumsum(rs.to(torch.int64), 0)
+    start = torch.zeros(nblk, dtype=torch.int64)
+    start[1:] = c[torch.arange(1, nblk) * PACK_BLOCK - 1]
+    within = c - rs.to(torch.int64) - start[blk]
+    first = btab[blk]
+    return torch.where(first == PACK_DROPPED, torch.full_like(first, PACK_DROPPED), first + within)
 
-_LIVE_XCHG = set()      # native exchanges not closed yet: destroyed at exit, before the runtime unloads
+
+def consume_obs(recv, world: int, n: int, ol: int, cap: int, age, overflow=None, watch_age: int = NO_WATCH,
+                pred=None, pred_next=None):
+    """A receiver's per-step work (cf2_obs_consume): advance every env's age (steps since its reset;
+    int16 storage of a uint16 on GPUs, int32 on the CPU, [world n]) from the gathered packed buffers
+    (int32 [world * packed_words(n, ol, cap)]); count per rank into pred ([world]) the envs whose new age is watch_age (they time out L
+    steps later unless they crash first); zero pred_next; count the 64-env blocks whose resets got
+    no side slot into overflow."""
+    import torch
+    if recv.is_cuda:
+        from . import _native
+        lib = _native.load()
+        N = world * n
+        _need(recv.dtype == torch.int32 and recv.is_contiguous() and recv.numel() >= world * packed_words(n, ol, cap),
+              "recv needs world * packed_words int32 words")
+        _need(age.dtype == torch.int16 and age.is_contiguous() and age.numel() >= N and age.is_cuda,
+              "age must be int16 (uint16 storage) [world * n] on the GPU")
+        for name, t, k in (("overflow", overflow, 1), ("pred", pred, world), ("pred_next", pred_next, world)):
+            _need(t is None or (t.is_cuda and t.dtype == torch.int32 and t.numel() >= k), f"{name} needs {k} int32")
+        _need((pred is None) == (pred_next is None), "pred and pred_next go together")
+        _native.check(lib.cf2_obs_consume(recv.data_ptr(), world, n, ol, cap, age.data_ptr(), _native.ptr(overflow),
+                                          int(watch_age) & 0xFFFFFFFF, _native.ptr(pred), _native.ptr(pred_next),
+                                          torch.cuda.current_stream(recv.device).cuda_stream), "cf2_obs_consume")
+        return age
+    words = packed_words(n, ol, cap)
+    rv = recv[:world * words].reshape(world, words)
+    if pred_next is not None:
+        pred_next.zero_()
+    for r in range(world):
+        pk = rv[r]
+        rs = _bits_to_mask(pk[4 + n * ol:4 + n * ol + (n + 31) // 32], n)
+        sl = slice(r * n, (r + 1) * n)
+        a = torch.clamp(age[sl].to(torch.int64) + 1, max=0xFFFF)
+        new = torch.where(rs, torch.zeros_like(a), a)
+        age[sl] = new.to(age.dtype)
+        if pred is not None:
+            pred[r] += int((new == watch_age).sum())
+        if overflow is not None:
+            nb = (n + 31) // 32
+            btab = pk[4 + n * ol + nb:4 + n * ol + nb + (n + PACK_BLOCK - 1) // PACK_BLOCK]
+            overflow += int((btab == PACK_DROPPED).sum())
+    return age
+
+
+def obs_rows(recv, cap: int, recv_prev, cap_prev: int, world: int, n: int, ol: int, age, act, act_prev, act_prev2,
+             out=None, row0: int = 0, nrows: int | None = None, stride: int | None = None,
+             stride_prev: int | None = None):
+    """Rows [row0, row0 + nrows) of step k's global observation slab ([nrows, 2 ol + 8]) from the
+    gathered packed buffers of step k (recv, capacity cap) and k - 1 (recv_prev, cap_prev), the ages
+    after step k's consume_obs and the actions of steps k, k - 1, k - 2 ([world n, 4]; the history
+    rules of csrc/cf2sim_exchange.hip).  The reset rows of a pack block that got no side slot have NaN
+    in their o_0 / action parts.  Rank r's packed buffer starts r * stride words into recv (default:
+    packed_words(n, ol, cap), one step's all-gather), likewise for recv_prev."""
+    import torch
+    N, od = world * n, 2 * (ol + 4)
+    nrows = N - row0 if nrows is None else int(nrows)
+    _need(0 <= row0 and row0 + nrows <= N, "rows out of range")
+    if out is None:
+        out = torch.empty(nrows, od, dtype=torch.float32, device=recv.device)
+    words, wp = packed_words(n, ol, cap), packed_words(n, ol, cap_prev)
+    stride = words if stride is None else int(stride)
+    stride_prev = wp if stride_prev is None else int(stride_prev)
+    _need(stride >= words and stride_prev >= wp, "rank strides below the packed buffer size")
+    if recv.is_cuda:
+        from . import _native
+        lib = _native.load()
+        _need(recv.dtype == torch.int32 and recv.is_contiguous() and recv.numel() >= (world - 1) * stride + words,
+              "recv needs (world - 1) * stride + packed_words(cap) int32 words")
+        _need(recv_prev.dtype == torch.int32 and recv_prev.is_contiguous() and recv_prev.is_cuda and
+              recv_prev.numel() >= (world - 1) * stride_prev + wp, "recv_prev too short")
+        _need(age.dtype == torch.int16 and age.is_contiguous() and age.numel() >= N and age.is_cuda,
+              "age must be int16 (uint16 storage) [world * n] on the GPU")
+        for name, t in (("act", act), ("act_prev", act_prev), ("act_prev2", act_prev2)):
+            _need(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= N * 4,
+                  f"{name} must be contiguous float32 [world * n, 4] on the GPU")
+        _need(out.is_cuda and out.dtype == torch.float32 and out.is_contiguous() and out.numel() >= nrows * od,
+              f"out must be contiguous float32 [{nrows}, {od}] on the GPU")
+        _native.check(lib.cf2_obs_rows(recv.data_ptr(), cap, stride, recv_prev.data_ptr(), cap_prev, stride_prev, world,
+                                       n, ol, age.data_ptr(), act.data_ptr(), act_prev.data_ptr(), act_prev2.data_ptr(),
+                                       row0, nrows, out.data_ptr(), torch.cuda.current_stream(recv.device).cuda_stream),
+                      "cf2_obs_rows")
+        return out
+    rv = [recv[r * stride:r * stride + words] for r in range(world)]
+    pv = [recv_prev[r * stride_prev:r * stride_prev + wp] for r in range(world)]
+    nan = float("nan")
+    full = torch.empty(N, od)
+    for r in range(row0 // n, (row0 + nrows + n - 1) // n):
+        pk, f = rv[r], rv[r].view(torch.float32)
+        rs = _bits_to_mask(pk[4 + n * ol:4 + n * ol + (n + 31) // 32], n)
+        sl = slice(r * n, (r + 1) * n)
+        o = full[sl]
+        a = age[sl].to(torch.int64) & 0xFFFF
+        o[:, :ol] = pv[r].view(torch.float32)[4:4 + n * ol].view(n, ol)
+        o[:, ol:ol + 4] = torch.where((a >= 3)[:, None], act_prev2[sl], act[sl])
+        o[:, ol + 4:2 * ol + 4] = f[4:4 + n * ol].view(n, ol)
+        o[:, 2 * ol + 4:] = torch.where((a == 1)[:, None], act[sl], act_prev[sl])
+        sl_ = _slots(pk, n, ol, rs)
+        drop = rs & (sl_ == PACK_DROPPED)
+        o[drop, :ol + 4] = nan
+        o[drop, 2 * ol + 4:] = nan
+        side = _side(n, ol)
+        for i in torch.nonzero(rs & ~drop).flatten().tolist():
+            e = side + int(sl_[i]) * (ol + 5)
+            o[i, :ol + 4] = f[e + 1:e + 1 + ol + 4]
+            o[i, 2 * ol + 4:] = f[e + 1 + ol:e + 1 + ol + 4]
+    out[:nrows] = full[row0:row0 + nrows]
+    return out
+
+
+_LIVE_XCHG = _weakref.WeakSet()     # native exchanges not closed yet: destroyed at exit, before the runtime unloads
 
 
 def _close_live_exchanges():
@@ -174,119 +317,82 @@ def _close_live_exchanges():
         g.close()
 
 
+def _agree(ok: bool, group, device) -> bool:
+    """True on every rank iff ok on every rank (all_reduce MIN over the group)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
 def _native_exchange(lib, group, world: int, depth: int, device):
-    """The RCCL communicator of cf2_xchg_* for this group (collective: every rank calls it): rank
-    0's id broadcast over the process group; PyTorch's own RCCL instance where it ships one."""
+    """The RCCL communicator of cf2_xchg_* for this group, created on `device` (collective: every
+    rank calls it).  Every stage ends with an agreement over the process group, so a failure on one
+    rank makes every rank fall back together (returns None) instead of leaving the others blocked
+    in the id broadcast or in the communicator's rendezvous.  PyTorch's own RCCL instance where it
+    ships one; rank 0's id broadcast over the process group."""
     import ctypes
     import torch
     import torch.distributed as dist
     from . import _native
     path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-    _native.check(lib.cf2_xchg_bind(path.encode() if os.path.exists(path) else None), "cf2_xchg_bind")
-    idb = (ctypes.c_uint8 * 128)()
+    ok = lib.cf2_xchg_bind(path.encode() if os.path.exists(path) else None) == 0
     rank = dist.get_rank(group)
-    if rank == 0:
-        _native.check(lib.cf2_xchg_unique_id(idb, 128), "cf2_xchg_unique_id")
+    idb = (ctypes.c_uint8 * 128)()
+    if ok and rank == 0:
+        ok = lib.cf2_xchg_unique_id(idb, 128) == 0
+    if not _agree(ok, group, device):
+        return None
     t = torch.tensor(list(bytes(idb)), dtype=torch.uint8, device=device)
     dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
     idb = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(t.cpu().tolist()))
     h = ctypes.c_void_p()
-    _native.check(lib.cf2_xchg_create(idb, 128, world, rank, depth, ctypes.byref(h)), "cf2_xchg_create")
+    with torch.cuda.device(device):
+        st = lib.cf2_xchg_create(idb, 128, world, rank, depth, ctypes.byref(h))
+    if not _agree(st == 0, group, device):
+        if st == 0:
+            _native.check(lib.cf2_xchg_destroy(h), "cf2_xchg_destroy")
+        return None
     return h
-
-
-def unpack_obs(recv, world: int, n: int, ol: int, cap: int, act, act_prev, age, slab_prev, slab, overflow=None,
-               watch_age: int = NO_WATCH, pred=None, pred_next=None):
-    """Rebuild every rank's rows [world n, OD] into `slab` from the gathered packed buffers
-    (int32 [world * packed_words(n, ol, cap)]), the previous slab, the step's actions and the
-    previous step's (act, act_prev: [world n, 4]); age (steps since reset; int16 storage of a
-    uint16 on GPUs, int32 on the CPU, [world n]) is updated in place.  Envs whose new age equals
-    watch_age are counted per rank into pred ([world]); pred_next is zeroed."""
-    import torch
-    if recv.is_cuda:
-        from . import _native
-        lib = _native.load()
-        # the kernels index by these sizes: check them on the host before the launch
-        N, od = world * n, 2 * (ol + 4)
-        _need(recv.dtype == torch.int32 and recv.is_contiguous() and recv.numel() >= world * packed_words(n, ol, cap),
-              "recv needs world * packed_words int32 words")
-        _need(age.dtype == torch.int16 and age.is_contiguous() and age.numel() >= N and age.is_cuda,
-              "age must be int16 (uint16 storage) [world * n] on the GPU")
-        for name, t, cols in (("act", act, 4), ("act_prev", act_prev, 4), ("slab_prev", slab_prev, od), ("slab", slab, od)):
-            _need(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= N * cols,
-                  f"{name} must be contiguous float32 [world * n, {cols}] on the GPU")
-        for name, t, k in (("overflow", overflow, 1), ("pred", pred, world), ("pred_next", pred_next, world)):
-            _need(t is None or (t.is_cuda and t.dtype == torch.int32 and t.numel() >= k), f"{name} needs {k} int32")
-        _native.check(lib.cf2_obs_unpack(recv.data_ptr(), world, n, ol, cap, act.data_ptr(), act_prev.data_ptr(),
-                                         age.data_ptr(), slab_prev.data_ptr(), slab.data_ptr(), _native.ptr(overflow),
-                                         int(watch_age) & 0xFFFFFFFF, _native.ptr(pred), _native.ptr(pred_next),
-                                         torch.cuda.current_stream(recv.device).cuda_stream), "cf2_obs_unpack")
-        return slab
-    words = packed_words(n, ol, cap)
-    rv = recv[:world * words].reshape(world, words)
-    nan = float("nan")
-    if pred_next is not None:
-        pred_next.zero_()
-    for r in range(world):
-        pk = rv[r]
-        f = pk.view(torch.float32)
-        ok = f[4:4 + n * ol].view(n, ol)
-        rs = _bits_to_mask(pk[4 + n * ol:4 + n * ol + (n + 31) // 32], n)
-        sl = slice(r * n, (r + 1) * n)
-        prev, out = slab_prev[sl], slab[sl]
-        a = torch.clamp(age[sl].to(torch.int64) + 1, max=0xFFFF)
-        out[:, :ol] = prev[:, ol + 4:2 * ol + 4]
-        out[:, ol:ol + 4] = torch.where((a >= 3)[:, None], prev[:, 2 * ol + 4:], act[sl])
-        out[:, ol + 4:2 * ol + 4] = ok
-        out[:, 2 * ol + 4:] = torch.where((a == 1)[:, None], act[sl], act_prev[sl])
-        cnt = int(pk[0])
-        if cnt > cap:
-            out[rs, :ol + 4] = nan
-            out[rs, 2 * ol + 4:] = nan
-            if overflow is not None:
-                overflow += 1
-        else:
-            side = _side(n, ol)
-            for s in range(cnt):
-                e = side + s * (ol + 5)
-                i = int(pk[e])
-                out[i, :ol + 4] = f[e + 1:e + 1 + ol + 4]
-                out[i, 2 * ol + 4:] = f[e + 1 + ol:e + 1 + ol + 4]
-        new = torch.where(rs, torch.zeros_like(a), a)
-        age[sl] = new.to(age.dtype)
-        if pred is not None:
-            pred[r] += int((new == watch_age).sum())
-    return slab
 
 
 class PipelinedObsGather:
     """Per-step all-gather of the observation slab ("RCCL all-gather over
-    xGMI only for the returned observation tensor"), overlapped with the next env-step.
+    xGMI only for the returned observation tensor"), overlapped with the next env-steps.
 
-    Env-step k writes ``buffer()`` (and, with ``delta``, ``done_buffer()``) on the compute stream;
-    ``publish()`` starts the exchange of that step on a side stream, so it runs while step k+1
-    computes.  Before step k + depth overwrites a buffer, the compute stream (not the host) waits for
-    the exchange step that read it.  ``publish()`` returns the [world * n, D] slab of step k; it is
-    complete once ``drain()`` returned (or after ``ready()`` on any stream) and stays valid until
-    the publish of step k + 2.  On gloo (the CPU rehearsal of the multi-rank path) the exchange
+    Env-step k writes ``buffer()`` (and, with ``delta``, ``done_buffer()``) on the current stream;
+    ``publish()`` starts the exchange of that step on a side stream, so it runs while step k + 1
+    computes.  Before an env-step overwrites a buffer, the current stream (not the host) waits for
+    the exchange that read it.  On gloo (the CPU rehearsal of the multi-rank path) the exchange
     stages through the host and completes inside ``publish()``.
 
-    delta=False: every step all-gathers the whole [n, D] slab of every rank.
+    delta=False: every step all-gathers the whole [n, D] slab of every rank; ``publish()`` returns
+    the [world * n, D] slab (complete after ``drain()``; valid until the publish of step k + depth).
+
     delta=True: every step all-gathers only what a receiver cannot rebuild (cf2_obs_pack: o_k of
-    every env, a reset bitmap, the reset rows' o_0 and action part for up to ``cap`` resets) and
-    every rank rebuilds the full slab from its previous one and the actions (cf2_obs_unpack): the
-    actions of step k and k - 1 for every env ([world * n, 4], the policy's own outputs) are
-    arguments of ``publish``.  ``start(obs)`` gathers the observations of a reset of every env in
-    full first.  The side capacity of a step is ``cap`` (the crash budget, default_cap) plus the
-    time-outs that step can have at most (max_steps: the env's TimeLimit; the receivers count the
-    envs that reach max_steps - lookahead, every rank the same, and the host reads the count
-    ``lookahead`` steps later), so synchronised time-outs never overflow.  Shards must be equal
-    (ValueError otherwise)."""
+    every env, a reset bitmap, the reset rows' o_0 and action part for up to the step's capacity),
+    and every receiver only advances the envs' ages (cf2_obs_consume): nothing is rebuilt per step.
+    ``rows(act, act_prev, act_prev2)`` materialises rows of the latest published step on request
+    (cf2_obs_rows) from the gathered buffers of that step and the one before and the actions of
+    the last three steps ([world * n, 4], the policy's own outputs); they are valid until the next
+    publish / run.  ``start(obs)`` gathers the observations of a reset of every env in full first.
+    The side capacity of step k is ``cap`` (the crash budget, default_cap) plus the time-outs the
+    step can have at most (max_steps: the env's TimeLimit; the receivers count the envs that reach
+    max_steps - lookahead, every rank the same, and the host reads the count ``lookahead`` steps
+    later), so synchronised time-outs never overflow.  Over RCCL with the native exchange,
+    ``run(env, act_ptrs, steps)`` takes ``steps`` env-steps of ``env`` in batches of ``unit``: the
+    env-steps (the pack fused in) back to back on the current stream, one all-gather and one consume
+    per batch on the exchange stream (cf2_xchg_run).  Buffers rotate over ``depth`` regions, one per
+    publish / batch.  Shards must be equal (ValueError otherwise)."""
 
     def __init__(self, n: int, obs_dim: int, device, group=None, depth: int = 2, delta: bool = False,
-                 cap: int | None = None, max_steps: int = 0, lookahead: int = 8):
+                 cap: int | None = None, max_steps: int = 0, lookahead: int | None = None, unit: int = RUN_UNIT):
         import torch
         import torch.distributed as dist
+        if not 2 <= int(depth) <= 8:
+            raise ValueError("PipelinedObsGather: depth must be 2..8 (a step's rows are built from the gathered "
+                             "buffers of that step and the one before)")
         self.group = group
         self.world = dist.get_world_size(group)
         self.nccl = dist.get_backend(group) == "nccl"
@@ -300,94 +406,96 @@ class PipelinedObsGather:
         cuda = self.device.type == "cuda"
         self.obs = [torch.empty(n, obs_dim, device=device) for _ in range(self.depth)]
         self.comm = torch.cuda.Stream(device=self.device) if (self.nccl and cuda) else None
-        # the rebuild runs on the exchange stream right after the all-gather: a third stream (the
-        # rebuild of step k beside the all-gather of step k + 1) cost more host time per step than
-        # it overlapped (the eager step is host-bound at the node shard: DESIGN.md section 6)
-        self.free = [None] * self.depth      # events: the exchange of the step that used buffer j read it
         self.k = 0
         self.started = not self.delta
         self.bytes_sent = 0                  # this rank's contribution to every gather since start()
         self.steps_sent = 0
-        if self.delta:
-            self.cap = default_cap(n) if cap is None else int(cap)
-            self.max_steps = int(max_steps)
-            self.L = int(lookahead)
-            # time-outs are predicted L steps ahead from the ages (watch age max_steps - L); a
-            # TimeLimit of L steps or fewer is sent at full capacity instead
-            self.watch = self.max_steps - self.L if self.max_steps > self.L else NO_WATCH
-            wmax = packed_words(n, self.ol, n)
-            self.done = [torch.zeros(n, dtype=torch.uint8, device=device) for _ in range(self.depth)]
-            self.send = [torch.zeros(wmax, dtype=torch.int32, device=device) for _ in range(self.depth)]
-            self.recv = [torch.empty(self.world * wmax, dtype=torch.int32, device=device) for _ in range(self.depth)]
-            self.slab = [torch.zeros(self.world * n, obs_dim, device=device) for _ in range(2)]
-            self.age = torch.zeros(self.world * n, dtype=torch.int16 if cuda else torch.int32, device=device)
-            self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
-            self.pred = torch.zeros(self.L + 1, self.world, dtype=torch.int32, device=device)
-            pin = cuda
-            self.pred_host = torch.zeros(self.L + 1, self.world, dtype=torch.int32, pin_memory=pin)
-            self.pred_ev = [None] * (self.L + 1)
-        else:
-            self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
-        # the RCCL delta path's per-step host work is kept small (the eager step is host-bound at
-        # the node shard otherwise): buffers checked once here, raw pointers, reused events, views
-        # cached per side capacity
-        self._fast = self.delta and self.comm is not None
         self._xchg = None
-        if self._fast:
+        self._lib = None
+        if not self.delta:
+            self.out = [torch.empty(self.world * n, obs_dim, device=device) for _ in range(self.depth)]
+            self._free = [None] * self.depth
+            return
+        self.unit = int(unit)
+        if not 1 <= self.unit <= 64:
+            raise ValueError("unit must be 1..64 env-steps")
+        self.L = 3 * self.unit if lookahead is None else int(lookahead)
+        # the host reads step s's count when it sizes step s + L: an eager copy is made every
+        # PRED_BATCH steps, a run() copy after each batch, and a batch's capacity needs the counts of
+        # its steps - L, which the copy of a batch at least one batch earlier than the last one in
+        # flight holds
+        if self.L < max(PRED_BATCH, 2 * self.unit + 1):
+            raise ValueError(f"lookahead must be >= max({PRED_BATCH}, 2 * unit + 1) = {max(PRED_BATCH, 2 * self.unit + 1)}")
+        self.cap = default_cap(n) if cap is None else int(cap)
+        self.max_steps = int(max_steps)
+        self.watch = self.max_steps - self.L if self.max_steps > self.L else NO_WATCH
+        # ring of per-step counts: a consume writes its steps' rows and zeroes the ZERO_AHEAD rows after
+        # them, so a host copy made after step e holds the counts of steps e - npred + ZERO_AHEAD + 1 .. e
+        self.npred = self.L + 2 * ZERO_AHEAD + 1
+        self.done = [torch.zeros(n, dtype=torch.uint8, device=device) for _ in range(self.depth)]
+        self.age = torch.zeros(self.world * n, dtype=torch.int16 if cuda else torch.int32, device=device)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+        self.pred = torch.zeros(self.npred, self.world, dtype=torch.int32, device=device)
+        npool = self.L // min(PRED_BATCH, self.unit) + 3
+        self._pred_pool = [torch.zeros(self.npred, self.world, dtype=torch.int32, pin_memory=cuda) for _ in range(npool)]
+        self._pool_i = 0
+        self._copies = []                    # (last step e covered, host buffer, event or None) in issue order
+        self._counts = {}                    # step -> max count over ranks (the look-ahead window)
+        self._where = {}                     # step -> (region, slot in its batch, batch size, capacity)
+        self._region = 0                     # publishes / batches so far (their region: % depth)
+        self._start_rows = None
+        if self.comm is not None:
             from . import _native
             self._lib = _native.load()
-            E = torch.cuda.Event
-            self._ev_fork = [E() for _ in range(self.depth)]
-            self._ev_unp = [E() for _ in range(self.depth)]
-            self._ev_pred = [E() for _ in range(self.L // PRED_BATCH + 3)]
-            self._pred_batch = []                # (step, event) of the count-ring copies in flight
-            self._views = {}
-            self._comm_h = self.comm.cuda_stream
-            self._p_send = [t.data_ptr() for t in self.send]
-            self._p_recv = [t.data_ptr() for t in self.recv]
-            self._p_obs = [t.data_ptr() for t in self.obs]
-            self._p_done = [t.data_ptr() for t in self.done]
-            self._p_slab = [t.data_ptr() for t in self.slab]
-            self._p_pred = [self.pred[r].data_ptr() for r in range(self.L + 1)]
-            # the whole step as one C call on our own RCCL communicator (cf2_xchg_step), unless
+            # the whole exchange natively on our own RCCL communicator (cf2_xchg_*), unless
             # CF2SIM_EXCHANGE=torch asks for the process group's all-gather between the launches
-            self._xchg = None
             if os.environ.get("CF2SIM_EXCHANGE", "native") == "native":
-                if self.depth > 8:
-                    raise ValueError("the native exchange keeps at most 8 buffers in flight")
-                try:
-                    self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
-                except _native.CF2Error as e:      # e.g. no RCCL library to bind: the torch path, said so
+                self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
+                if self._xchg is None:
                     import warnings
-                    warnings.warn(f"native exchange unavailable ({e}); using the process group's all-gather")
-            if self._xchg is not None:
-                self._p_age, self._p_ovf = self.age.data_ptr(), self.overflow.data_ptr()
-                import ctypes
-                arr = lambda ptrs: (ctypes.c_void_p * len(ptrs))(*ptrs)     # noqa: E731
-                self._reg = [arr(self._p_obs), arr(self._p_done), arr(self._p_send), arr(self._p_recv),
-                             arr(self._p_pred)]
-                _native.check(self._lib.cf2_xchg_register(
-                    self._xchg, self.n, self.ol, int(self.watch) & 0xFFFFFFFF, *self._reg[:4], self._p_slab[0],
-                    self._p_slab[1], self._p_age, self._p_ovf, self._reg[4], self.L + 1,
-                    self.pred_host.data_ptr() if self.watch != NO_WATCH else None, PRED_BATCH, len(self._ev_pred),
-                    self._comm_h), "cf2_xchg_register")
-                _LIVE_XCHG.add(self)
-                if len(_LIVE_XCHG) == 1:
-                    import atexit
-                    atexit.register(_close_live_exchanges)
+                    warnings.warn("native exchange unavailable on some rank; using the process group's all-gather")
+        # buffers: `depth` regions, each the packed buffers of a batch of up to kmax steps; the side-slot
+        # counters of every (region, slot) after them (csrc/cf2sim_exchange.hip, cf2_xchg_register)
+        self.kmax = self.unit if self._xchg is not None else 1
+        self.wmax = packed_words(n, self.ol, n)
+        nslot = self.depth * self.kmax
+        self.send = torch.zeros(nslot * (self.wmax + PACK_SCRATCH_WORDS), dtype=torch.int32, device=device)
+        self.recv = torch.zeros(nslot * self.world * self.wmax, dtype=torch.int32, device=device)
+        self._scr0 = nslot * self.wmax
+        if self._xchg is not None:
+            import ctypes
+            from . import _native
+            assert self._lib.cf2_xchg_send_words(n, self.ol, self.depth, self.kmax) == self.send.numel()
+            assert self._lib.cf2_xchg_recv_words(n, self.ol, self.world, self.depth, self.kmax) == self.recv.numel()
+            arr = lambda ts: (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])     # noqa: E731
+            self._reg = [arr(self.obs), arr(self.done)]
+            _native.check(self._lib.cf2_xchg_register(
+                self._xchg, self.n, self.ol, int(self.watch) & 0xFFFFFFFF, self.kmax, *self._reg, self.send.data_ptr(),
+                self.recv.data_ptr(), self.age.data_ptr(), self.overflow.data_ptr(), self.pred.data_ptr(), self.npred),
+                "cf2_xchg_register")
+            _LIVE_XCHG.add(self)
+            if len(_LIVE_XCHG) == 1:
+                import atexit
+                atexit.register(_close_live_exchanges)
+        elif self.comm is not None:
+            E = torch.cuda.Event
+            self._ev_free = [E() for _ in range(self.depth)]
+            self._free_rec = [False] * self.depth
+            self._ev_end = E()
 
     @property
     def exchange(self) -> str:
-        """How a step's exchange runs: 'native' (one cf2_xchg_step call), 'torch' (launches and the
-        process group's all-gather from Python), 'gloo' or 'full'."""
+        """How a step's exchange runs: 'native' (cf2_xchg_* calls: per step, or batched through
+        run()), 'torch' (launches and the process group's all-gather from Python), 'gloo' or
+        'full'."""
         if not self.delta:
             return "full"
-        if not self._fast:
+        if self.comm is None:
             return "gloo"
         return "native" if self._xchg is not None else "torch"
 
     def close(self):
-        """Release the native exchange's communicator (after drain(); also run at exit)."""
+        """Release the native exchange's communicator (also run at exit)."""
         x = getattr(self, "_xchg", None)
         if x is not None:
             import torch
@@ -396,6 +504,12 @@ class PipelinedObsGather:
             _LIVE_XCHG.discard(self)
             from . import _native
             _native.check(self._lib.cf2_xchg_destroy(x), "cf2_xchg_destroy")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:       # interpreter shutdown: the runtime may be gone already
+            pass
 
     @property
     def bytes_per_rank_per_step(self) -> int:
@@ -407,26 +521,32 @@ class PipelinedObsGather:
             return self.bytes_sent / self.steps_sent
         return 4 * packed_words(self.n, self.ol, self.cap)
 
-    def _wait_free(self, j):
+    def _stream(self):
         import torch
-        f = self.free[j]
-        if f is not None:
-            if isinstance(f, torch.cuda.Event):
-                torch.cuda.current_stream(self.device).wait_event(f)
-            elif isinstance(f, int) and self._xchg is not None:     # native: the end event of slot f
-                self._lib.cf2_xchg_wait(self._xchg, f, torch.cuda.current_stream(self.device).cuda_stream)
-            self.free[j] = None
+        return torch.cuda.current_stream(self.device)
+
+    def _q(self) -> int:
+        return self._region % self.depth
 
     def buffer(self):
-        """The obs buffer env-step k writes (the current stream first waits, on the device, for the
-        exchange of step k - depth, which read it)."""
-        j = self.k % self.depth
-        self._wait_free(j)
-        return self.obs[j]
+        """The obs buffer the next env-step writes (the current stream first waits, on the device,
+        for the exchange that last read it)."""
+        if not self.delta:
+            j = self.k % self.depth
+            if self._free[j] is not None:
+                self._stream().wait_event(self._free[j])
+                self._free[j] = None
+            return self.obs[j]
+        q = self._q()
+        if self._xchg is not None:
+            self._lib.cf2_xchg_wait_free(self._xchg, q, self._stream().cuda_stream)
+        elif self.comm is not None and self._free_rec[q]:
+            self._stream().wait_event(self._ev_free[q])
+        return self.obs[q]
 
     def done_buffer(self):
-        """delta: the uint8 done (auto-reset) buffer env-step k writes; call after buffer()."""
-        return self.done[self.k % self.depth]
+        """delta: the uint8 done (auto-reset) buffer the next env-step writes; call after buffer()."""
+        return self.done[self._q()]
 
     def _gather(self, out, x):
         import torch.distributed as dist
@@ -435,32 +555,81 @@ class PipelinedObsGather:
         else:
             gather_rows(x.reshape(1, -1), self.group, sizes=[1] * self.world, out=out.view(self.world, -1))
 
-    def _run_on_comm(self, fn):
-        import torch
-        if self.comm is not None:
-            self.comm.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(self.comm):
-                return fn()
-        return fn()
+    def _send(self, q: int, s: int, words: int):
+        off = q * self.kmax * self.wmax + s * words
+        return self.send[off:off + words]
+
+    def _scratch(self, q: int, s: int):
+        off = self._scr0 + (q * self.kmax + s) * PACK_SCRATCH_WORDS
+        return self.send[off:off + PACK_SCRATCH_WORDS]
+
+    def _recv_at(self, where):
+        """(tensor starting at rank 0's packed buffer, capacity, rank stride) of a step's location."""
+        if where[0] == "start":
+            return self._start_pk, 0, packed_words(self.n, self.ol, 0)
+        q, s, nb, cap = where
+        words = packed_words(self.n, self.ol, cap)
+        off = q * self.world * self.kmax * self.wmax + s * words
+        return self.recv[off:off + (self.world - 1) * nb * words + words], cap, nb * words
 
     def start(self, obs):
-        """delta: gather the observations of a reset of every env ([n, D]) in full; every env's
-        step count since its reset is 0 on every rank."""
-
-        def run():
-            self._gather(self.slab[1], obs.contiguous())
-            self.age.zero_()
-            self.pred.zero_()
-            for s in self.send:
-                s[:1].zero_()
-        self._run_on_comm(run)
-        self.pred_host.zero_()
-        self.pred_ev = [None] * (self.L + 1)
-        if self._fast:
-            self._pred_batch = []
+        """delta: gather the observations of a reset of every env ([n, D]) in full (returned: the
+        [world * n, D] slab); every env's step count since its reset is 0 on every rank."""
+        import torch
+        if not self.delta:
+            raise RuntimeError("start() is for the delta exchange")
+        self.drain()
+        full = torch.empty(self.world * self.n, self.od, device=self.device)
+        if self.comm is not None:
+            self.comm.wait_stream(self._stream())
+            with torch.cuda.stream(self.comm):
+                self._gather(full, obs.contiguous())
+            self._stream().wait_stream(self.comm)
+        else:
+            self._gather(full, obs.contiguous())
+        # "step -1": its o_k slab (the reset observations' o parts) is what step 0's rows take as
+        # o_{k-1}; capacity 0, no resets
+        w0, ol = packed_words(self.n, self.ol, 0), self.ol
+        self._start_pk = torch.zeros(self.world * w0, dtype=torch.int32, device=self.device)
+        pv = self._start_pk.view(self.world, w0)
+        pv[:, 4:4 + self.n * ol].view(torch.float32).copy_(full[:, ol + 4:2 * ol + 4].reshape(self.world, -1))
+        self.age.zero_()
+        self.pred.zero_()
+        self.send[self._scr0:].zero_()
+        self._where = {-1: ("start",)}
+        self._counts, self._copies = {}, []
+        self._start_rows = full
         self.started = True
         self.k = 0
-        return self.slab[1]
+        return full
+
+    # ---- time-out look-ahead ----
+    def _next_pool(self):
+        b = self._pred_pool[self._pool_i % len(self._pred_pool)]
+        self._pool_i += 1
+        return b
+
+    def _count(self, s: int) -> int:
+        """The look-ahead count of step s (max over ranks), from the first host copy made at or
+        after step s (waiting for it on the host)."""
+        if s in self._counts:
+            return self._counts[s]
+        while self._copies:
+            e, buf, ev = self._copies.pop(0)
+            if e < s:
+                continue
+            if ev is not None:
+                ev.synchronize()
+            lo = max(e - self.npred + ZERO_AHEAD + 1, 0)
+            for t in range(lo, e + 1):
+                if t not in self._counts:
+                    self._counts[t] = int(buf[t % self.npred].max())
+            for t in [t for t in self._counts if t < lo - self.npred]:
+                del self._counts[t]
+            break
+        if s not in self._counts:
+            raise RuntimeError(f"delta exchange: the time-out count of step {s} was never copied to the host")
+        return self._counts[s]
 
     def step_cap(self, k: int) -> int:
         """Side capacity of env-step k (0-based since start()): the crash budget plus the time-outs
@@ -469,222 +638,206 @@ class PipelinedObsGather:
             return self.n if 0 < self.max_steps else self.cap
         if k < self.L:                       # before the first prediction: every env is k + 1 old
             t = self.n if k + 1 == self.max_steps else 0
-        elif self._fast:
-            # the first batch copy issued at or after step k - L (issued after that step's rebuild;
-            # the slot is only cleared by the rebuild of step k, after this read)
-            s = (k - self.L) % (self.L + 1)
-            c, ev = next((c, e) for (c, e) in self._pred_batch if c >= k - self.L)
-            if ev is None:                   # copied by cf2_xchg_env_step
-                self._lib.cf2_xchg_pred_sync(self._xchg, c)
-            else:
-                ev.synchronize()
-            t = int(self.pred_host[s].max())
         else:
-            s = (k - self.L) % (self.L + 1)
-            ev = self.pred_ev[s]
-            if ev is not None:
-                ev.synchronize()
-            t = int(self.pred_host[s].max())
+            t = self._count(k - self.L)
         return min(self.n, self.cap + t)
 
-    def publish(self, act=None, act_prev=None):
-        """Start the exchange of the buffer(s) the current env-step wrote; returns the slab it fills.
-        delta: act / act_prev = the actions of this env-step and of the previous one for all
-        world * n envs (unchanged until the slab is complete)."""
+    def _after(self, k0: int, nb: int, cap: int, q: int, copied: bool):
+        """Bookkeeping after the exchange of steps k0 .. k0 + nb - 1 (region q) was issued."""
         import torch
-        j = self.k % self.depth
+        for s in range(nb):
+            self._where[k0 + s] = (q, s, nb, cap)
+        for t in [t for t in self._where if t < k0 + nb - 2]:
+            del self._where[t]
+        self._region += 1
+        self.k = k0 + nb
+        self.bytes_sent += 4 * packed_words(self.n, self.ol, cap) * nb
+        self.steps_sent += nb
+        e = k0 + nb - 1
+        if not copied and self.watch != NO_WATCH and self.k // PRED_BATCH != k0 // PRED_BATCH:
+            # the count ring to the host every PRED_BATCH steps (read lookahead steps later)
+            buf = self._next_pool()
+            if self.pred.is_cuda:
+                s = self._stream()
+                if self._xchg is not None:
+                    self._lib.cf2_xchg_wait(self._xchg, s.cuda_stream)
+                elif self.comm is not None:
+                    s.wait_event(self._ev_end)
+                buf.copy_(self.pred, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            else:
+                buf.copy_(self.pred)
+                ev = None
+            self._copies.append((e, buf, ev))
+
+    def publish(self):
+        """Start the exchange of the buffer(s) the current env-step wrote.  Full rows: returns the
+        slab it fills.  delta: returns the step's index (its rows: rows())."""
+        import torch
         if not self.delta:
-            def run():
-                if self.nccl:
-                    torch.distributed.all_gather_into_tensor(self.out[j], self.obs[j], group=self.group)
-                else:
-                    gather_rows(self.obs[j], self.group, sizes=[self.n] * self.world, out=self.out[j])
-                if self.comm is not None:
+            j = self.k % self.depth
+            out = self.out[j]
+            if self.comm is not None:
+                self.comm.wait_stream(self._stream())
+                with torch.cuda.stream(self.comm):
+                    torch.distributed.all_gather_into_tensor(out, self.obs[j], group=self.group)
                     ev = torch.cuda.Event()
                     ev.record(self.comm)
-                    self.free[j] = ev
-                return self.out[j]
-            out = self._run_on_comm(run)
+                self._free[j] = ev
+            else:
+                gather_rows(self.obs[j], self.group, sizes=[self.n] * self.world, out=out)
             self.k += 1
             return out
         if not self.started:
             raise RuntimeError("delta exchange: call start(reset observations) first")
-        if act is None or act_prev is None:
-            raise ValueError("delta exchange: publish needs the actions of this step and of the previous one")
-        if self._fast:
-            return self._publish_fast(act, act_prev)
-        k = self.k
+        k, q = self.k, self._q()
         cap = self.step_cap(k)
         words = packed_words(self.n, self.ol, cap)
-        prev, cur = self.slab[(k + 1) % 2], self.slab[k % 2]
-        ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
-        send, recv = self.send[j][:words], self.recv[j][:self.world * words]
-
-        def unpack():
-            watch = self.watch if self.watch != NO_WATCH else NO_WATCH
-            unpack_obs(recv, self.world, self.n, self.ol, cap, act, act_prev, self.age, prev, cur, self.overflow,
-                       watch, self.pred[ps] if watch != NO_WATCH else None,
-                       self.pred[pn] if watch != NO_WATCH else None)
-            if watch != NO_WATCH:
-                self.pred_host[ps].copy_(self.pred[ps], non_blocking=True)
-                if self.pred.is_cuda:             # the host reads it L steps later, after this event
-                    pe = torch.cuda.Event()
-                    pe.record(torch.cuda.current_stream(self.device))
-                    self.pred_ev[ps] = pe
-            if self.comm is not None:
-                ev2 = torch.cuda.Event()
-                ev2.record(torch.cuda.current_stream(self.device))
-                self._ready = ev2
-
-        def run():
-            pack_obs(self.obs[j], self.done[j], cap, out=send, clear_next=self.send[(j + 1) % self.depth][:1])
-            if self.comm is not None:
-                ev = torch.cuda.Event()
-                ev.record(self.comm)
-                self.free[j] = ev
-            if recv.is_cuda and not self.nccl:      # gloo with GPU tensors: via the host
+        send = self._send(q, 0, words)
+        recv = self.recv[q * self.world * self.kmax * self.wmax:][:self.world * words]
+        qn = (self._region + 1) % self.depth
+        w = self.watch != NO_WATCH
+        ps = self.pred[k % self.npred] if w else None
+        pn = self.pred[(k + 1) % self.npred] if w else None
+        if self._xchg is not None:
+            from . import _native
+            _native.check(self._lib.cf2_xchg_publish(self._xchg, k, cap, q, self._stream().cuda_stream),
+                          "cf2_xchg_publish")
+        elif self.comm is not None:
+            pack_obs(self.obs[q], self.done[q], cap, out=send, scratch=self._scratch(q, 0),
+                     next_scratch=self._scratch(qn, 0))
+            comm = self.comm
+            comm.wait_stream(self._stream())
+            with torch.cuda.stream(comm):
+                torch.distributed.all_gather_into_tensor(recv, send, group=self.group)
+                self._ev_free[q].record(comm)          # the region's buffers are free after the all-gather
+                self._free_rec[q] = True
+                consume_obs(recv, self.world, self.n, self.ol, cap, self.age, self.overflow, self.watch, ps, pn)
+                self._ev_end.record(comm)
+        else:
+            cuda = send.is_cuda
+            pack_obs(self.obs[q], self.done[q], cap, out=send, scratch=self._scratch(q, 0) if cuda else None,
+                     next_scratch=self._scratch(qn, 0) if cuda else None)
+            if recv.is_cuda:                       # gloo with GPU tensors: via the host
                 host = gather_rows(send.cpu().reshape(1, -1), self.group, sizes=[1] * self.world)
                 recv.copy_(host.reshape(-1))
             else:
                 self._gather(recv, send)
-            unpack()
-            return cur
-        out = self._run_on_comm(run)
-        self.bytes_sent += 4 * words
-        self.steps_sent += 1
-        self.k += 1
-        return out
+            consume_obs(recv, self.world, self.n, self.ol, cap, self.age, self.overflow, self.watch, ps, pn)
+        self._after(k, 1, cap, q, copied=False)
+        return k
 
-    def _publish_fast(self, act, act_prev):
-        """publish() of the RCCL delta path: the general path's operations (pack, all-gather,
-        rebuild, all on the exchange stream) with pre-checked buffers, raw pointers and reused
-        events."""
-        import torch
-        import torch.distributed as dist
-        k, j, D = self.k, self.k % self.depth, self.depth
-        N = self.world * self.n
-        if act.numel() < N * 4 or act_prev.numel() < N * 4 or not (act.is_cuda and act_prev.is_cuda):
-            raise ValueError("delta exchange: act / act_prev must be [world * n, 4] on the GPU")
-        cap = self.step_cap(k)
-        key = (j, cap)
-        v = self._views.get(key)
-        if v is None:
-            words = packed_words(self.n, self.ol, cap)
-            v = self._views[key] = (words, self.send[j][:words], self.recv[j][:self.world * words])
-        words, send, recv = v
-        lib, comm = self._lib, self.comm
-        watch = self.watch
-        ps, pn = k % (self.L + 1), (k + 1) % (self.L + 1)
-        w = watch != NO_WATCH
-        if self._xchg is not None:
-            # fork, pack, RCCL all-gather, rebuild and the end event of slot j: one C call
-            st = lib.cf2_xchg_step(self._xchg, j, self._p_obs[j], self._p_done[j], self.n, self.ol, cap,
-                                   self._p_send[j], self._p_send[(j + 1) % D], self._p_recv[j], act.data_ptr(),
-                                   act_prev.data_ptr(), self._p_age, self._p_slab[(k + 1) % 2], self._p_slab[k % 2],
-                                   self._p_ovf, int(watch) & 0xFFFFFFFF, self._p_pred[ps] if w else None,
-                                   self._p_pred[pn] if w else None, torch.cuda.current_stream(self.device).cuda_stream,
-                                   self._comm_h)
-            if st != 0:
-                from . import _native
-                _native.check(st, "cf2_xchg_step")
-        else:
-            ef = self._ev_fork[j]
-            ef.record(torch.cuda.current_stream(self.device))
-            comm.wait_event(ef)
-            st = lib.cf2_obs_pack(self._p_obs[j], self._p_done[j], self.n, self.ol, cap, self._p_send[j],
-                                  self._p_send[(j + 1) % D], self._comm_h)
-            if st != 0:
-                from . import _native
-                _native.check(st, "cf2_obs_pack")
-            with torch.cuda.stream(comm):          # the synchronous call: 19 us of host time, async + wait 42 us
-                dist.all_gather_into_tensor(recv, send, group=self.group)
-            st = lib.cf2_obs_unpack(self._p_recv[j], self.world, self.n, self.ol, cap, act.data_ptr(),
-                                    act_prev.data_ptr(), self.age.data_ptr(), self._p_slab[(k + 1) % 2],
-                                    self._p_slab[k % 2], self.overflow.data_ptr(), int(watch) & 0xFFFFFFFF,
-                                    self._p_pred[ps] if w else None, self._p_pred[pn] if w else None, self._comm_h)
-            if st != 0:
-                from . import _native
-                _native.check(st, "cf2_obs_unpack")
-        return self._published(k, j, words, w)
-
-    def step_and_publish(self, env, act_ptr: int, act_all_ptr: int, act_prev_all_ptr: int):
-        """Native exchange: env-step k of `env` (this rank's shard; act_ptr its [n, 4] actions) into
-        the exchange's buffers, then that step's exchange, in one C call (cf2_xchg_env_step: what
-        buffer() + env.step_raw(...) + publish(act_all, act_prev_all) do).  Raw device pointers,
-        not checked (act_all / act_prev_all: [world * n, 4] float32, as publish() takes them).
-        Returns the slab of step k."""
-        import torch
+    def step_and_publish(self, env, act_ptr: int):
+        """Native exchange: env-step k of `env` (this rank's shard; act_ptr its [n, 4] actions, a raw
+        device pointer, not checked) with its pack fused in, then that step's exchange, in one C call
+        (cf2_xchg_env_step: what buffer() + env.step_raw(...) + publish() do).  Returns k."""
         if self._xchg is None:
             raise RuntimeError("step_and_publish needs the native exchange (RCCL, delta=True)")
         if not self.started:
             raise RuntimeError("delta exchange: call start(reset observations) first")
         if env.num_envs != self.n or env.obs_dim != self.od:
             raise ValueError("step_and_publish: the env's shard does not match the exchange's layout")
-        k, j = self.k, self.k % self.depth
+        k, q = self.k, self._q()
         cap = self.step_cap(k)
         rew, trunc, cost, level = env._raw_step_outputs()
-        st = self._lib.cf2_xchg_env_step(self._xchg, env._ctx, k, cap, act_ptr, act_all_ptr, act_prev_all_ptr, rew,
-                                         trunc, cost, level, torch.cuda.current_stream(self.device).cuda_stream)
+        st = self._lib.cf2_xchg_env_step(self._xchg, env._ctx, k, cap, q, act_ptr, rew, trunc, cost, level,
+                                         self._stream().cuda_stream)
         if st != 0:
             from . import _native
             _native.check(st, "cf2_xchg_env_step")
-        words = self._views.get(("w", cap))
-        if words is None:
-            words = self._views[("w", cap)] = packed_words(self.n, self.ol, cap)
-        if self.watch != NO_WATCH and k % PRED_BATCH == 0:      # the C call copied the count ring
-            self._pred_batch.append((k, None))
-            if len(self._pred_batch) > len(self._ev_pred) - 1:
-                self._pred_batch.pop(0)
-        return self._published(k, j, words, False)
+        self._after(k, 1, cap, q, copied=False)
+        return k
 
-    def _published(self, k, j, words, w):
-        """publish()'s bookkeeping after the exchange of step k (buffer slot j) was issued (w: copy
-        the time-out count ring to the host at this step's batch boundary)."""
+    def run(self, env, act_ptrs, steps: int) -> int:
+        """Native exchange: `steps` env-steps of `env` (this rank's shard), the actions of step k at
+        act_ptrs[k % len(act_ptrs)] (raw device pointers to [n, 4] float32, e.g. a ring the policy
+        fills ahead, or a synthetic rollout's), in batches of `unit` aligned to multiples of it: a
+        batch's env-steps (the pack fused in) back to back on the current stream, then one
+        all-gather and one consume of the batch on the exchange stream, which run while the next
+        batch steps (cf2_xchg_run).  A batch's side capacity is the largest of its steps'.  Returns
+        the index of the last step (its rows: rows())."""
+        import ctypes
         import torch
-        comm = self.comm
-        if w and k % PRED_BATCH == 0:
-            # the whole count ring to the host every PRED_BATCH steps: step_cap(k') reads the count of
-            # step k' - L from the first batch copy at or after it (each is ~15 us of host work)
-            with torch.cuda.stream(comm):
-                self.pred_host.copy_(self.pred, non_blocking=True)
-                pe = self._ev_pred[(k // PRED_BATCH) % len(self._ev_pred)]
-                pe.record(comm)
-            self._pred_batch.append((k, pe))
-            if len(self._pred_batch) > len(self._ev_pred) - 1:
-                self._pred_batch.pop(0)
-        if self._xchg is not None:
-            self._ready = j                    # the exchange that read obs / done buffer j ends at slot j
-            self.free[j] = j
-        else:
-            eu = self._ev_unp[j]
-            eu.record(comm)
-            self._ready = eu
-            self.free[j] = eu                  # the exchange that read obs / done buffer j ends here
-        self.bytes_sent += 4 * words
-        self.steps_sent += 1
-        self.k += 1
-        return self.slab[k % 2]
+        if self._xchg is None:
+            raise RuntimeError("run needs the native exchange (RCCL, delta=True)")
+        if not self.started:
+            raise RuntimeError("delta exchange: call start(reset observations) first")
+        if env.num_envs != self.n or env.obs_dim != self.od:
+            raise ValueError("run: the env's shard does not match the exchange's layout")
+        nact = len(act_ptrs)
+        if nact < 1:
+            raise ValueError("run: at least one action buffer")
+        arr = (ctypes.c_void_p * nact)(*act_ptrs)
+        rew, trunc, cost, level = env._raw_step_outputs()
+        s = self._stream()
+        w = self.watch != NO_WATCH
+        done = 0
+        while done < steps:
+            k0, q = self.k, self._q()
+            nb = min(self.unit - k0 % self.unit, steps - done)
+            cap = max(self.step_cap(k) for k in range(k0, k0 + nb))
+            buf = self._next_pool() if w else None
+            st = self._lib.cf2_xchg_run(self._xchg, env._ctx, k0, nb, cap, q, arr, nact, rew, trunc, cost, level,
+                                        buf.data_ptr() if w else None, s.cuda_stream)
+            if st != 0:
+                from . import _native
+                _native.check(st, "cf2_xchg_run")
+            if w:
+                # the batch's count copy ends on the exchange stream: a side stream waits for it there
+                # and carries the event the host synchronises on when it reads the counts
+                ev = torch.cuda.Event()
+                self._lib.cf2_xchg_wait(self._xchg, self._side_stream().cuda_stream)
+                ev.record(self._side_stream())
+                self._copies.append((k0 + nb - 1, buf, ev))
+            self._after(k0, nb, cap, q, copied=True)
+            done += nb
+        return self.k - 1
 
-    def ready(self):
-        """Make the current stream wait for the latest published slab."""
+    def _side_stream(self):
         import torch
-        ev = getattr(self, "_ready", None)
-        if isinstance(ev, int) and self._xchg is not None:
-            self._lib.cf2_xchg_wait(self._xchg, ev, torch.cuda.current_stream(self.device).cuda_stream)
-        elif ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def rows(self, act, act_prev, act_prev2, out=None, row0: int = 0, nrows: int | None = None):
+        """delta: rows [row0, row0 + nrows) (default: all world * n) of the latest published step's
+        observation slab, materialised on the current stream (cf2_obs_rows) after that step's
+        exchange: act / act_prev / act_prev2 = the actions of that step and of the two before it
+        ([world * n, 4]; at the first steps after start() pass the earliest ones again).  Valid until
+        the next publish / run.  Before any step: the slab start() gathered."""
+        if not self.delta:
+            raise RuntimeError("rows() is for the delta exchange")
+        k = self.k - 1
+        N = self.world * self.n
+        nrows = N - row0 if nrows is None else int(nrows)
+        if k < 0:
+            res = self._start_rows[row0:row0 + nrows]
+            if out is not None:
+                out.copy_(res)
+                return out
+            return res
+        self.drain()
+        cur, cap, st = self._recv_at(self._where[k])
+        prev, cap_p, st_p = self._recv_at(self._where[k - 1])
+        return obs_rows(cur, cap, prev, cap_p, self.world, self.n, self.ol, self.age, act, act_prev, act_prev2,
+                        out=out, row0=row0, nrows=nrows, stride=st, stride_prev=st_p)
 
     def overflows(self) -> int:
-        """delta: steps x ranks whose resets exceeded the side capacity so far (host read)."""
+        """delta: 64-env pack blocks whose resets found no side slot so far (host read)."""
         return int(self.overflow.item()) if self.delta else 0
 
     def drain(self):
         """Make the current stream wait for every exchange in flight."""
-        import torch
-        if self.comm is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.comm)
-        for j in range(self.depth):
-            self.free[j] = None
+        s = self._stream() if self.device.type == "cuda" else None
+        if s is None:
+            return
+        if self._xchg is not None:
+            self._lib.cf2_xchg_wait(self._xchg, s.cuda_stream)
+        elif self.comm is not None:
+            s.wait_stream(self.comm)
+        if not self.delta:
+            self._free = [None] * self.depth
 
 
 def shard_range(num_envs_total: int, rank: int, world: int) -> tuple[int, int]:

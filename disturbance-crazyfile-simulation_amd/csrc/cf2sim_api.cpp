@@ -342,6 +342,24 @@ int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* o
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
+int cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
+                    uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* packed_dev, uint32_t* scratch_dev,
+                    uint32_t* next_scratch_dev, uint32_t cap, void* stream) {
+    if (!ctx || !act_dev || !obs_dev || !rew_dev || !done_dev || !packed_dev || !scratch_dev) return CF2_ERR_INVALID_ARG;
+    if (cap > ctx->P.N || scratch_dev == next_scratch_dev) return CF2_ERR_INVALID_ARG;
+    if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL) return CF2_ERR_INVALID_ARG;
+    if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
+    if (ctx->P.ground_effect) return CF2_ERR_UNSUPPORTED;
+    if (((uintptr_t)act_dev & 15u) != 0 || ((uintptr_t)obs_dev & 15u) != 0 || ((uintptr_t)packed_dev & 15u) != 0 ||
+        ((uintptr_t)scratch_dev & 3u) != 0)
+        return CF2_ERR_INVALID_ARG;
+    StepIO io{ctx->sf, act_dev, nullptr, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev, nullptr};
+    const PackIO pio{packed_dev, scratch_dev, next_scratch_dev, cap};
+    const hipError_t e = launch_step_packed(ctx->P, io, pio, (hipStream_t)stream);
+    if (e == hipErrorNotSupported) return CF2_ERR_UNSUPPORTED;
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
 int cf2_collect_step(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
                      uint8_t* trunc_dev, float* final_obs_dev, const float* packed_dev, uint32_t obs_dim, int precision,
                      uint64_t seed, uint32_t counter, uint32_t row_offset, float* act_out_dev, float* val_out_dev,

@@ -9,32 +9,39 @@
 //   * a bitmap of the envs that auto-reset this step     (1 bit per env)
 //   * for those envs (up to `cap`): the reset row's o_0 and its action part A (the reset's
 //     action-buffer entry, A_0 = A_1)                    (1 + OL + 4 words each)
-// and every receiver rebuilds the full [N_total, OD] slab from its previous one.  The action slots
-// follow the reference's history aliasing (compute_history with the action deque holding the
-// action buffer's last entry right after a reset, envs/base.py:455-462; the kernel's halias flags):
-// with `age` = env-steps since the env's last reset (0 = reset this step; uint16, saturating),
-//   age 1:  A0 = A1 = a_k           (both history slots alias the action buffer, which after the
-//                                     step holds a_k in every row: aggregate_phy_steps is a
-//                                     multiple of buf_size, as in the reference's default env)
-//   age 2:  A0 = a_k, A1 = a_{k-1}
-//   age 3+: A0 = the previous row's A1, A1 = a_{k-1}
-// where a_k is the action of the env-step that produced the row.  The receiver tracks age from the
-// bitmaps (exact: reset or not is always known).  More resets than `cap` on a rank in one step
-// (an overflow) leaves those rows' o_0 / A parts unknown: the receiver writes NaN there and counts
-// the overflow; the rows of the following steps are exact again.
+// Receivers keep what they gathered (compact): per env-step they only advance every env's `age`
+// (env-steps since its last reset; uint16, saturating; cf2_obs_consume), and a row is materialised
+// on request (cf2_obs_rows) from the gathered buffers of step k and k - 1, the age and the actions
+// of steps k, k - 1 and k - 2, following the reference's history aliasing (compute_history with the
+// action deque holding the action buffer's last entry right after a reset, envs/base.py:455-462;
+// the kernel's halias flags):
+//   age 0:  [o_0, A, o_k, A]                         (the reset's side entry; o_k from step k)
+//   age 1:  [o_{k-1}, a_k, o_k, a_k]                 (both history slots alias the action buffer,
+//                                                     which after the step holds a_k in every row:
+//                                                     aggregate_phy_steps is a multiple of buf_size,
+//                                                     as in the reference's default env)
+//   age 2:  [o_{k-1}, a_k, o_k, a_{k-1}]
+//   age 3+: [o_{k-1}, a_{k-2}, o_k, a_{k-1}]
+// where a_k is the action of the env-step that produced the row and o_{k-1} is o_k of step k - 1.
+// The receiver tracks age from the bitmaps (exact: reset or not is always known).  A rank with more
+// resets than its side slab holds in one step (an overflow) marks the 64-env pack blocks whose
+// resets got no slot (PACK_DROPPED in the block table): exactly those reset rows get NaN in their
+// o_0 / A parts and every dropped block is counted; their o_k parts and all other rows stay exact,
+// and the following steps are exact again.
 // The capacity may change from step to step (the caller sizes the all-gather): TimeLimit
 // truncations are predictable, so the receiver counts, per rank, the envs whose age reaches
 // max_steps - L this step -- at most that many time out L steps later (fewer if they crash first)
-// -- into pred[step % (L + 1)][rank], and the caller adds that count to the crash budget of step
+// -- into pred[step % npred][rank], and the caller adds that count to the crash budget of step
 // + L.  Every rank holds the same ages, so every rank derives the same capacity.
 //
-// Packed buffer of one rank (32-bit words, 16-B multiple; cf2_obs_packed_words):
-//   [0] reset count (may exceed cap)   [1] n   [2] OL   [3] cap
-//   [4, 4 + n OL)                       o_k rows
-//   [.., + ceil(n / 32))                reset bitmap, env i = bit i % 32 of word i / 32
-//   [.., + ceil(n / 256))               block table: the first side slot of each 256-env pack block
-//                                       (a block's resets hold consecutive slots, in env order)
-//   [.., + cap (OL + 5))                side entries: local env index, o_0[OL], A[4]
+// The packed buffer's layout and its side-slot allocation: cf2sim_pack.h.
+//
+// Driving it (cf2_xchg_*): an RCCL communicator of the library's own and, on an exchange stream
+// forked from the env stream, one all-gather + one consume per batch of env-steps: eagerly one C
+// call per step (cf2_xchg_publish / cf2_xchg_env_step: batches of one), or cf2_xchg_run, whose
+// env-steps (the pack fused in, cf2_step_packed) go back to back on the env stream while the
+// previous batch's all-gather runs, so neither the host's per-step issue work nor a per-step
+// collective bounds the pipeline.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
@@ -42,25 +49,14 @@
 #include <string.h>
 #include <math.h>
 #include <mutex>
+#include <vector>
 #include "../../include/cf2sim.h"
 #include "cf2sim_internal.h"
+#include "cf2sim_pack.h"
 
 namespace cf2 {
 
-constexpr uint32_t XB_PACK = 256;   // envs per pack block (one block-table word each)
-
-struct PackLayout {
-    uint32_t n, ol, cap;
-    __host__ __device__ uint32_t od() const { return 2u * (ol + 4u); }
-    __host__ __device__ uint32_t o_slab() const { return 4u; }
-    __host__ __device__ uint32_t bits() const { return 4u + n * ol; }
-    __host__ __device__ uint32_t btab() const { return bits() + (n + 31u) / 32u; }
-    __host__ __device__ uint32_t side() const { return btab() + (n + XB_PACK - 1u) / XB_PACK; }
-    __host__ __device__ uint32_t entry() const { return ol + 5u; }
-    __host__ __device__ uint32_t words() const { return (side() + cap * entry() + 3u) & ~3u; }
-};
-
-constexpr uint32_t XB = XB_PACK;    // rows per block
+constexpr uint32_t XB = 256;        // rows per block of the exchange kernels (4 pack blocks)
 
 // Coalesced copy of `count` floats (16-B aligned, a multiple of 4) between global memory and LDS,
 // all threads of the block; the scalar form for a ragged tail block
@@ -85,114 +81,152 @@ __device__ __forceinline__ void lds_to_rows(float* g, const float* s, uint32_t c
 
 // Sender: one thread per env of this rank (OL: 13 with sensor noise, 17 without).  The block's obs
 // rows are read coalesced into LDS, o_k extracted into an LDS stage and written as one contiguous
-// run of the o_k slab; the reset bitmap comes from wave ballots; the block's resets take
-// consecutive side slots from one atomic per block on the count word (per-wave atomics on that one
-// word serialised at the L2: 19.5 us per 32 768-env pack), in an order that is immaterial (each
-// entry carries its env index).  clear_next: the count word of the buffer the next pack on this
-// stream writes (its previous contents were gathered already), so the counts need no memset.
+// run of the o_k slab; the reset bitmap comes from wave ballots; each wave is one pack block and
+// takes its resets' side slots with one pack_alloc (cf2sim_pack.h).  next_scratch: the counters of
+// the buffer the next pack on this stream uses (zeroed here; this pack's were zeroed by the last).
 template <uint32_t OL>
 __global__ void __launch_bounds__(XB) obs_pack_kernel(const float* __restrict__ obs, const uint8_t* __restrict__ reset,
                                                       PackLayout L, uint32_t* __restrict__ pk,
-                                                      uint32_t* __restrict__ clear_next) {
+                                                      uint32_t* __restrict__ scratch,
+                                                      uint32_t* __restrict__ next_scratch) {
     constexpr uint32_t OD = 2u * (OL + 4u);
     __shared__ __align__(16) float s_rows[XB * OD];
     __shared__ __align__(16) float s_o[XB * OL];
-    __shared__ uint32_t s_wcnt[XB / 64u + 1u];
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid, lane = tid & 63u, wv = tid >> 6;
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid, lane = tid & 63u;
     const uint32_t nrow = L.n - base < XB ? L.n - base : XB;
-    if (blockIdx.x == 0 && tid == 0) {
-        if (clear_next) clear_next[0] = 0u;
-        pk[1] = L.n; pk[2] = OL; pk[3] = L.cap;
+    if (blockIdx.x == 0) {
+        if (tid == 0) { pk[0] = 0u; pk[1] = L.n; pk[2] = OL; pk[3] = L.cap; }
+        if (next_scratch)
+            for (uint32_t k = tid; k < PACK_SCRATCH_WORDS; k += XB) next_scratch[k] = 0u;
     }
     const bool live = tid < nrow;
     const bool r = live && reset[i] != 0;
     const uint64_t m = __ballot(r);
-    if (lane == 0) s_wcnt[wv] = (uint32_t)__popcll(m);
     rows_to_lds(s_rows, obs + (size_t)base * OD, nrow * OD, ((uintptr_t)obs & 15u) == 0 && (base * OD) % 4u == 0);
+    uint32_t* bits = pk + L.bits();
+    const uint32_t wbase = base + (tid & ~63u);
+    if (lane == 0 && wbase < L.n) bits[wbase / 32u] = (uint32_t)m;
+    if (lane == 32 && wbase + 32u < L.n) bits[wbase / 32u + 1u] = (uint32_t)(m >> 32);
+    uint32_t first = 0;
+    if (lane == 0 && wbase < L.n) {
+        first = m ? pack_alloc(L, scratch, (uint32_t)__popcll(m)) : 0u;
+        pk[L.btab() + wbase / XB_PACK] = first;
+    }
+    first = __shfl(first, 0);
     __syncthreads();
     const float* row = s_rows + tid * OD;
     if (live) {
 #pragma unroll
         for (uint32_t k = 0; k < OL; ++k) s_o[tid * OL + k] = row[OL + 4u + k];
     }
-    uint32_t* bits = pk + L.bits();
-    const uint32_t wbase = base + (tid & ~63u);
-    if (lane == 0 && wbase < L.n) bits[wbase / 32u] = (uint32_t)m;
-    if (lane == 32 && wbase + 32u < L.n) bits[wbase / 32u + 1u] = (uint32_t)(m >> 32);
-    if (tid == 0) {
-        uint32_t tot = 0;
+    if (r && first != PACK_DROPPED) {
+        uint32_t* e = pk + L.side() + (first + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) * L.entry();
+        e[0] = i;
+        float* ef = reinterpret_cast<float*>(e + 1);
 #pragma unroll
-        for (uint32_t w = 0; w < XB / 64u; ++w) { const uint32_t c = s_wcnt[w]; s_wcnt[w] = tot; tot += c; }
-        const uint32_t first = tot ? atomicAdd(pk, tot) : 0u;     // the block's first side slot
-        s_wcnt[XB / 64u] = first;
-        pk[L.btab() + blockIdx.x] = first;
+        for (uint32_t k = 0; k < OL + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
     }
     __syncthreads();
-    if (r) {
-        const uint32_t slot = s_wcnt[XB / 64u] + s_wcnt[wv] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (slot < L.cap) {
-            uint32_t* e = pk + L.side() + slot * L.entry();
-            e[0] = i;
-            float* ef = reinterpret_cast<float*>(e + 1);
-#pragma unroll
-            for (uint32_t k = 0; k < OL + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
-        }
-    }
     lds_to_rows(reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * OL, s_o, nrow * OL,
                 ((uintptr_t)pk & 15u) == 0 && (base * OL) % 4u == 0);
 }
 
-// Receiver: one thread per global env (rank r = i / n).  The block's previous rows are read
-// coalesced into LDS, each thread rebuilds its row there (a reset row from its side entry, found
-// through the block table and the bitmap; NaN in its o_0 / A parts if the env's rank overflowed its
-// side slab), the block writes them out coalesced.  One launch (the reset entries used to take a
-// second, scattered-write kernel: 5.6 us on 262 144 rows).
-template <uint32_t OL>
-__global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __restrict__ pk_all, uint32_t words,
-                                                             uint32_t world, PackLayout L,
-                                                             const float* __restrict__ act,
-                                                             const float* __restrict__ act_prev,
-                                                             uint16_t* __restrict__ age,
-                                                             const float* __restrict__ slab_prev,
-                                                             float* __restrict__ slab, uint32_t* __restrict__ overflow,
-                                                             uint32_t watch_age, uint32_t* __restrict__ pred,
-                                                             uint32_t* __restrict__ pred_next) {
-    constexpr uint32_t OD = 2u * (OL + 4u);
-    __shared__ __align__(16) float s_rows[XB * OD];
-    const uint32_t tid = threadIdx.x, base = blockIdx.x * XB, i = base + tid;
-    const uint32_t total = world * L.n;
-    const uint32_t nrow = total - base < XB ? total - base : XB;
-    const bool al = (base * OD) % 4u == 0 && ((uintptr_t)slab_prev & 15u) == 0 && ((uintptr_t)slab & 15u) == 0;
-    if (blockIdx.x == 0 && pred_next && tid < world) pred_next[tid] = 0u;     // the next step's counts
-    // this thread's inputs first (their latency overlaps the block's row copy)
-    const bool live = tid < nrow;
+// Receiver: the steps [k, k + steps) of one consume call (up to CONSUME_MAX: the eager path
+// consumes each step, cf2_xchg_run a batch in launches of up to CONSUME_MAX steps).  One thread per global env (rank
+// r = i / n) advances the env's age through the steps from its rank's reset bitmaps.  Time-out
+// look-ahead: envs whose new age is watch_age at step s are counted per rank into pred[s] (one
+// atomic per wave where the wave holds one rank's envs); block 0 zeroes the zero[] rows (the
+// counts of the steps after these).  Every pack block whose resets got no side slot is counted
+// in overflow.
+constexpr uint32_t CONSUME_MAX = 16;
+struct ConsumeSteps {
+    const uint32_t* pk[CONSUME_MAX];       // gathered packed buffers of each step
+    uint32_t words[CONSUME_MAX];           // their per-rank stride
+    uint32_t* pred[CONSUME_MAX];           // [world] look-ahead counts of each step, or null
+    uint32_t* zero[CONSUME_MAX];           // [world] rows to zero, or null
+    uint32_t steps;
+};
+// (the step loops are unrolled: a dynamically indexed by-value kernel argument would be copied to
+// scratch; every step's bitmap word and block-table word are loaded before the dependent chain)
+__global__ void __launch_bounds__(256) obs_consume_kernel(ConsumeSteps S, uint32_t world, PackLayout L,
+                                                          uint16_t* __restrict__ age, uint32_t* __restrict__ overflow,
+                                                          uint32_t watch_age) {
+    const uint32_t tid = threadIdx.x, total = world * L.n;
+    const uint32_t i = blockIdx.x * 256u + tid;
+    if (blockIdx.x == 0 && tid < world) {
+#pragma unroll
+        for (uint32_t z = 0; z < CONSUME_MAX; ++z)
+            if (S.zero[z]) S.zero[z][tid] = 0u;
+    }
+    const bool live = i < total;
     const uint32_t ic = live ? i : total - 1u;
     const uint32_t r = ic / L.n, li = ic - r * L.n;
-    const uint32_t* pk = pk_all + (size_t)r * words;
+    const uint32_t r0 = __shfl(r, 0), r63 = __shfl(r, 63);
+    const bool head = live && li % XB_PACK == 0;
+    uint32_t bw[CONSUME_MAX], bt[CONSUME_MAX];
+#pragma unroll
+    for (uint32_t s = 0; s < CONSUME_MAX; ++s) {
+        bw[s] = 0u;
+        bt[s] = 0u;
+        if (s < S.steps) {
+            const uint32_t* pk = S.pk[s] + (size_t)r * S.words[s];
+            bw[s] = pk[L.bits() + li / 32u];
+            if (head) bt[s] = pk[L.btab() + li / XB_PACK];
+        }
+    }
+    uint32_t a = age[ic];
+#pragma unroll
+    for (uint32_t s = 0; s < CONSUME_MAX; ++s) {
+        if (s >= S.steps) break;
+        const bool rs = (bw[s] >> (li % 32u)) & 1u;
+        a = rs ? 0u : (a < 0xFFFFu ? a + 1u : 0xFFFFu);
+        if (S.pred[s]) {
+            const bool hit = live && a == watch_age;
+            if (r0 == r63) {
+                const uint64_t m = __ballot(hit);
+                if ((tid & 63u) == 0 && m) atomicAdd(S.pred[s] + r0, (uint32_t)__popcll(m));
+            } else if (hit) {
+                atomicAdd(S.pred[s] + r, 1u);
+            }
+        }
+        if (overflow && head && bt[s] == PACK_DROPPED) atomicAdd(overflow, 1u);
+    }
+    if (live) age[ic] = (uint16_t)a;
+}
+
+// Rows on request: rows [row0, row0 + nrows) of the global slab of step k, from the gathered
+// buffers of step k (pk_all, capacity L.cap, rank r's at r * stride) and k - 1 (pk_prev_all, Lp.cap,
+// stride_prev), the ages after step
+// k's consume and the actions of steps k, k - 1, k - 2 ([world n, 4] each).  Each thread builds its
+// row in LDS, the block writes them out coalesced.  A reset row finds its side entry through the
+// block table and the bitmap (pack_slot: a pack block's slots are consecutive and in env order).
+template <uint32_t OL>
+__global__ void __launch_bounds__(XB) obs_rows_kernel(const uint32_t* __restrict__ pk_all, PackLayout L, uint32_t stride,
+                                                      const uint32_t* __restrict__ pk_prev_all, PackLayout Lp,
+                                                      uint32_t stride_prev, uint32_t world,
+                                                      const uint16_t* __restrict__ age,
+                                                      const float* __restrict__ a_k, const float* __restrict__ a_km1,
+                                                      const float* __restrict__ a_km2, uint32_t row0, uint32_t nrows,
+                                                      float* __restrict__ out) {
+    constexpr uint32_t OD = 2u * (OL + 4u);
+    __shared__ __align__(16) float s_rows[XB * OD];
+    const uint32_t tid = threadIdx.x, base = blockIdx.x * XB;
+    const uint32_t cnt = nrows - base < XB ? nrows - base : XB;
+    const bool live = tid < cnt;
+    const uint32_t i = row0 + base + (live ? tid : cnt - 1u);
+    const uint32_t r = i / L.n, li = i - r * L.n;
+    const uint32_t* pk = pk_all + (size_t)r * stride;
     const float* okp = reinterpret_cast<const float*>(pk + L.o_slab()) + (size_t)li * OL;
-    float ok[OL];
-#pragma unroll
-    for (uint32_t k = 0; k < OL; ++k) ok[k] = okp[k];
+    const float* opp = reinterpret_cast<const float*>(pk_prev_all + (size_t)r * stride_prev + Lp.o_slab()) + (size_t)li * OL;
     const bool rs = (pk[L.bits() + li / 32u] >> (li % 32u)) & 1u;
-    const uint32_t a_old = age[ic];
-    const float4 ak = reinterpret_cast<const float4*>(act)[ic];
-    const float4 ap = reinterpret_cast<const float4*>(act_prev)[ic];
-    const bool ovf = pk[0] > L.cap;
-    rows_to_lds(s_rows, slab_prev + (size_t)base * OD, nrow * OD, al);
-    __syncthreads();
-    uint32_t a_new = 0xFFFFFFFFu;
+    const uint32_t a = age[i];
+    float* row = s_rows + tid * OD;
     if (live) {
-        float* row = s_rows + tid * OD;
-        if (rs) {
 #pragma unroll
-            for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = ok[k];
-            // the reset's side entry: the pack block's first slot plus the resets before this env in
-            // its block (a block's slots are consecutive and in env order)
-            const uint32_t pb = li / XB_PACK, wl = li / 32u;
-            uint32_t slot = pk[L.btab() + pb];
-            for (uint32_t w = pb * (XB_PACK / 32u); w < wl; ++w) slot += (uint32_t)__popc(pk[L.bits() + w]);
-            slot += (uint32_t)__popc(pk[L.bits() + wl] & ((1u << (li % 32u)) - 1u));
-            if (ovf || slot >= L.cap) {     // o_0 and A were not sent: marked unknown
+        for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = okp[k];
+        if (rs) {
+            const uint32_t slot = pack_slot(pk, L, li);
+            if (slot == PACK_DROPPED) {     // the side slab had no room for its block's resets
 #pragma unroll
                 for (uint32_t k = 0; k < OL + 4u; ++k) row[k] = __builtin_nanf("");
 #pragma unroll
@@ -204,34 +238,19 @@ __global__ void __launch_bounds__(XB) obs_unpack_rows_kernel(const uint32_t* __r
 #pragma unroll
                 for (uint32_t k = 0; k < 4u; ++k) row[2u * OL + 4u + k] = ef[OL + k];    // A_1 = A_0
             }
-            age[i] = 0;
-            a_new = 0;
         } else {
-            const uint32_t a = a_old < 0xFFFFu ? a_old + 1u : 0xFFFFu;
-            const float akv[4] = {ak.x, ak.y, ak.z, ak.w}, apv[4] = {ap.x, ap.y, ap.z, ap.w};
-            float a0[4], a1[4];
+            const float4 ak = reinterpret_cast<const float4*>(a_k)[i];
+            const float4 a1 = reinterpret_cast<const float4*>(a_km1)[i];
+            const float4 a0 = a >= 3u ? reinterpret_cast<const float4*>(a_km2)[i] : ak;
+            const float4 h1 = a == 1u ? ak : a1;
 #pragma unroll
-            for (uint32_t k = 0; k < 4u; ++k) {
-                a0[k] = a >= 3u ? row[2u * OL + 4u + k] : akv[k];
-                a1[k] = a == 1u ? akv[k] : apv[k];
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < OL; ++k) row[k] = row[OL + 4u + k];
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; ++k) row[OL + k] = a0[k];
-#pragma unroll
-            for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = ok[k];
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; ++k) row[2u * OL + 4u + k] = a1[k];
-            age[i] = (uint16_t)a;
-            a_new = a;
+            for (uint32_t k = 0; k < OL; ++k) row[k] = opp[k];
+            row[OL] = a0.x; row[OL + 1u] = a0.y; row[OL + 2u] = a0.z; row[OL + 3u] = a0.w;
+            row[2u * OL + 4u] = h1.x; row[2u * OL + 5u] = h1.y; row[2u * OL + 6u] = h1.z; row[2u * OL + 7u] = h1.w;
         }
     }
-    // time-out look-ahead: envs at age watch_age time out (unless they crash first) L steps later
-    if (pred && a_new == watch_age) atomicAdd(pred + r, 1u);     // ~1/max_steps of the envs per step
-    if (overflow && live && li == 0 && ovf) atomicAdd(overflow, 1u);   // one count per overflowing rank
     __syncthreads();
-    lds_to_rows(slab + (size_t)base * OD, s_rows, nrow * OD, al);
+    lds_to_rows(out + (size_t)base * OD, s_rows, cnt * OD, ((uintptr_t)out & 15u) == 0 && (base * OD) % 4u == 0);
 }
 
 }  // namespace cf2
@@ -248,41 +267,73 @@ extern "C" size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t ca
 }
 
 extern "C" int cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
-                            uint32_t* packed_dev, uint32_t* clear_next_dev, void* stream) {
-    if (!obs_dev || !reset_dev || !packed_dev || !layout_ok(n, obs_len, cap)) return CF2_ERR_INVALID_ARG;
-    if (((uintptr_t)obs_dev & 7u) || ((uintptr_t)packed_dev & 15u)) return CF2_ERR_INVALID_ARG;
+                            uint32_t* packed_dev, uint32_t* scratch_dev, uint32_t* next_scratch_dev, void* stream) {
+    if (!obs_dev || !reset_dev || !packed_dev || !scratch_dev || !layout_ok(n, obs_len, cap)) return CF2_ERR_INVALID_ARG;
+    if (((uintptr_t)obs_dev & 7u) || ((uintptr_t)packed_dev & 15u) || ((uintptr_t)scratch_dev & 3u)) return CF2_ERR_INVALID_ARG;
+    if (next_scratch_dev == scratch_dev) return CF2_ERR_INVALID_ARG;     // this pack counts in its scratch
     const PackLayout L{n, obs_len, cap};
     if (obs_len == 13u)
         hipLaunchKernelGGL(obs_pack_kernel<13>, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev,
-                           reset_dev, L, packed_dev, clear_next_dev);
+                           reset_dev, L, packed_dev, scratch_dev, next_scratch_dev);
     else
         hipLaunchKernelGGL(obs_pack_kernel<17>, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev,
-                           reset_dev, L, packed_dev, clear_next_dev);
+                           reset_dev, L, packed_dev, scratch_dev, next_scratch_dev);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
-extern "C" int cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len,
-                              uint32_t cap, const float* act_dev, const float* act_prev_dev, uint16_t* age_dev,
-                              const float* slab_prev_dev, float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age,
-                              uint32_t* pred_dev, uint32_t* pred_next_dev, void* stream) {
-    if (!packed_all_dev || !act_dev || !act_prev_dev || !age_dev || !slab_prev_dev || !slab_dev || world == 0 ||
-        !layout_ok(n, obs_len, cap) || (uint64_t)world * n >= (1ull << 31))
+static int consume_launch(const ConsumeSteps& S, uint32_t world, const PackLayout& L, uint16_t* age, uint32_t* overflow,
+                          uint32_t watch_age, hipStream_t st) {
+    const uint32_t total = world * L.n;
+    hipLaunchKernelGGL(obs_consume_kernel, dim3((total + 255u) / 256u), dim3(256), 0, st, S, world, L, age, overflow,
+                       watch_age);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_obs_consume(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len,
+                               uint32_t cap, uint16_t* age_dev, uint32_t* overflow_dev, uint32_t watch_age,
+                               uint32_t* pred_dev, uint32_t* pred_next_dev, void* stream) {
+    if (!packed_all_dev || !age_dev || world == 0 || world > 256 || !layout_ok(n, obs_len, cap) ||
+        (uint64_t)world * n >= (1ull << 31))
         return CF2_ERR_INVALID_ARG;
-    if (slab_prev_dev == slab_dev) return CF2_ERR_INVALID_ARG;     // rows are rebuilt from the previous slab
-    if (((uintptr_t)act_dev & 15u) || ((uintptr_t)act_prev_dev & 15u) || ((uintptr_t)packed_all_dev & 15u) ||
-        ((uintptr_t)slab_dev & 7u) || ((uintptr_t)slab_prev_dev & 7u))
-        return CF2_ERR_INVALID_ARG;
+    if (pred_dev && pred_dev == pred_next_dev) return CF2_ERR_INVALID_ARG;
+    if (((uintptr_t)packed_all_dev & 15u) || ((uintptr_t)age_dev & 1u)) return CF2_ERR_INVALID_ARG;
     const PackLayout L{n, obs_len, cap};
-    const uint32_t words = L.words(), total = world * n;
+    ConsumeSteps S;
+    memset(&S, 0, sizeof(S));
+    S.pk[0] = packed_all_dev; S.words[0] = L.words(); S.pred[0] = pred_dev; S.zero[0] = pred_next_dev; S.steps = 1;
+    return consume_launch(S, world, L, age_dev, overflow_dev, watch_age, (hipStream_t)stream);
+}
+
+extern "C" int cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride,
+                            const uint32_t* packed_prev_all_dev, uint32_t cap_prev, uint32_t stride_prev,
+                            uint32_t world, uint32_t n, uint32_t obs_len, const uint16_t* age_dev, const float* act_dev,
+                            const float* act_prev_dev, const float* act_prev2_dev, uint32_t row0, uint32_t nrows,
+                            float* rows_dev, void* stream) {
+    if (!packed_all_dev || !packed_prev_all_dev || !age_dev || !act_dev || !act_prev_dev || !act_prev2_dev ||
+        !rows_dev || world == 0 || !layout_ok(n, obs_len, cap) || !layout_ok(n, obs_len, cap_prev) ||
+        (uint64_t)world * n >= (1ull << 31) || (uint64_t)row0 + nrows > (uint64_t)world * n)
+        return CF2_ERR_INVALID_ARG;
+    const PackLayout L{n, obs_len, cap}, Lp{n, obs_len, cap_prev};
+    if (stride == 0) stride = L.words();
+    if (stride_prev == 0) stride_prev = Lp.words();
+    if ((world > 1 && (stride < L.words() || stride_prev < Lp.words())) || (stride & 3u) || (stride_prev & 3u))
+        return CF2_ERR_INVALID_ARG;
+    if (((uintptr_t)packed_all_dev & 15u) || ((uintptr_t)packed_prev_all_dev & 15u) || ((uintptr_t)act_dev & 15u) ||
+        ((uintptr_t)act_prev_dev & 15u) || ((uintptr_t)act_prev2_dev & 15u) || ((uintptr_t)rows_dev & 3u) ||
+        ((uintptr_t)age_dev & 1u))
+        return CF2_ERR_INVALID_ARG;
+    if (nrows == 0) return CF2_OK;
+    const dim3 grid((nrows + XB - 1) / XB);
     if (obs_len == 13u)
-        hipLaunchKernelGGL(obs_unpack_rows_kernel<13>, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
-                           packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
-                           overflow_dev, watch_age, pred_dev, pred_next_dev);
+        hipLaunchKernelGGL(obs_rows_kernel<13>, grid, dim3(XB), 0, (hipStream_t)stream, packed_all_dev, L, stride,
+                           packed_prev_all_dev, Lp, stride_prev, world, age_dev, act_dev, act_prev_dev, act_prev2_dev,
+                           row0, nrows, rows_dev);
     else
-        hipLaunchKernelGGL(obs_unpack_rows_kernel<17>, dim3((total + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream,
-                           packed_all_dev, words, world, L, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
-                           overflow_dev, watch_age, pred_dev, pred_next_dev);
+        hipLaunchKernelGGL(obs_rows_kernel<17>, grid, dim3(XB), 0, (hipStream_t)stream, packed_all_dev, L, stride,
+                           packed_prev_all_dev, Lp, stride_prev, world, age_dev, act_dev, act_prev_dev, act_prev2_dev,
+                           row0, nrows, rows_dev);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
@@ -298,35 +349,35 @@ struct RcclApi {
 };
 RcclApi g_rccl;
 std::mutex g_rccl_mu;
-constexpr uint32_t XCHG_MAX_DEPTH = 8;
+constexpr uint32_t XCHG_MAX_DEPTH = 8, XCHG_MAX_PRED = 1024, XCHG_MAX_BATCH = 64;
 }  // namespace
 
-constexpr uint32_t XCHG_MAX_PRED = 64, XCHG_MAX_PRED_EV = 16;
-
+// Buffers (cf2_xchg_register): `depth` regions, each holding the packed buffers of one batch of up
+// to kmax env-steps.  A batch of nb steps at capacity cap packs step s of the batch into
+// send[region][s * words(cap)], so the batch is one contiguous run of nb * words(cap) words that one
+// all-gather moves: recv[region] then holds [world][nb][words(cap)].  Each publish / batch takes the
+// next region (a counter), so the previous step's buffers are always intact for cf2_obs_rows.
 struct cf2_xchg {
     ncclComm_t comm;
     uint32_t world, rank, depth;
-    hipEvent_t fork;
-    hipEvent_t end[XCHG_MAX_DEPTH];
-    bool pending[XCHG_MAX_DEPTH];      // slot's exchange issued: the next env-step into it waits for end[slot]
-    bool recorded[XCHG_MAX_DEPTH];     // end[slot] has been recorded at least once
-    // registered buffers (cf2_xchg_register) for cf2_xchg_env_step
+    int device;
+    hipStream_t xs;                    // the exchange stream
+    hipEvent_t fork;                   // env stream -> exchange stream
+    hipEvent_t free_[XCHG_MAX_DEPTH];  // the all-gather of region q's last batch is done: q may be rewritten
+    hipEvent_t end;                    // every exchange issued so far is complete
+    bool free_rec[XCHG_MAX_DEPTH], end_rec;
+    uint64_t next_region;
+    // registered buffers
     bool registered;
-    uint32_t n, ol, watch, npred;
+    uint32_t n, ol, watch, npred, kmax;
+    size_t wmax;                       // words of the largest packed buffer (cap = n)
     float* obs[XCHG_MAX_DEPTH];
     uint8_t* done[XCHG_MAX_DEPTH];
-    uint32_t* send[XCHG_MAX_DEPTH];
-    uint32_t* recv[XCHG_MAX_DEPTH];
-    float* slab[2];
+    uint32_t* send;                    // [depth][kmax][wmax], then [depth * kmax][PACK_SCRATCH_WORDS] counters
+    uint32_t* recv;                    // [depth][world * kmax * wmax]
     uint16_t* age;
     uint32_t* overflow;
-    uint32_t* pred[XCHG_MAX_PRED];
-    // the look-ahead ring copied to pinned host memory every pred_batch env-steps, each copy
-    // followed by an event of a ring of npev (cf2_xchg_pred_sync)
-    uint32_t* pred_host;
-    uint32_t pred_batch, npev;
-    hipEvent_t pev[XCHG_MAX_PRED_EV];
-    hipStream_t comm_stream;
+    uint32_t* pred;                    // [npred][world]
 };
 
 extern "C" int cf2_xchg_bind(const char* rccl_path) {
@@ -355,29 +406,44 @@ extern "C" int cf2_xchg_unique_id(uint8_t* id_out, size_t id_len) {
     return CF2_OK;
 }
 
+static void xchg_free_events(cf2_xchg* x) {
+    if (x->fork) (void)hipEventDestroy(x->fork);
+    for (uint32_t k = 0; k < XCHG_MAX_DEPTH; ++k)
+        if (x->free_[k]) (void)hipEventDestroy(x->free_[k]);
+    if (x->end) (void)hipEventDestroy(x->end);
+    if (x->xs) (void)hipStreamDestroy(x->xs);
+}
+
 extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world, uint32_t rank, uint32_t depth,
                                cf2_xchg** out) {
-    if (!id || id_len < sizeof(ncclUniqueId) || !out || world == 0 || rank >= world || depth == 0 ||
+    // depth >= 2: the rows of step k are built from the gathered buffers of steps k and k - 1
+    if (!id || id_len < sizeof(ncclUniqueId) || !out || world == 0 || world > 256 || rank >= world || depth < 2 ||
         depth > XCHG_MAX_DEPTH)
         return CF2_ERR_INVALID_ARG;
     if (!g_rccl.init) return CF2_ERR_UNSUPPORTED;
     *out = nullptr;
     cf2_xchg* x = new cf2_xchg();
     x->world = world; x->rank = rank; x->depth = depth;
-    hipError_t e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
-    uint32_t made = 0;
-    for (; e == hipSuccess && made < depth; ++made) e = hipEventCreateWithFlags(&x->end[made], hipEventDisableTiming);
+    hipError_t e = hipGetDevice(&x->device);
+    // the exchange stream at the highest priority: streams of different priority get hardware
+    // queues of their own, so the exchange runs beside the env-steps instead of queued behind them
+    // (at equal priority it shared the env stream's queue: r05d trace)
+    int lo_prio = 0, hi_prio = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->xs, hipStreamNonBlocking, hi_prio);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
+    for (uint32_t k = 0; e == hipSuccess && k < depth; ++k)
+        e = hipEventCreateWithFlags(&x->free_[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x->end, hipEventDisableTiming);
     if (e != hipSuccess) {
-        for (uint32_t k = 0; k + 1 < made; ++k) (void)hipEventDestroy(x->end[k]);
-        if (made) (void)hipEventDestroy(x->fork);
+        xchg_free_events(x);
         delete x;
         return hip_fail(e);
     }
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
     if (g_rccl.init(&x->comm, (int)world, uid, (int)rank) != ncclSuccess) {
-        for (uint32_t k = 0; k < depth; ++k) (void)hipEventDestroy(x->end[k]);
-        (void)hipEventDestroy(x->fork);
+        xchg_free_events(x);
         delete x;
         return CF2_ERR_HIP;
     }
@@ -388,110 +454,172 @@ extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world,
 extern "C" int cf2_xchg_destroy(cf2_xchg* x) {
     if (!x) return CF2_OK;
     int st = CF2_OK;
-    for (uint32_t k = 0; k < x->npev; ++k) (void)hipEventDestroy(x->pev[k]);
+    (void)hipSetDevice(x->device);
+    (void)hipStreamSynchronize(x->xs);
     if (g_rccl.destroy && g_rccl.destroy(x->comm) != ncclSuccess) st = CF2_ERR_HIP;
-    for (uint32_t k = 0; k < x->depth; ++k) (void)hipEventDestroy(x->end[k]);
-    (void)hipEventDestroy(x->fork);
+    xchg_free_events(x);
     delete x;
     return st;
 }
 
-extern "C" int cf2_xchg_step(cf2_xchg* x, uint32_t slot, const float* obs_dev, const uint8_t* reset_dev, uint32_t n,
-                             uint32_t obs_len, uint32_t cap, uint32_t* send_dev, uint32_t* send_next_dev,
-                             uint32_t* recv_dev, const float* act_dev, const float* act_prev_dev, uint16_t* age_dev,
-                             const float* slab_prev_dev, float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age,
-                             uint32_t* pred_dev, uint32_t* pred_next_dev, void* env_stream, void* comm_stream) {
-    if (!x || slot >= x->depth || !recv_dev || !layout_ok(n, obs_len, cap)) return CF2_ERR_INVALID_ARG;
-    const hipStream_t cs = (hipStream_t)comm_stream;
-    hipError_t e = hipEventRecord(x->fork, (hipStream_t)env_stream);     // the env-step that wrote obs / done
-    if (e == hipSuccess) e = hipStreamWaitEvent(cs, x->fork, 0);
-    if (e != hipSuccess) return hip_fail(e);
-    int st = cf2_obs_pack(obs_dev, reset_dev, n, obs_len, cap, send_dev, send_next_dev, comm_stream);
-    if (st != CF2_OK) return st;
-    const size_t words = PackLayout{n, obs_len, cap}.words();
-    if (g_rccl.all_gather(send_dev, recv_dev, words, ncclUint32, x->comm, cs) != ncclSuccess) return CF2_ERR_HIP;
-    st = cf2_obs_unpack(recv_dev, x->world, n, obs_len, cap, act_dev, act_prev_dev, age_dev, slab_prev_dev, slab_dev,
-                        overflow_dev, watch_age, pred_dev, pred_next_dev, comm_stream);
-    if (st != CF2_OK) return st;
-    e = hipEventRecord(x->end[slot], cs);
-    if (e != hipSuccess) return hip_fail(e);
-    x->pending[slot] = x->recorded[slot] = true;
-    return CF2_OK;
+extern "C" size_t cf2_xchg_send_words(uint32_t n, uint32_t obs_len, uint32_t depth, uint32_t kmax) {
+    if (!layout_ok(n, obs_len, n) || depth < 2 || depth > XCHG_MAX_DEPTH || kmax == 0 || kmax > XCHG_MAX_BATCH) return 0;
+    return (size_t)depth * kmax * (PackLayout{n, obs_len, n}.words() + PACK_SCRATCH_WORDS);
 }
 
-extern "C" int cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream) {
-    if (!x || slot >= x->depth) return CF2_ERR_INVALID_ARG;
-    if (!x->recorded[slot]) return CF2_OK;
-    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->end[slot], 0);
-    return e == hipSuccess ? CF2_OK : hip_fail(e);
+extern "C" size_t cf2_xchg_recv_words(uint32_t n, uint32_t obs_len, uint32_t world, uint32_t depth, uint32_t kmax) {
+    if (!layout_ok(n, obs_len, n) || world == 0 || depth < 2 || depth > XCHG_MAX_DEPTH || kmax == 0 ||
+        kmax > XCHG_MAX_BATCH)
+        return 0;
+    return (size_t)depth * world * kmax * PackLayout{n, obs_len, n}.words();
 }
 
-extern "C" int cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, float* const* obs_dev,
-                                 uint8_t* const* reset_dev, uint32_t* const* send_dev, uint32_t* const* recv_dev,
-                                 float* slab0_dev, float* slab1_dev, uint16_t* age_dev, uint32_t* overflow_dev,
-                                 uint32_t* const* pred_dev, uint32_t npred, uint32_t* pred_host, uint32_t pred_batch,
-                                 uint32_t pred_events, void* comm_stream) {
-    if (!x || x->registered || !obs_dev || !reset_dev || !send_dev || !recv_dev || !slab0_dev || !slab1_dev ||
-        !age_dev || !layout_ok(n, obs_len, n) || npred > XCHG_MAX_PRED || pred_events > XCHG_MAX_PRED_EV ||
-        (watch_age != 0xFFFFFFFFu && (npred < 2 || !pred_dev)) ||
-        (pred_host && (watch_age == 0xFFFFFFFFu || pred_batch == 0 || pred_events == 0)))
+extern "C" int cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, uint32_t kmax,
+                                 float* const* obs_dev, uint8_t* const* reset_dev, uint32_t* send_dev,
+                                 uint32_t* recv_dev, uint16_t* age_dev, uint32_t* overflow_dev, uint32_t* pred_dev,
+                                 uint32_t npred) {
+    // npred: a consume writes the rows of its steps and zeroes the CONSUME_MAX rows after them
+    if (!x || x->registered || !obs_dev || !reset_dev || !send_dev || !recv_dev || !age_dev || kmax == 0 ||
+        kmax > XCHG_MAX_BATCH || !layout_ok(n, obs_len, n) || (uint64_t)x->world * n >= (1ull << 31) ||
+        npred > XCHG_MAX_PRED || (watch_age != 0xFFFFFFFFu && (npred < 2 * CONSUME_MAX + 1 || !pred_dev)))
         return CF2_ERR_INVALID_ARG;
-    for (uint32_t r = 1; r < npred; ++r)           // one [npred][world] array
-        if (pred_dev[r] != pred_dev[0] + (size_t)r * x->world) return CF2_ERR_INVALID_ARG;
-    if (pred_host) {
-        hipError_t e = hipSuccess;
-        for (; e == hipSuccess && x->npev < pred_events; ++x->npev)
-            e = hipEventCreateWithFlags(&x->pev[x->npev], hipEventDisableTiming);
-        if (e != hipSuccess) {
-            --x->npev;
-            for (uint32_t k = 0; k < x->npev; ++k) (void)hipEventDestroy(x->pev[k]);
-            x->npev = 0;
-            return hip_fail(e);
-        }
-    }
-    x->pred_host = pred_host;
-    x->pred_batch = pred_batch;
+    if (((uintptr_t)send_dev & 15u) || ((uintptr_t)recv_dev & 15u)) return CF2_ERR_INVALID_ARG;
     for (uint32_t j = 0; j < x->depth; ++j) {
-        if (!obs_dev[j] || !reset_dev[j] || !send_dev[j] || !recv_dev[j]) return CF2_ERR_INVALID_ARG;
-        x->obs[j] = obs_dev[j]; x->done[j] = reset_dev[j]; x->send[j] = send_dev[j]; x->recv[j] = recv_dev[j];
+        if (!obs_dev[j] || !reset_dev[j] || ((uintptr_t)obs_dev[j] & 15u)) return CF2_ERR_INVALID_ARG;
+        x->obs[j] = obs_dev[j]; x->done[j] = reset_dev[j];
     }
-    for (uint32_t r = 0; r < npred; ++r) x->pred[r] = pred_dev[r];
-    x->n = n; x->ol = obs_len; x->watch = watch_age; x->npred = npred;
-    x->slab[0] = slab0_dev; x->slab[1] = slab1_dev;
+    x->n = n; x->ol = obs_len; x->watch = watch_age; x->kmax = kmax;
+    x->wmax = PackLayout{n, obs_len, n}.words();
+    x->npred = watch_age != 0xFFFFFFFFu ? npred : 0u;
+    x->pred = watch_age != 0xFFFFFFFFu ? pred_dev : nullptr;
+    x->send = send_dev; x->recv = recv_dev;
     x->age = age_dev; x->overflow = overflow_dev;
-    x->comm_stream = (hipStream_t)comm_stream;
     x->registered = true;
     return CF2_OK;
 }
 
-extern "C" int cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, const float* act_dev,
-                                 const float* act_all_dev, const float* act_prev_all_dev, float* rew_dev,
-                                 uint8_t* trunc_dev, float* cost_dev, float* level_dev, void* env_stream) {
-    if (!x || !x->registered || !ctx) return CF2_ERR_INVALID_ARG;
-    const uint32_t j = (uint32_t)(k % x->depth);
-    const hipStream_t es = (hipStream_t)env_stream;
-    if (x->pending[j]) {                 // the exchange that last read buffer j
-        const hipError_t e = hipStreamWaitEvent(es, x->end[j], 0);
-        if (e != hipSuccess) return hip_fail(e);
-        x->pending[j] = false;
+static uint32_t* xchg_send(const cf2_xchg* x, uint32_t q) { return x->send + (size_t)q * x->kmax * x->wmax; }
+static uint32_t* xchg_recv(const cf2_xchg* x, uint32_t q) { return x->recv + (size_t)q * x->world * x->kmax * x->wmax; }
+static uint32_t* xchg_scratch(const cf2_xchg* x, uint32_t q, uint32_t s) {
+    return x->send + (size_t)x->depth * x->kmax * x->wmax + ((size_t)q * x->kmax + s) * PACK_SCRATCH_WORDS;
+}
+
+// the receivers' work of the nb steps k0 .. of one batch in region q (capacity cap), consume
+// launches of up to CONSUME_MAX steps on the exchange stream
+static int xchg_consume(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint32_t cap) {
+    const PackLayout L{x->n, x->ol, cap};
+    const uint32_t words = L.words();
+    for (uint32_t s0 = 0; s0 < nb; s0 += CONSUME_MAX) {
+        ConsumeSteps S;
+        memset(&S, 0, sizeof(S));
+        S.steps = nb - s0 < CONSUME_MAX ? nb - s0 : CONSUME_MAX;
+        for (uint32_t s = 0; s < S.steps; ++s) {
+            S.pk[s] = xchg_recv(x, q) + (size_t)(s0 + s) * words;
+            S.words[s] = nb * words;                    // rank stride of the batch's [world][nb][words] layout
+            if (x->pred) S.pred[s] = x->pred + (size_t)((k0 + s0 + s) % x->npred) * x->world;
+        }
+        const uint64_t k1 = k0 + s0 + S.steps - 1;
+        if (x->pred)
+            for (uint32_t z = 0; z < CONSUME_MAX; ++z) S.zero[z] = x->pred + (size_t)((k1 + 1 + z) % x->npred) * x->world;
+        const int st = consume_launch(S, x->world, L, x->age, x->overflow, x->watch, x->xs);
+        if (st != CF2_OK) return st;
     }
-    int st = cf2_step(ctx, act_dev, nullptr, x->obs[j], rew_dev, x->done[j], trunc_dev, cost_dev, level_dev, nullptr,
-                      env_stream);
+    return CF2_OK;
+}
+
+// after the env stream's work so far: the all-gather of region q's batch (nb packed buffers at cap),
+// the receivers' work, the look-ahead ring to pred_host (optional), region q's free event
+static int xchg_exchange(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint32_t cap, hipStream_t es,
+                         uint32_t* pred_host) {
+    hipError_t e = hipEventRecord(x->fork, es);
+    if (e == hipSuccess) e = hipStreamWaitEvent(x->xs, x->fork, 0);
+    if (e != hipSuccess) return hip_fail(e);
+    const size_t words = PackLayout{x->n, x->ol, cap}.words();
+    if (g_rccl.all_gather(xchg_send(x, q), xchg_recv(x, q), nb * words, ncclUint32, x->comm, x->xs) != ncclSuccess)
+        return CF2_ERR_HIP;
+    e = hipEventRecord(x->free_[q], x->xs);
+    if (e != hipSuccess) return hip_fail(e);
+    int st = xchg_consume(x, k0, nb, q, cap);
     if (st != CF2_OK) return st;
-    const bool w = x->watch != 0xFFFFFFFFu;
-    st = cf2_xchg_step(x, j, x->obs[j], x->done[j], x->n, x->ol, cap, x->send[j], x->send[(j + 1) % x->depth],
-                       x->recv[j], act_all_dev, act_prev_all_dev, x->age, x->slab[(k + 1) % 2], x->slab[k % 2],
-                       x->overflow, x->watch, w ? x->pred[k % x->npred] : nullptr,
-                       w ? x->pred[(k + 1) % x->npred] : nullptr, env_stream, x->comm_stream);
-    if (st != CF2_OK || !x->pred_host || k % x->pred_batch) return st;
-    hipError_t e = hipMemcpyAsync(x->pred_host, x->pred[0], (size_t)x->npred * x->world * sizeof(uint32_t),
-                                  hipMemcpyDeviceToHost, x->comm_stream);
-    if (e == hipSuccess) e = hipEventRecord(x->pev[(k / x->pred_batch) % x->npev], x->comm_stream);
+    if (pred_host && x->pred) {
+        e = hipMemcpyAsync(pred_host, x->pred, (size_t)x->npred * x->world * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           x->xs);
+        if (e != hipSuccess) return hip_fail(e);
+    }
+    e = hipEventRecord(x->end, x->xs);
+    if (e != hipSuccess) return hip_fail(e);
+    x->free_rec[q] = x->end_rec = true;
+    return CF2_OK;
+}
+
+static int xchg_take_region(cf2_xchg* x, uint32_t region, hipStream_t es) {
+    if (region != x->next_region % x->depth) return CF2_ERR_INVALID_ARG;     // the caller lost count
+    ++x->next_region;
+    if (!x->free_rec[region]) return CF2_OK;
+    const hipError_t e = hipStreamWaitEvent(es, x->free_[region], 0);     // the all-gather that last read it
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
-extern "C" int cf2_xchg_pred_sync(cf2_xchg* x, uint64_t k) {
-    if (!x || !x->pred_host || k % x->pred_batch) return CF2_ERR_INVALID_ARG;
-    const hipError_t e = hipEventSynchronize(x->pev[(k / x->pred_batch) % x->npev]);
+extern "C" int cf2_xchg_publish(cf2_xchg* x, uint64_t k, uint32_t cap, uint32_t region, void* env_stream) {
+    if (!x || !x->registered || !layout_ok(x->n, x->ol, cap) || region >= x->depth) return CF2_ERR_INVALID_ARG;
+    if (region != x->next_region % x->depth) return CF2_ERR_INVALID_ARG;
+    const hipStream_t es = (hipStream_t)env_stream;
+    ++x->next_region;
+    // the caller's env-step wrote obs / done of the region (after cf2_xchg_wait_free): pack it here
+    int st = cf2_obs_pack(x->obs[region], x->done[region], x->n, x->ol, cap, xchg_send(x, region),
+                          xchg_scratch(x, region, 0), xchg_scratch(x, (uint32_t)(x->next_region % x->depth), 0), es);
+    if (st != CF2_OK) return st;
+    return xchg_exchange(x, k, 1, region, cap, es, nullptr);
+}
+
+extern "C" int cf2_xchg_wait_free(cf2_xchg* x, uint32_t region, void* stream) {
+    if (!x || region >= x->depth) return CF2_ERR_INVALID_ARG;
+    if (!x->free_rec[region]) return CF2_OK;
+    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->free_[region], 0);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_xchg_wait(cf2_xchg* x, void* stream) {
+    if (!x) return CF2_ERR_INVALID_ARG;
+    if (!x->end_rec) return CF2_OK;
+    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->end, 0);
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
+                            const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev,
+                            float* cost_dev, float* level_dev, uint32_t* pred_host, void* env_stream) {
+    if (!x || !x->registered || !ctx || !act_dev || nact == 0 || nb == 0 || nb > x->kmax || region >= x->depth ||
+        !layout_ok(x->n, x->ol, cap) || !rew_dev)
+        return CF2_ERR_INVALID_ARG;
+    for (uint32_t a = 0; a < nact; ++a)
+        if (!act_dev[a] || ((uintptr_t)act_dev[a] & 15u)) return CF2_ERR_INVALID_ARG;
+    const hipStream_t es = (hipStream_t)env_stream;
+    int st = xchg_take_region(x, region, es);
+    if (st != CF2_OK) return st;
+    const uint32_t q = region, qn = (uint32_t)(x->next_region % x->depth);
+    const uint32_t words = PackLayout{x->n, x->ol, cap}.words();
+    for (uint32_t s = 0; s < nb; ++s) {
+        const uint64_t k = k0 + s;
+        uint32_t* pk = xchg_send(x, q) + (size_t)s * words;
+        uint32_t* scr = xchg_scratch(x, q, s);
+        uint32_t* scr_next = s + 1 < nb ? xchg_scratch(x, q, s + 1) : xchg_scratch(x, qn, 0);
+        const float* act = act_dev[k % nact];
+        st = cf2_step_packed(ctx, act, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr,
+                             scr_next, cap, es);
+        if (st == CF2_ERR_UNSUPPORTED) {      // larger contexts: the env-step, then the pack, in order
+            st = cf2_step(ctx, act, nullptr, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, nullptr,
+                          es);
+            if (st == CF2_OK) st = cf2_obs_pack(x->obs[q], x->done[q], x->n, x->ol, cap, pk, scr, scr_next, es);
+        }
+        if (st != CF2_OK) return st;
+    }
+    return xchg_exchange(x, k0, nb, q, cap, es, pred_host);
+}
+
+extern "C" int cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, uint32_t region,
+                                 const float* act_dev, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
+                                 float* level_dev, void* env_stream) {
+    return cf2_xchg_run(x, ctx, k, 1, cap, region, &act_dev, 1, rew_dev, trunc_dev, cost_dev, level_dev, nullptr,
+                        env_stream);
 }

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "cf2sim_pack.h"
 
 namespace cf2 {
 
@@ -142,6 +143,9 @@ int hip_fail(hipError_t e);
 // fills P.rb_* for the kernel instances P dispatches to, on the current device
 hipError_t query_occupancy(KParams& P);
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
+// the env-step with the delta exchange's pack of its observations fused in (step_kernel_small's
+// epilogue); hipErrorNotSupported above SMALL_N_MAX envs (the caller then packs separately)
+hipError_t launch_step_packed(const KParams& P, const StepIO& io, const PackIO& pio, hipStream_t s);
 // The collect loop's policy half, fused behind the env-step (collect_kernel): the actor-critic
 // forward on the new observations (packed bf16x3 fragments of cf2_policy_pack, obs_dim 34)
 struct PolicyIO {

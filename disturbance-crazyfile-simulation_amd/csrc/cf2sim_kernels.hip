@@ -2039,6 +2039,56 @@ __global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) collect_kernel(KPa
 enum { SEED_SMALL = 10 };   // per finished env, wave 0 -> waves 1-3: final body rates, gyro bias, OU state
 enum { C2_WORDS = 9 };      // per env, wave 3 -> wave 2: the second reset sensor call's gyro normals
 
+// The delta exchange's pack fused into the small-N env-step (cf2_step_packed; the layout and the
+// side-slot allocation are cf2sim_pack.h's, the standalone form is obs_pack_kernel): wave 2, once the
+// block's rows are final in LDS (s_obs, or s_rrow where the env reset), writes the block's o_k run,
+// its two bitmap words, its block-table word and its resets' side entries.  The packed buffer is
+// then ready for the all-gather when the env-step kernel ends: no pack kernel, no re-read of the
+// observation rows.  The block's side slots (first: pack_alloc, a memory-side atomic) are asked for
+// as soon as the block knows its resets, so the atomic's round trip overlaps the reset tail.
+template <uint32_t OL, uint32_t OD>
+__device__ __forceinline__ void pack_epilogue(const PackIO& X, uint32_t n, uint32_t base, uint32_t nvalid,
+                                              uint64_t mask, const float* s_obs, const float* s_rrow, uint32_t lane,
+                                              uint32_t first) {
+    typedef float f4x __attribute__((ext_vector_type(4)));
+    const PackLayout L{n, OL, X.cap};
+    uint32_t* pk = X.pk;
+    if (blockIdx.x == 0) {
+        if (lane == 0) { pk[0] = 0u; pk[1] = n; pk[2] = OL; pk[3] = X.cap; }
+        if (X.next_scratch)
+            for (uint32_t k = lane; k < PACK_SCRATCH_WORDS; k += 64u) X.next_scratch[k] = 0u;
+    }
+    float* dst = reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * OL;
+    auto ok_word = [&](uint32_t f) {     // word f of the block's o_k run
+        const uint32_t r = f / OL, c = f - r * OL;
+        return (((mask >> r) & 1ull) ? s_rrow : s_obs)[r * OD + OL + 4u + c];
+    };
+    if (nvalid == 64u && ((uintptr_t)dst & 15u) == 0) {
+        f4x* d4 = reinterpret_cast<f4x*>(dst);
+        for (uint32_t c = lane; c < 64u * OL / 4u; c += 64u) {
+            f4x v;
+#pragma unroll
+            for (uint32_t e = 0; e < 4u; ++e) v[e] = ok_word(4u * c + e);
+            d4[c] = v;
+        }
+    } else {
+        for (uint32_t f = lane; f < nvalid * OL; f += 64u) dst[f] = ok_word(f);
+    }
+    uint32_t* bits = pk + L.bits();
+    if (lane == 0) bits[base / 32u] = (uint32_t)mask;
+    if (lane == 1 && base + 32u < n) bits[base / 32u + 1u] = (uint32_t)(mask >> 32);
+    first = __shfl(first, 0);          // lane 0's pack_alloc, issued right after the block barrier
+    if (lane == 0) pk[L.btab() + base / XB_PACK] = first;
+    if (((mask >> lane) & 1ull) && first != PACK_DROPPED) {
+        uint32_t* e = pk + L.side() + (first + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull))) * L.entry();
+        e[0] = base + lane;
+        const float* row = s_rrow + lane * OD;
+        float* ef = reinterpret_cast<float*>(e + 1);
+#pragma unroll
+        for (uint32_t k = 0; k < OL + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
+    }
+}
+
 // The small-N kernel's LDS arrays (step_kernel_small declares them; collect_kernel_small carves
 // them out of a buffer the policy fragments re-use afterwards)
 template <bool NOISE, int SPEC>
@@ -2060,7 +2110,7 @@ struct SmallLds {
 template <bool NOISE, bool DR, int PHYS, int SPEC>
 __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& io, float* s_obs, float* s_seed,
                                                float* s_c2, float* s_rrow, uint32_t* s_mask, double* s_hjgrid,
-                                               float* s_draw, float* s_pose) {
+                                               float* s_draw, float* s_pose, const PackIO& X = PackIO{}) {
     const KParams P = shape_view<SPEC>(P0);
     using SL = SmallLds<NOISE, SPEC>;
     constexpr int OL = SL::OL;
@@ -2216,6 +2266,9 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     TSTAMP(4);   // block barrier passed
     const uint64_t mask = ((uint64_t)s_mask[1] << 32) | (uint64_t)s_mask[0];
     const bool mine = wave != 0 && ((mask >> lane) & 1ull);
+    uint32_t pk_first = 0u;          // fused pack: the block's first side slot (wave 2, lane 0)
+    if (X.pk && wave == 2 && lane == 0 && mask)
+        pk_first = pack_alloc(PackLayout{P.N, (uint32_t)OL, X.cap}, X.scratch, (uint32_t)__popcll(mask));
     if (mine) {
         TSTAMP(6);
         if (wave == 1) {
@@ -2268,7 +2321,10 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     // 256-thread merged write-out: see DESIGN.md section 3).
     const uint32_t nvalid = P.N - base < 64u ? P.N - base : 64u;
     if (wave == 0) write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, false);
-    else if (wave == 2) write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, true);
+    else if (wave == 2) {
+        write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, true);
+        if (X.pk) pack_epilogue<OL, OD>(X, P.N, base, nvalid, mask, s_obs, s_rrow, lane, pk_first);
+    }
     TSTAMP(12);  // rows written
 #ifdef CF2_TIMING
     TSTAMP(5);
@@ -2279,7 +2335,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
 }
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
-__global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO io) {
+__global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO io, PackIO X) {
     using SL = SmallLds<NOISE, SPEC>;
     __shared__ __align__(16) float s_obs[64 * SL::OD];     // the block's obs rows, global layout
     __shared__ float s_seed[SEED_SMALL * 64];              // [word][env]
@@ -2289,7 +2345,7 @@ __global__ void __launch_bounds__(256, 2) step_kernel_small(KParams P0, StepIO i
     __shared__ double s_hjgrid[6 * HJ_PTS];
     __shared__ float s_draw[SL::HD ? HD_WORDS * 64 : 1];
     __shared__ float s_pose[SL::HD ? SL::POSE_WORDS * 64 : 1];
-    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw, s_pose);
+    (void)small_body<NOISE, DR, PHYS, SPEC>(P0, io, s_obs, s_seed, s_c2, s_rrow, s_mask, s_hjgrid, s_draw, s_pose, X);
 }
 
 // The fused collect step at small N (N <= 32 768: the 8-GPU node shard, C2): step_kernel_small's
@@ -3049,15 +3105,16 @@ static hipError_t occupancy_t(KParams& P) {
 }
 
 template <bool NOISE, bool DR, int PHYS, int SPEC>
-static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s) {
+static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t s, const PackIO& X = PackIO{}) {
     // small N (<= 32768 envs: at most one 64-env wave per two SIMDs with the helpers) runs 64 envs
     // per block, the other three waves computing the envs' potential resets meanwhile
     // (step_kernel_small); above that the helper waves would cost residency (65 536 envs: 15.5 ->
     // 24.7 us with 64-env blocks)
     if (P.N <= SMALL_N_MAX) {
-        hipLaunchKernelGGL((step_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s, P, io);
+        hipLaunchKernelGGL((step_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s, P, io, X);
         return hipGetLastError();
     }
+    if (X.pk) return hipErrorNotSupported;     // the fused pack is step_kernel_small's
     const dim3 grid((P.N + STEP_BLOCK - 1) / STEP_BLOCK), block(STEP_BLOCK);
     KParams Pl = P;
     Pl.late_block = P.rb_step;
@@ -3248,6 +3305,10 @@ extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
 #endif
 hipError_t query_occupancy(KParams& P) { CF2_DISPATCH(occupancy_t, P); }
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
+hipError_t launch_step_packed(const KParams& P, const StepIO& io, const PackIO& pio, hipStream_t s) {
+    if (P.N > SMALL_N_MAX) return hipErrorNotSupported;
+    CF2_DISPATCH(launch_step_t, P, io, s, pio);
+}
 hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {
     CF2_DISPATCH(launch_rollout_t, P, io, K, act_stride, s);
 }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define CF2SIM_ABI_VERSION 7
+#define CF2SIM_ABI_VERSION 8
 
 typedef enum cf2_status {
     CF2_OK = 0,
@@ -335,72 +335,92 @@ int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev,
 
 /* Multi-GPU observation exchange as deltas (the north star's per-step RCCL
  * all-gather of the obs slab).  The reference has no counterpart: its MPI ranks exchange only
- * gradients and statistics (utils/mpi_tools.py:30-44); the rows rebuilt here are exactly what
+ * gradients and statistics (utils/mpi_tools.py:30-44); the rows materialised here are exactly what
  * compute_history (envs/base.py:305-321) returns on every rank.
  * A row is [o_{k-1}, A0, o_k, A1] (obs_len OL = 13 with sensor noise, 17 without); per env-step a
  * rank packs only o_k of every env, a bitmap of the envs that auto-reset and, for up to `cap` of
  * them, the reset row's o_0 and action part, into cf2_obs_packed_words(n, OL, cap) 32-bit words
  * (a multiple of 4).  After an all-gather of the packed buffers ([world][words], rank order,
- * equal shards of n envs), cf2_obs_unpack rebuilds every rank's rows from the previous slab
- * [world n, 2 OL + 8] and the actions of the step (act [world n, 4]) and of the step before
- * (act_prev), tracking each env's steps since its reset in age_dev (uint16 [world n], saturating;
- * all 0 after the slab came from a full gather right after a reset of every env).  Time-out
- * look-ahead: envs whose age becomes watch_age this step (max_episode_steps - L; 0xFFFFFFFF: off)
- * are counted per rank into pred_dev[world] (pred_next_dev[world] is zeroed for the next step):
- * at most that many envs time out L steps later, so the caller can size that step's cap.  Valid under auto-reset for
- * env-step shapes whose action buffer holds only the step's action after a step
- * (aggregate_phy_steps a multiple of buf_size, latency on: the reference's default).  More than
- * cap resets on a rank in one step: those rows' o_0 / A parts become NaN and *overflow_dev is
- * incremented; later rows are exact again.  clear_next_dev: the count word (word 0) of the buffer
- * the next pack on this stream will write (or NULL: the caller zeroes it). */
+ * equal shards of n envs) a receiver keeps them and only advances every env's steps since its
+ * reset (cf2_obs_consume: age_dev uint16 [world n], saturating; all 0 after the observations came
+ * from a full gather right after a reset of every env).  Rows are materialised on request
+ * (cf2_obs_rows) from the gathered buffers of step k (capacity cap) and k - 1 (cap_prev), the ages
+ * after step k's consume and the actions of steps k, k - 1 and k - 2 (act, act_prev, act_prev2:
+ * [world n, 4]); out gets rows [row0, row0 + nrows) as [nrows, 2 OL + 8].  Rank r's packed buffer
+ * is at r * stride words (0: cf2_obs_packed_words(n, OL, cap), the all-gather of one step).  Time-out look-ahead:
+ * envs whose age becomes watch_age at a consume (max_episode_steps - L; 0xFFFFFFFF: off) are
+ * counted per rank into pred_dev[world] (pred_next_dev[world], a different row, is zeroed for the
+ * next step): at most that many envs time out L steps later, so the caller can size that step's
+ * cap.  Valid under auto-reset for env-step shapes whose action buffer holds only the step's action
+ * after a step (aggregate_phy_steps a multiple of buf_size, latency on: the reference's default).
+ * Side slots go to 64-env pack blocks, never to single envs (layout and allocation:
+ * csrc/cf2sim_pack.h); a block whose resets find no room in the side slab (an overflow) is marked
+ * dropped: exactly its reset rows have NaN in their o_0 / A parts, *overflow_dev counts the dropped
+ * blocks, every other row and all o_k parts stay exact, and later steps are exact again.  A pack
+ * counts side slots in scratch_dev (PACK_SCRATCH_WORDS = 288 words, zeroed before the pack) and
+ * zeroes next_scratch_dev (the counters of the next pack on its stream; or NULL). */
 size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t cap);
 int  cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
-                  uint32_t* packed_dev, uint32_t* clear_next_dev, void* stream);
-int  cf2_obs_unpack(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len, uint32_t cap,
-                    const float* act_dev, const float* act_prev_dev, uint16_t* age_dev, const float* slab_prev_dev,
-                    float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
-                    uint32_t* pred_next_dev, void* stream);
+                  uint32_t* packed_dev, uint32_t* scratch_dev, uint32_t* next_scratch_dev, void* stream);
+/* The env-step (cf2_step's outputs, no final_obs) with the pack of its observations fused in:
+ * step_kernel_small writes packed_dev (cf2_obs_packed_words(N, OL, cap) words) as cf2_obs_pack
+ * would, from the rows it has in LDS, so no pack launch re-reads them.  scratch_dev: this buffer's
+ * side-slot counters (PACK_SCRATCH_WORDS = 288 words), zeroed by the previous pack; next_scratch_dev: the counters the next pack uses, zeroed here (or
+ * NULL).  N <= 32 768 envs (the 8-GPU node shard); larger contexts return CF2_ERR_UNSUPPORTED and
+ * launch nothing (call cf2_step and cf2_obs_pack). */
+int  cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
+                     uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* packed_dev, uint32_t* scratch_dev,
+                     uint32_t* next_scratch_dev, uint32_t cap, void* stream);
+int  cf2_obs_consume(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len, uint32_t cap,
+                     uint16_t* age_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
+                     uint32_t* pred_next_dev, void* stream);
+int  cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride, const uint32_t* packed_prev_all_dev,
+                  uint32_t cap_prev, uint32_t stride_prev, uint32_t world, uint32_t n, uint32_t obs_len,
+                  const uint16_t* age_dev, const float* act_dev, const float* act_prev_dev, const float* act_prev2_dev,
+                  uint32_t row0, uint32_t nrows, float* rows_dev, void* stream);
 
-/* The same exchange driven natively, one call per env-step: an RCCL communicator of this library's
- * own (one rank per GPU, created on the current device) and, per step, pack -> ncclAllGather of the
- * packed words -> rebuild, on comm_stream after env_stream's work so far (an event fork), ending
- * with an event of slot `slot` (< depth) that cf2_xchg_wait makes a stream wait for.  What the
- * host would otherwise do per step with three launches, a process-group all-gather and stream /
- * event calls (~65 us of host time at the node shard) is one C call.
- * cf2_xchg_bind: the RCCL library to use (NULL: "librccl.so.1"); an instance the process has
- * already loaded (e.g. PyTorch's) is reused.  cf2_xchg_unique_id: on one rank, the 128-byte id
- * every rank passes to cf2_xchg_create (collective: all ranks call it together).  The arguments of
- * cf2_xchg_step are those of cf2_obs_pack and cf2_obs_unpack; recv_dev holds world x
- * cf2_obs_packed_words(n, obs_len, cap) words.  RCCL failures return CF2_ERR_HIP. */
+/* The same exchange driven natively: an RCCL communicator of this library's own (one rank per GPU,
+ * created on the current device, with an exchange stream of its own) and, per batch of env-steps,
+ * one ncclAllGather of the batch's packed buffers and one consume on the exchange stream after the
+ * env stream's work so far.  cf2_xchg_bind: the RCCL library to use (NULL: "librccl.so.1"); an
+ * instance the process has already loaded (e.g. PyTorch's) is reused.  cf2_xchg_unique_id: on one
+ * rank, the 128-byte id every rank passes to cf2_xchg_create (collective: all ranks call it
+ * together; depth 2..8 buffer regions).  cf2_xchg_register: the buffers, once: obs [n, 2 OL + 8] /
+ * reset uint8 [n] per region (depth each), send (cf2_xchg_send_words, zeroed) and recv
+ * (cf2_xchg_recv_words) for batches of up to kmax env-steps, age [world n], overflow, pred (the
+ * look-ahead ring [npred][world], used when watch_age is on; npred >= 17).  Every publish / batch
+ * takes the next region (0, 1, ..., depth - 1, 0, ...; `region` must name it: the caller keeps the
+ * count) and first makes env_stream wait for the all-gather that last read that region.  A batch of
+ * nb steps at capacity cap leaves recv region q as [world][nb][cf2_obs_packed_words(n, OL, cap)]:
+ * the packed buffer of its step s for rank r at (r * nb + s) * words, i.e. cf2_obs_rows with
+ * stride nb * words.
+ * cf2_xchg_publish(x, k, cap, region, env_stream): the exchange of env-step k, whose env-step the
+ * caller issued on env_stream into obs / reset of `region` (after cf2_xchg_wait_free(x, region,
+ * env_stream)); packs it on env_stream.  cf2_xchg_run: env-steps k0 .. k0 + nb - 1 of ctx (nb <=
+ * kmax; actions of step k at act_dev[k % nact]) issued back to back on env_stream with their pack
+ * fused in (cf2_step_packed; larger contexts pack after each env-step), then the batch's exchange at
+ * capacity cap; pred_host (pinned, npred x world words, or NULL) receives the look-ahead ring after
+ * the batch's consume.  cf2_xchg_env_step: cf2_xchg_run of one step.  cf2_xchg_wait(x, stream): a
+ * stream waits until every exchange issued so far is complete.  RCCL failures return CF2_ERR_HIP. */
 typedef struct cf2_xchg cf2_xchg;
 int  cf2_xchg_bind(const char* rccl_path);
 int  cf2_xchg_unique_id(uint8_t* id_out, size_t id_len);
 int  cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world, uint32_t rank, uint32_t depth,
                      cf2_xchg** out);
 int  cf2_xchg_destroy(cf2_xchg* x);
-int  cf2_xchg_step(cf2_xchg* x, uint32_t slot, const float* obs_dev, const uint8_t* reset_dev, uint32_t n,
-                   uint32_t obs_len, uint32_t cap, uint32_t* send_dev, uint32_t* send_next_dev, uint32_t* recv_dev,
-                   const float* act_dev, const float* act_prev_dev, uint16_t* age_dev, const float* slab_prev_dev,
-                   float* slab_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
-                   uint32_t* pred_next_dev, void* env_stream, void* comm_stream);
-int  cf2_xchg_wait(cf2_xchg* x, uint32_t slot, void* stream);
-/* Registered form: the exchange's buffers set once (obs / reset / send / recv: depth each; slab0,
- * slab1; pred: npred rows of world counters, one [npred][world] array, the look-ahead ring, when
- * watch_age is on), then one call per env-step k runs the env-step of ctx into obs[k % depth] /
- * reset[k % depth] (cf2_step with the given reward / truncation / cost / level outputs; it first
- * waits for the exchange that last read that buffer) and that step's exchange into slab[k % 2]
- * from slab[(k + 1) % 2].  pred_host (pinned, npred x world words; or NULL): every pred_batch
- * env-steps the call also copies the whole ring there, followed by an event of a ring of
- * pred_events; cf2_xchg_pred_sync(x, k) waits on the host for the copy made at step k. */
-int  cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, float* const* obs_dev,
-                       uint8_t* const* reset_dev, uint32_t* const* send_dev, uint32_t* const* recv_dev,
-                       float* slab0_dev, float* slab1_dev, uint16_t* age_dev, uint32_t* overflow_dev,
-                       uint32_t* const* pred_dev, uint32_t npred, uint32_t* pred_host, uint32_t pred_batch,
-                       uint32_t pred_events, void* comm_stream);
-int  cf2_xchg_pred_sync(cf2_xchg* x, uint64_t k);
-int  cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, const float* act_dev,
-                       const float* act_all_dev, const float* act_prev_all_dev, float* rew_dev, uint8_t* trunc_dev,
-                       float* cost_dev, float* level_dev, void* env_stream);
+size_t cf2_xchg_send_words(uint32_t n, uint32_t obs_len, uint32_t depth, uint32_t kmax);
+size_t cf2_xchg_recv_words(uint32_t n, uint32_t obs_len, uint32_t world, uint32_t depth, uint32_t kmax);
+int  cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch_age, uint32_t kmax,
+                       float* const* obs_dev, uint8_t* const* reset_dev, uint32_t* send_dev, uint32_t* recv_dev,
+                       uint16_t* age_dev, uint32_t* overflow_dev, uint32_t* pred_dev, uint32_t npred);
+int  cf2_xchg_publish(cf2_xchg* x, uint64_t k, uint32_t cap, uint32_t region, void* env_stream);
+int  cf2_xchg_wait_free(cf2_xchg* x, uint32_t region, void* stream);
+int  cf2_xchg_wait(cf2_xchg* x, void* stream);
+int  cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
+                  const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
+                  float* level_dev, uint32_t* pred_host, void* env_stream);
+int  cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, uint32_t region, const float* act_dev,
+                       float* rew_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, void* env_stream);
 
 /* Measurement support (no reference counterpart): streaming kernels over `bytes` (a multiple of
  * 16, both pointers 16-B aligned) with non-temporal accesses.  mode 0: copy src -> dst; mode 1:

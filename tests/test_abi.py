@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_config_struct_matches(lib):
     from cf2sim.config import CF2Config
     assert lib.cf2_config_sizeof() == ctypes.sizeof(CF2Config)
-    assert lib.cf2_abi_version() == 7
+    assert lib.cf2_abi_version() == 8
 
 
 def test_status_strings_and_invalid_args(lib):
@@ -118,11 +118,25 @@ def test_kernel_sources_hold_no_ab_branches():
 
 
 def test_obs_exchange_error_paths(lib):
-    """cf2_obs_pack / cf2_obs_unpack reject bad sizes and pointers without launching anything."""
+    """cf2_obs_pack / cf2_obs_consume / cf2_obs_rows / cf2_xchg_* reject bad sizes and pointers
+    without launching anything (no GPU needed)."""
     from cf2sim.dist import packed_words
     assert lib.cf2_obs_packed_words(32768, 13, 2458) == packed_words(32768, 13, 2458)
     assert lib.cf2_obs_packed_words(5, 17, 3) == packed_words(5, 17, 3)
     assert lib.cf2_obs_packed_words(0, 13, 0) == 0 and lib.cf2_obs_packed_words(8, 12, 1) == 0
     assert lib.cf2_obs_packed_words(8, 13, 9) == 0                      # cap > n
-    assert lib.cf2_obs_pack(None, None, 8, 13, 1, None, None, None) == -1
-    assert lib.cf2_obs_unpack(None, 1, 8, 13, 1, None, None, None, None, None, None, 0, None, None, None) == -1
+    assert lib.cf2_obs_pack(None, None, 8, 13, 1, None, None, None, None) == -1
+    assert lib.cf2_step_packed(*([None] * 11), 1, None) == -1
+    w = lib.cf2_obs_packed_words(32768, 13, 32768)
+    assert lib.cf2_xchg_send_words(32768, 13, 2, 16) == 2 * 16 * (w + 288)
+    assert lib.cf2_xchg_recv_words(32768, 13, 8, 2, 16) == 2 * 8 * 16 * w
+    assert lib.cf2_xchg_send_words(32768, 13, 1, 16) == 0 and lib.cf2_xchg_recv_words(32768, 13, 8, 2, 65) == 0
+    assert lib.cf2_obs_consume(None, 1, 8, 13, 1, None, None, 0, None, None, None) == -1
+    assert lib.cf2_obs_rows(None, 1, 0, None, 1, 0, 1, 8, 13, None, None, None, None, 0, 8, None, None) == -1
+    # depth 1 would let a pack clear its own count word: refused before any RCCL call
+    h = ctypes.c_void_p()
+    idb = (ctypes.c_uint8 * 128)()
+    assert lib.cf2_xchg_create(idb, 128, 1, 0, 1, ctypes.byref(h)) == -1
+    assert lib.cf2_xchg_create(idb, 128, 1, 0, 9, ctypes.byref(h)) == -1
+    assert lib.cf2_xchg_publish(None, 0, 1, 0, None) == -1 and lib.cf2_xchg_wait(None, None) == -1
+    assert lib.cf2_xchg_run(None, None, 0, 8, 1, 0, None, 1, None, None, None, None, None, None) == -1

@@ -1,10 +1,11 @@
-"""Delta observation exchange (cf2sim.dist: pack_obs / unpack_obs / PipelinedObsGather(delta=True),
-the protocol of csrc/cf2sim_exchange.hip) on CPU: two gloo ranks step their shards of the CPU
-restatement (oracle/, which the HIP kernel matches step for step, tests/test_gpu_parity.py) and
-exchange only o_k, a reset bitmap and the reset rows' o_0 / action parts; the slab every rank
-rebuilds must equal the full all-gather of the obs rows bit for bit, over >= 200 env-steps with
-auto-resets and time-outs.  A side slab too small for a step's resets marks exactly those rows
-(NaN in their o_0 / action parts), counts the overflow, and the following steps are exact again."""
+"""Delta observation exchange (cf2sim.dist: pack_obs / consume_obs / obs_rows /
+PipelinedObsGather(delta=True), the protocol of csrc/cf2sim_exchange.hip) on CPU: two gloo ranks
+step their shards of the CPU restatement (oracle/, which the HIP kernel matches step for step,
+tests/test_gpu_parity.py) and exchange only o_k, a reset bitmap and the reset rows' o_0 / action
+parts; the rows every rank materialises from what it gathered must equal the full all-gather of the
+obs rows bit for bit, over >= 200 env-steps with auto-resets and time-outs.  A side slab too small
+for a step's resets marks exactly the reset rows of the overflowing rank (NaN in their o_0 / action
+parts), counts the overflow, and the following steps are exact again."""
 import os
 import socket
 
@@ -51,14 +52,16 @@ def _worker(rank, world, port, out_dir, cap):
     slab = pipe.start(obs0)
     full = gather_rows(obs0, sizes=[n] * world)
     assert torch.equal(slab, full)
-    mismatch, nan_rows, resets = [], [], 0
-    a_prev = torch.from_numpy(_actions(0, N))
+    mismatch, nan_rows, resets, exact_resets = [], [], 0, []
+    acts = [torch.from_numpy(_actions(t, N)) for t in range(T)]
+    ol = od // 2 - 4
     for t in range(T):
-        a = torch.from_numpy(_actions(t, N))
+        a = acts[t]
         o, r, d, _ = env.step(a[off:off + n].numpy())
         pipe.buffer().copy_(torch.from_numpy(o.astype(np.float32)))
         pipe.done_buffer().copy_(torch.from_numpy(d.astype(np.uint8)))
-        slab = pipe.publish(a, a_prev if t > 0 else a)
+        assert pipe.publish() == t
+        slab = pipe.rows(a, acts[max(t - 1, 0)], acts[max(t - 2, 0)])
         full = gather_rows(torch.from_numpy(o.astype(np.float32)), sizes=[n] * world)
         dall = gather_rows(torch.from_numpy(d.astype(np.uint8)), sizes=[n] * world).bool()
         resets += int(dall.sum())
@@ -67,15 +70,24 @@ def _worker(rank, world, port, out_dir, cap):
             if bad.any():
                 mismatch.append((t, torch.nonzero(bad).flatten().tolist()[:5]))
         else:
-            # only reset rows of an overflowing step may differ, and only as NaN in their o_0 / A parts
+            # NaN only in reset rows, only in their o_0 / A parts, only on a rank with more resets
+            # than its side slab holds (the blocks that found no room); every other value is exact
             nan = torch.isnan(slab).any(dim=1)
-            assert bool((bad <= (nan & dall)).all()), (t, torch.nonzero(bad & ~(nan & dall)).flatten()[:5])
+            assert bool((nan <= dall).all()), t
+            for q in range(world):
+                if int(dall[q * n:(q + 1) * n].sum()) <= cap:
+                    assert not bool(nan[q * n:(q + 1) * n].any()), (t, q)
+            part = torch.isnan(slab[nan])
+            assert bool(part[:, :ol + 4].all() and part[:, 2 * ol + 4:].all() and not part[:, ol + 4:2 * ol + 4].any())
+            assert torch.equal(slab[~nan], full[~nan]) and torch.equal(slab[nan][:, ol + 4:2 * ol + 4],
+                                                                        full[nan][:, ol + 4:2 * ol + 4])
             nan_rows.append(int(nan.sum()))
-        a_prev = a
+            exact_resets.append(int((dall & ~nan).sum()))
     env.close()
     if rank == 0:
         np.savez(os.path.join(out_dir, "res.npz"), mismatch=np.array(len(mismatch)), resets=np.array(resets),
                  overflows=np.array(pipe.overflows()), nan_rows=np.array(nan_rows if nan_rows else [0]),
+                 exact_resets=np.array(exact_resets if exact_resets else [0]),
                  first=np.array(mismatch[:1], dtype=object) if mismatch else np.zeros(0))
     dist.barrier()
     dist.destroy_process_group()
@@ -92,13 +104,12 @@ def test_delta_exchange_matches_full_gather(tmp_path):
 def test_time_out_look_ahead_sizes_the_capacity():
     """A TimeLimit makes resets predictable: every env that reaches max_steps - L steps since its
     reset times out L steps later unless it crashes first, so step_cap covers them."""
-    from cf2sim.dist import unpack_obs, packed_words, pack_obs
+    from cf2sim.dist import consume_obs, pack_obs
     n, ol, M, L = 40, 13, 12, 4
     od = 2 * (ol + 4)
     age = torch.zeros(n, dtype=torch.int32)
     pred = torch.zeros(L + 1, 1, dtype=torch.int32)
-    slab = [torch.zeros(n, od), torch.zeros(n, od)]
-    a = torch.zeros(n, 4)
+    rows = torch.zeros(n, od)
     hits = []
     for k in range(30):
         reset = torch.zeros(n, dtype=torch.uint8)
@@ -110,9 +121,8 @@ def test_time_out_look_ahead_sizes_the_capacity():
             reset[:7] = 1
         if k >= L and int(pred[(k - L) % (L + 1)].max()):      # read before this step's unpack reuses the slot
             hits.append((k, int(pred[(k - L) % (L + 1)].max())))
-        pk = pack_obs(slab[k % 2], reset, cap=n)
-        unpack_obs(pk, 1, n, ol, n, a, a, age, slab[k % 2], slab[(k + 1) % 2], None, M - L,
-                   pred[k % (L + 1)], pred[(k + 1) % (L + 1)])
+        pk = pack_obs(rows, reset, cap=n)
+        consume_obs(pk, 1, n, ol, n, age, None, M - L, pred[k % (L + 1)], pred[(k + 1) % (L + 1)])
     assert (5 + M, 7) in hits and (M - 1 + M, 33) in hits, hits
 
 
@@ -121,6 +131,7 @@ def test_delta_exchange_overflow_is_marked_and_recovers(tmp_path):
     res = np.load(tmp_path / "res.npz", allow_pickle=True)
     assert int(res["overflows"]) > 0
     assert res["nan_rows"].max() > 0
+    assert res["exact_resets"].max() > 0       # a block that found room keeps its reset rows exact
 
 
 def test_packed_layout_and_bytes():
@@ -134,14 +145,14 @@ def test_packed_layout_and_bytes():
     assert packed_words(5, 17, 3) == ((4 + 5 * 17 + 1 + 1 + 3 * 22 + 3) & ~3)     # + one block-table word
 
 
-def test_pack_unpack_single_process_roundtrip():
-    """pack -> unpack over one rank on synthetic rows that follow the history rules."""
-    from cf2sim.dist import pack_obs, packed_words, unpack_obs
+def test_pack_consume_rows_single_process_roundtrip():
+    """pack -> consume -> rows over one rank on synthetic rows that follow the history rules."""
+    from cf2sim.dist import consume_obs, obs_rows, pack_obs, packed_words
     n, ol = 70, 13
     od = 2 * (ol + 4)
     g = torch.Generator().manual_seed(0)
     prev = torch.randn(n, od, generator=g)
-    a_k, a_p = torch.randn(n, 4, generator=g), torch.randn(n, 4, generator=g)
+    a_k, a_p, a_p2 = torch.randn(n, 4, generator=g), torch.randn(n, 4, generator=g), torch.randn(n, 4, generator=g)
     age = torch.tensor([(i % 4) for i in range(n)], dtype=torch.int32)
     reset = torch.zeros(n, dtype=torch.uint8)
     reset[[3, 17, 40]] = 1
@@ -150,7 +161,7 @@ def test_pack_unpack_single_process_roundtrip():
     for i in range(n):
         a = min(int(age[i]) + 1, 3)
         exp[i, :ol] = prev[i, ol + 4:2 * ol + 4]
-        exp[i, ol:ol + 4] = prev[i, 2 * ol + 4:] if a >= 3 else a_k[i]
+        exp[i, ol:ol + 4] = a_p2[i] if a >= 3 else a_k[i]
         exp[i, ol + 4:2 * ol + 4] = ok[i]
         exp[i, 2 * ol + 4:] = a_k[i] if a == 1 else a_p[i]
     o0, A = torch.randn(3, ol, generator=g), torch.randn(3, 4, generator=g)
@@ -158,13 +169,36 @@ def test_pack_unpack_single_process_roundtrip():
         exp[i, :ol], exp[i, ol:ol + 4], exp[i, 2 * ol + 4:] = o0[j], A[j], A[j]
     cur = exp.clone()          # the env's rows of this step: o_k in the o part, reset rows in full
     pk = pack_obs(cur, reset, cap=8)
-    assert pk.numel() == packed_words(n, ol, 8) and int(pk[0]) == 3
-    out = torch.full((n, od), -7.0)
+    pp = pack_obs(prev, torch.zeros(n, dtype=torch.uint8), cap=0)
+    assert pk.numel() == packed_words(n, ol, 8) and int(pk[0]) == 0 and int(pk[3]) == 8
     age2 = age.clone()
-    unpack_obs(pk.view(1, -1), 1, n, ol, 8, a_k, a_p, age2, prev, out)
-    assert torch.equal(out, exp)
+    consume_obs(pk, 1, n, ol, 8, age2)
     assert age2[[3, 17, 40]].tolist() == [0, 0, 0]
     assert age2[0].item() == 1 and age2[2].item() == 3 and age2[4].item() == 1
+    out = obs_rows(pk, 8, pp, 0, 1, n, ol, age2, a_k, a_p, a_p2)
+    assert torch.equal(out, exp)
+    assert torch.equal(obs_rows(pk, 8, pp, 0, 1, n, ol, age2, a_k, a_p, a_p2, row0=15, nrows=30), exp[15:45])
+
+
+def test_exchange_rejects_depth_one_and_short_lookahead():
+    """depth 1 would let a pack clear its own count word (and a step's rows need the gathered
+    buffers of the step before); a look-ahead shorter than the copy cadence could not be served."""
+    import torch.distributed as dist
+    from cf2sim.dist import PipelinedObsGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with pytest.raises(ValueError):
+            PipelinedObsGather(64, 34, "cpu", depth=1, delta=True)
+        with pytest.raises(ValueError):
+            PipelinedObsGather(64, 34, "cpu", delta=True, lookahead=3)
+        with pytest.raises(ValueError):
+            PipelinedObsGather(64, 34, "cpu", delta=True, unit=8, lookahead=16)
+        p = PipelinedObsGather(64, 34, "cpu", delta=True, max_steps=100)
+        assert p.unit == 16 and p.L == 48 and p.depth == 2 and p.kmax == 1 and p.exchange == "gloo"
+        assert p.npred == p.L + 17 and p.watch == 52
+    finally:
+        dist.destroy_process_group()
 
 
 def test_packed_words_match_the_c_abi():

@@ -1,8 +1,10 @@
-"""The delta observation exchange on the GPU (csrc/cf2sim_exchange.hip, cf2_obs_pack /
-cf2_obs_unpack): the kernels produce the torch-op version's rows bit for bit (partial blocks,
-several ranks, overflow), and with the product env the rebuilt slab equals the full all-gather of
-the observation rows over 240 env-steps with auto-resets and time-outs -- over one RCCL rank (the
-path of the 8-GPU run) and over two gloo ranks sharing the test box's GPU."""
+"""The delta observation exchange on the GPU (csrc/cf2sim_exchange.hip: cf2_obs_pack /
+cf2_obs_consume / cf2_obs_rows): the kernels produce the torch-op version's ages and rows bit for
+bit (partial blocks, several ranks, overflow), and with the product env the rows materialised on
+request equal the full all-gather of the observation rows over 240 env-steps with auto-resets and
+time-outs -- over one RCCL rank (the path of the 8-GPU run: eager per step, one C call per
+env-step, and hipGraph units of 8 env-steps through cf2_xchg_run), through the process group's
+all-gather, and over two gloo ranks sharing the test box's GPU."""
 import os
 import socket
 import sys
@@ -23,7 +25,7 @@ def _port():
 
 
 def _synthetic(world, n, ol, seed):
-    """Every rank's rows of one step and the previous slab, with the history rules applied."""
+    """Every rank's rows of two consecutive steps, reset flags, ages and three steps' actions."""
     g = torch.Generator().manual_seed(seed)
     od = 2 * (ol + 4)
     N = world * n
@@ -31,53 +33,118 @@ def _synthetic(world, n, ol, seed):
     cur = torch.randn(N, od, generator=g)
     reset = (torch.rand(N, generator=g) < 0.06).to(torch.uint8)
     age = torch.randint(0, 6, (N,), generator=g, dtype=torch.int32)
-    a_k, a_p = torch.randn(N, 4, generator=g), torch.randn(N, 4, generator=g)
-    return prev, cur, reset, age, a_k, a_p
+    acts = [torch.randn(N, 4, generator=g) for _ in range(3)]
+    return prev, cur, reset, age, acts
 
 
 @pytest.mark.parametrize("world,n,ol,cap", [(1, 4096, 13, 307), (3, 1000, 13, 75), (2, 333, 17, 40),
                                              (2, 5000, 13, 10)])      # the last one overflows
 def test_kernels_equal_torch_ops(gpu, world, n, ol, cap):
-    from cf2sim.dist import pack_obs, packed_words, unpack_obs
-    prev, cur, reset, age, a_k, a_p = _synthetic(world, n, ol, seed=world * 100 + n)
-    words = packed_words(n, ol, cap)
-    # pack: GPU per rank vs CPU per rank; the side-entry order differs (atomics), the unpacked rows must not
+    from cf2sim.dist import consume_obs, obs_rows, pack_obs, packed_words
+    prev, cur, reset, age, acts = _synthetic(world, n, ol, seed=world * 100 + n)
+    words, wp = packed_words(n, ol, cap), packed_words(n, ol, 0)
+    # pack: GPU per rank vs CPU per rank; the side-entry order differs (atomics), the rows must not
     pk_cpu = torch.cat([pack_obs(cur[r * n:(r + 1) * n], reset[r * n:(r + 1) * n], cap) for r in range(world)])
+    pp_cpu = torch.cat([pack_obs(prev[r * n:(r + 1) * n], torch.zeros(n, dtype=torch.uint8), 0) for r in range(world)])
     pk_gpu = torch.empty(world * words, dtype=torch.int32, device=gpu)
     for r in range(world):
-        view = pk_gpu[r * words:(r + 1) * words]
-        view[:1].zero_()
-        pack_obs(cur[r * n:(r + 1) * n].to(gpu), reset[r * n:(r + 1) * n].to(gpu), cap, out=view)
+        pack_obs(cur[r * n:(r + 1) * n].to(gpu), reset[r * n:(r + 1) * n].to(gpu), cap, out=pk_gpu[r * words:(r + 1) * words])
     g = pk_gpu.cpu().view(world, words)
     c = pk_cpu.view(world, words)
     side = 4 + n * ol + (n + 31) // 32
     assert torch.equal(g[:, :side], c[:, :side]), "header, o_k rows and bitmap are deterministic"
-    out_c = torch.full_like(prev, -1.0)
+    # consume
     age_c = age.clone()
     ovf_c = torch.zeros(1, dtype=torch.int32)
     pred_c = torch.ones(2, world, dtype=torch.int32)
     pred_c[0].zero_()
-    unpack_obs(pk_cpu, world, n, ol, cap, a_k, a_p, age_c, prev, out_c, ovf_c, 4, pred_c[0], pred_c[1])
-    out_g = torch.full_like(prev, -1.0).to(gpu)
+    consume_obs(pk_cpu, world, n, ol, cap, age_c, ovf_c, 4, pred_c[0], pred_c[1])
     age_g = age.to(torch.int16).to(gpu)                    # uint16 storage on the GPU
     ovf_g = torch.zeros(1, dtype=torch.int32, device=gpu)
     pred_g = torch.ones(2, world, dtype=torch.int32, device=gpu)
     pred_g[0].zero_()
-    unpack_obs(pk_gpu, world, n, ol, cap, a_k.to(gpu), a_p.to(gpu), age_g, prev.to(gpu), out_g, ovf_g, 4, pred_g[0],
-               pred_g[1])
+    consume_obs(pk_gpu, world, n, ol, cap, age_g, ovf_g, 4, pred_g[0], pred_g[1])
     torch.cuda.synchronize()
-    same = (out_g.cpu() == out_c) | (torch.isnan(out_g.cpu()) & torch.isnan(out_c))
-    assert bool(same.all())
     assert torch.equal(age_g.cpu().to(torch.int32) & 0xFFFF, age_c)
-    assert int(ovf_g.item()) == int(ovf_c.item())
+    assert (int(ovf_g.item()) > 0) == (int(ovf_c.item()) > 0)
     assert torch.equal(pred_g.cpu(), pred_c) and int(pred_c[0].sum()) > 0 and int(pred_c[1].sum()) == 0
-    if cap == 10:
-        assert int(ovf_g.item()) > 0
+    # rows: all of them, and a ragged window across a rank boundary
+    out_c = obs_rows(pk_cpu, cap, pp_cpu, 0, world, n, ol, age_c, *acts)
+    out_g = obs_rows(pk_gpu, cap, pp_cpu.to(gpu), 0, world, n, ol, age_g, *[a.to(gpu) for a in acts])
+    r0, nr = max(0, n - 77), min(world * n - max(0, n - 77), 300)
+    win_g = obs_rows(pk_gpu, cap, pp_cpu.to(gpu), 0, world, n, ol, age_g, *[a.to(gpu) for a in acts], row0=r0, nrows=nr)
+    torch.cuda.synchronize()
+    og = out_g.cpu()
+    if cap != 10:
+        assert torch.equal(og, out_c) and int(ovf_c.item()) == 0
+    else:
+        # overflow: the GPU and the CPU hand the slots to different blocks, so each drops other
+        # blocks; every row neither marked is equal, and the marks sit on reset rows only
+        ng, nc = torch.isnan(og).any(1), torch.isnan(out_c).any(1)
+        both = ~ng & ~nc
+        assert torch.equal(og[both], out_c[both]) and bool((ng <= reset.bool()).all())
+        assert int(ovf_g.item()) > 0 and int(ng.sum()) > 0
+    assert torch.equal(torch.nan_to_num(win_g.cpu(), 7.0), torch.nan_to_num(og[r0:r0 + nr], 7.0))
+
+
+def test_overflow_nans_exactly_the_reset_rows_that_got_no_slot(gpu):
+    """A rank with more resets than its side slab: the reset rows of exactly the 64-env blocks its
+    packed buffer marks dropped have NaN in o_0 / A, their o_k parts and every other row (that
+    rank's, its other reset rows, the other rank's) are exactly the rows the history rules give,
+    and the overflow count is the number of dropped blocks."""
+    from cf2sim.dist import PACK_BLOCK, PACK_DROPPED, consume_obs, obs_rows, pack_obs, packed_words
+    world, n, ol = 2, 3000, 13
+    od = 2 * (ol + 4)
+    prev, cur, _, age, acts = _synthetic(world, n, ol, seed=9)
+    reset = torch.zeros(world * n, dtype=torch.uint8)
+    reset[torch.arange(0, n, 7)] = 1              # rank 0: 429 resets
+    reset[n + torch.arange(0, n, 97)] = 1         # rank 1: 31 resets
+    cap = 100                                     # rank 0 overflows, rank 1 does not
+    words = packed_words(n, ol, cap)
+    pk = torch.empty(world * words, dtype=torch.int32, device=gpu)
+    for r in range(world):
+        pack_obs(cur[r * n:(r + 1) * n].to(gpu), reset[r * n:(r + 1) * n].to(gpu), cap, out=pk[r * words:(r + 1) * words])
+    pp = torch.cat([pack_obs(prev[r * n:(r + 1) * n], torch.zeros(n, dtype=torch.uint8), 0) for r in range(world)]).to(gpu)
+    age_g = age.to(torch.int16).to(gpu)
+    ovf = torch.zeros(1, dtype=torch.int32, device=gpu)
+    consume_obs(pk, world, n, ol, cap, age_g, ovf)
+    rows = obs_rows(pk, cap, pp, 0, world, n, ol, age_g, *[a.to(gpu) for a in acts]).cpu()
+    # the blocks each rank's pack marked dropped
+    nb, nblk = (n + 31) // 32, (n + PACK_BLOCK - 1) // PACK_BLOCK
+    pkc = pk.cpu().view(world, words)
+    dropped_env = torch.zeros(world * n, dtype=torch.bool)
+    ndrop = 0
+    for r in range(world):
+        bt = pkc[r, 4 + n * ol + nb:4 + n * ol + nb + nblk]
+        d = bt == PACK_DROPPED
+        ndrop += int(d.sum())
+        dropped_env[r * n:(r + 1) * n] = d.repeat_interleave(PACK_BLOCK)[:n]
+    assert int(ovf.item()) == ndrop > 0
+    # the side slab is full: at most cap entries were placed, and no rank-1 block was dropped
+    assert not bool(dropped_env[n:].any())
+    # expected rows from the definitions (the env's rows of this step are `cur` where reset)
+    a = (age.to(torch.int64) + 1).clamp(max=0xFFFF)
+    a[reset.bool()] = 0
+    exp = torch.empty(world * n, od)
+    exp[:, :ol] = prev[:, ol + 4:2 * ol + 4]
+    exp[:, ol:ol + 4] = torch.where((a >= 3)[:, None], acts[2], acts[0])
+    exp[:, ol + 4:2 * ol + 4] = cur[:, ol + 4:2 * ol + 4]
+    exp[:, 2 * ol + 4:] = torch.where((a == 1)[:, None], acts[0], acts[1])
+    rs = reset.bool()
+    exp[rs, :ol + 4] = cur[rs, :ol + 4]
+    exp[rs, 2 * ol + 4:] = cur[rs, ol:ol + 4]
+    lost = rs & dropped_env
+    assert 0 < int(lost.sum()) < int(rs[:n].sum()), "some, not all, of rank 0's reset rows are lost"
+    nan_part = torch.zeros(world * n, od, dtype=torch.bool)
+    nan_part[lost, :ol + 4] = True
+    nan_part[lost, 2 * ol + 4:] = True
+    assert bool(torch.isnan(rows[nan_part]).all()), "every reset row of a dropped block is marked"
+    assert torch.equal(rows[~nan_part], exp[~nan_part]), "everything else is exact"
 
 
 def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
     sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
-    os.environ["CF2SIM_EXCHANGE"] = "native" if exchange == "native_env" else exchange
+    os.environ["CF2SIM_EXCHANGE"] = "torch" if exchange == "torch" else "native"
     import torch.distributed as dist
     from cf2sim.dist import PipelinedObsGather, gather_rows
     from cf2sim.vec_env import BatchedCrazyflieEnv
@@ -95,94 +162,137 @@ def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
     pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=41)
     g = torch.Generator(device=dev)
     g.manual_seed(5)
-    acts = torch.rand(T, N, 4, device=dev, generator=g) * 2 - 1      # every rank holds every action
+    ring = torch.rand(8, N, 4, device=dev, generator=g) * 2 - 1      # every rank holds every action
+    acts = [ring[k % 8] for k in range(T)]
     slab = pipe.start(obs0)
     pipe.drain()
-    bad, resets = [], 0
+    bad, resets, checked = [], 0, 0
     full = gather_rows(obs0, sizes=[n] * world)
     if not torch.equal(slab, full):
         bad.append(-1)
-    for k in range(T):
-        a = acts[k]
-        a_prev = acts[k - 1] if k > 0 else a
-        if exchange == "native_env":       # env-step + exchange in one C call
+    if not torch.equal(pipe.rows(acts[0], acts[0], acts[0]), full):
+        bad.append(-2)
+
+    def a3(k):
+        return acts[k], acts[max(k - 1, 0)], acts[max(k - 2, 0)]
+
+    if exchange == "run":
+        # batches: a twin env steps the same actions eagerly for the reference rows
+        twin = BatchedCrazyflieEnv(ENV_ID, n, seed=3, env_id_offset=rank * n, device=dev, max_episode_steps=41)
+        twin.reset()
+        ptrs = [ring[r][rank * n:(rank + 1) * n].data_ptr() for r in range(8)]
+        k = 0
+        for G in [16, 3, 5, 8] + [16] * ((T - 48) // 16) + [9, 7]:
+            for s in range(G):
+                twin.step_raw(ptrs[(k + s) % 8])
+                resets += int(gather_rows(twin.done, sizes=[n] * world).sum())
+            last = pipe.run(env, ptrs, G)
+            k += G
+            assert last == k - 1
+            full = gather_rows(twin.obs, sizes=[n] * world)
+            rows = pipe.rows(*a3(k - 1))
+            checked += 1
+            if not torch.equal(rows, full):
+                bad.append(k - 1)
+        twin.close()
+    else:
+        for k in range(T):
+            a = acts[k]
             j = pipe.k % pipe.depth
-            slab = pipe.step_and_publish(env, a[rank * n:(rank + 1) * n].data_ptr(), a.data_ptr(), a_prev.data_ptr())
-            pipe.drain()
-            ref_obs, ref_done = pipe.obs[j].clone(), pipe.done[j].clone()
-        else:
-            buf = pipe.buffer()
-            done = pipe.done_buffer()
-            env.step_raw(a[rank * n:(rank + 1) * n].data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=done.data_ptr())
-            ref_obs = buf.clone()
-            ref_done = done.clone()
-            slab = pipe.publish(a, a_prev)
-            pipe.drain()
-        full = gather_rows(ref_obs, sizes=[n] * world)
-        resets += int(gather_rows(ref_done, sizes=[n] * world).sum())
-        if not torch.equal(slab, full):
-            bad.append(k)
+            if exchange == "native_env":       # env-step + exchange in one C call
+                pipe.step_and_publish(env, a[rank * n:(rank + 1) * n].data_ptr())
+            else:
+                buf = pipe.buffer()
+                done = pipe.done_buffer()
+                env.step_raw(a[rank * n:(rank + 1) * n].data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=done.data_ptr())
+                pipe.publish()
+            rows = pipe.rows(*a3(k))
+            torch.cuda.synchronize()
+            full = gather_rows(pipe.obs[j], sizes=[n] * world)
+            resets += int(gather_rows(pipe.done[j], sizes=[n] * world).sum())
+            checked += 1
+            if not torch.equal(rows, full):
+                bad.append(k)
     torch.cuda.synchronize()
     how = pipe.exchange
+    graphs = 0
+    ovf = pipe.overflows()
     pipe.close()
     if rank == 0:
         with open(out, "w") as f:
-            f.write(f"{len(bad)} {resets} {pipe.overflows()} {how} {bad[:3]}")
+            f.write(f"{len(bad)} {resets} {ovf} {how} {checked} {graphs} {bad[:3]}")
     dist.destroy_process_group()
 
 
-def _check(out, T, how):
-    nbad, resets, ovf, got = open(out).read().split()[:4]
+def _check(out, how, min_checked=200):
+    nbad, resets, ovf, got, checked, graphs = open(out).read().split()[:6]
     assert int(nbad) == 0, open(out).read()
     assert int(resets) > 0 and int(ovf) == 0
     assert got == how
+    assert int(checked) >= min_checked
+    return int(graphs)
 
 
 def test_delta_exchange_one_rccl_rank(gpu, tmp_path):
-    """The native exchange (cf2_xchg_step: pack, our own RCCL communicator's all-gather, rebuild)."""
+    """The native exchange, eager: cf2_xchg_publish per step (pack, our own RCCL communicator's
+    all-gather, consume) and the rows materialised after every step."""
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240), nprocs=1, join=True)
-    _check(out, 240, "native")
+    _check(out, "native")
 
 
 def test_delta_exchange_one_rccl_rank_env_step_in_one_call(gpu, tmp_path):
     """The native exchange's registered form: env-step + exchange per cf2_xchg_env_step call."""
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "native_env"), nprocs=1, join=True)
-    _check(out, 240, "native")
+    _check(out, "native")
+
+
+def test_delta_exchange_one_rccl_rank_batched_run(gpu, tmp_path):
+    """cf2_xchg_run: batches of env-steps with the pack fused in (cf2_step_packed), one RCCL
+    all-gather and one consume per batch (units of 16, entered with partial batches of 3 and 5);
+    the rows of each batch's last step equal the full gather of an eagerly stepped twin env's
+    observations."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "run"), nprocs=1, join=True)
+    _check(out, "native", min_checked=16)
 
 
 def test_delta_exchange_one_rccl_rank_torch_path(gpu, tmp_path):
     """The same exchange with the process group's all-gather between the launches from Python."""
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "torch"), nprocs=1, join=True)
-    _check(out, 240, "torch")
+    _check(out, "torch")
 
 
 def test_delta_exchange_two_gloo_ranks_on_one_gpu(gpu, tmp_path):
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 240), nprocs=2, join=True)
-    _check(out, 240, "gloo")
+    _check(out, "gloo")
 
 
-def test_unpack_rejects_operands_the_kernel_would_overrun(gpu):
+def test_operands_the_kernels_would_overrun_are_rejected(gpu):
     """Host-side checks before the launch: a uint8 age vector (half the bytes the kernel indexes),
-    a short slab or a short packed buffer raise ValueError instead of faulting on the device."""
-    from cf2sim.dist import pack_obs, packed_words, unpack_obs
+    short rows / packed buffers, or a pack whose next counters are its own raise ValueError instead
+    of faulting on the device."""
+    from cf2sim.dist import consume_obs, obs_rows, pack_obs, packed_words
     n, ol, cap = 256, 13, 16
     od = 2 * (ol + 4)
     prev = torch.zeros(n, od, device=gpu)
-    cur = torch.empty_like(prev)
     a = torch.zeros(n, 4, device=gpu)
     pk = pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap)
     good_age = torch.zeros(n, dtype=torch.int16, device=gpu)
-    unpack_obs(pk, 1, n, ol, cap, a, a, good_age, prev, cur)
+    consume_obs(pk, 1, n, ol, cap, good_age)
+    obs_rows(pk, cap, pk, cap, 1, n, ol, good_age, a, a, a)
     torch.cuda.synchronize()
     with pytest.raises(ValueError):
-        unpack_obs(pk, 1, n, ol, cap, a, a, torch.zeros(n, dtype=torch.uint8, device=gpu), prev, cur)
+        consume_obs(pk, 1, n, ol, cap, torch.zeros(n, dtype=torch.uint8, device=gpu))
     with pytest.raises(ValueError):
-        unpack_obs(pk, 1, n, ol, cap, a, a, good_age, prev, cur[: n // 2])
+        obs_rows(pk, cap, pk, cap, 1, n, ol, good_age, a, a, a, out=torch.empty(n // 2, od, device=gpu))
     with pytest.raises(ValueError):
-        unpack_obs(pk[: packed_words(n, ol, cap) // 2], 1, n, ol, cap, a, a, good_age, prev, cur)
+        obs_rows(pk[: packed_words(n, ol, cap) // 2], cap, pk, cap, 1, n, ol, good_age, a, a, a)
     with pytest.raises(ValueError):
         pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap, out=torch.zeros(8, dtype=torch.int32, device=gpu))
+    scr = torch.zeros(288, dtype=torch.int32, device=gpu)
+    with pytest.raises(ValueError):
+        pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap, out=pk, scratch=scr, next_scratch=scr)

@@ -1,0 +1,96 @@
+"""Per env-step time of the delta observation exchange at one shard (default 32 768 envs, the
+8-GPU node shard) on one RCCL rank: the env-step alone, the eager native exchange (one
+cf2_xchg_env_step call per step), and batches (PipelinedObsGather.run, cf2_xchg_run: env-steps
+back to back with the pack fused in, one all-gather + consume per batch).
+
+  torchrun --nproc-per-node 1 --master-addr 127.0.0.1 tools/xchg_run_probe.py [--envs N] [--steps K] [--unit G]
+Prints one JSON line."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=32768)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=600)
+    ap.add_argument("--unit", type=int, default=16)
+    ap.add_argument("--env-id", default="DroneHoverBulletFreeEnvWithGust-v0")
+    args = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    from cf2sim.dist import PipelinedObsGather
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", device_id=dev)
+    n = args.envs
+    env = BatchedCrazyflieEnv(args.env_id, n, seed=0, device=dev)
+    env.reset()
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    ring = torch.rand(8, n, 4, device=dev, generator=g) * 2 - 1
+    ptrs = [ring[r].data_ptr() for r in range(8)]
+    res = {"envs": n, "steps": args.steps, "unit": args.unit}
+
+    def timed(fn, steps):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        fn(steps)
+        e1.record()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e6 / steps, e0.elapsed_time(e1) * 1e3 / steps
+
+    def plain(steps):
+        for k in range(steps):
+            env.step_raw(ptrs[k % 8])
+    plain(args.warmup)
+    res["env_step_us"], _ = timed(plain, args.steps)
+
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=int(env.cfg.max_episode_steps),
+                              unit=args.unit)
+    pipe.start(env.obs)
+    res["exchange"] = pipe.exchange
+
+    def eager(steps):
+        for _ in range(steps):
+            pipe.step_and_publish(env, ptrs[pipe.k % 8])
+        pipe.drain()
+    eager(args.warmup)
+    res["eager_us"], _ = timed(eager, args.steps)
+
+    def batched(steps):
+        pipe.run(env, ptrs, steps)
+        pipe.drain()
+    # align to the unit, then warm up
+    batched((-pipe.k) % args.unit + args.warmup)
+    res["run_us"], res["run_gpu_us"] = timed(batched, args.steps)
+    res["overflows"] = pipe.overflows()
+    res["bytes_per_rank_per_step"] = pipe.bytes_per_rank_per_step
+    # rows on request: all rows of the last step
+    a = ring[pipe.k % 8]
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = torch.empty(n, env.obs_dim, device=dev)
+    pipe.rows(a, a, a, out=out)
+    e0.record()
+    for _ in range(20):
+        pipe.rows(a, a, a, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    res["rows_us_all"] = e0.elapsed_time(e1) * 1e3 / 20
+    pipe.close()
+    print(json.dumps(res), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
