@@ -103,6 +103,19 @@ def _host_threads() -> int:
     return max(1, len(os.sched_getaffinity(0)))
 
 
+def _cpu_model() -> str:
+    """The host CPU's model name (name the cores the baseline ran on)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
     """Time the CPU restatement (oracle/, scalar C fp64) on a bounded sample of the same workload:
     one thread, then OpenMP over the host threads this process may use (envs split by index).
@@ -129,7 +142,7 @@ def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
 
     one, dt1 = rate(2048, 600, 1)
     allt, dtn = rate(n_envs, steps, threads) if threads > 1 else (one, dt1)
-    return {"value": allt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {"value": allt, "unit": "env-steps/s", "cores": threads, "kind": "port", "cpu_model": _cpu_model(),
             "sample": f"oracle/cf2_oracle.c fp64 on {ENV_ID} (gust, noise, DR): {n_envs} envs x {steps} "
                       f"env-steps on {threads} OpenMP threads in {dtn:.1f} s; 1 thread: {one:.3g} env-steps/s "
                       f"(2048 envs x 600 env-steps, {dt1:.1f} s)"}
@@ -870,6 +883,7 @@ def main(argv=None):
             "delta_exchange": exchange,
         }
         print(json.dumps(line), flush=True)
+    env.check_device_errors()
     env.close()
     if use_pg:
         dist.destroy_process_group()

@@ -21,7 +21,7 @@ REPO_INCLUDE = os.path.abspath(os.path.join(PKG_DIR, "..", "..", "include", "cf2
 
 # every symbol include/cf2sim.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
-    "cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
+    "cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error", "cf2_device_errors",
     "cf2_create", "cf2_destroy", "cf2_layout_get", "cf2_bind_hj_tables", "cf2_reset", "cf2_step", "cf2_collect_step",
     "cf2_collect_rollout", "cf2_physics_step",
     "cf2_set_ground_effect",
@@ -71,6 +71,7 @@ def load() -> ctypes.CDLL:
     lib.cf2_last_hip_error.restype = ctypes.c_int
     lib.cf2_create.argtypes = [P(CF2Config), P(vp)]
     lib.cf2_destroy.argtypes = [vp]
+    lib.cf2_device_errors.argtypes = [vp, P(ctypes.c_uint32), ctypes.c_int]
     lib.cf2_layout_get.argtypes = [vp, P(CF2Layout)]
     lib.cf2_bind_hj_tables.argtypes = [vp, vp, ctypes.c_int, P(ctypes.c_int32)]
     lib.cf2_reset.argtypes = [vp, vp, vp, vp]

@@ -437,6 +437,14 @@ class BatchedCrazyflieEnv:
         _native.check(self.lib.cf2_set_state(self._ctx, sf.data_ptr(), si.data_ptr(), self.stream), "cf2_set_state")
         self._state_version += 1
 
+    def check_device_errors(self, clear: bool = True):
+        """Raise CF2Error if a kernel of this batch recorded a device-side error (cf2_device_errors:
+        a helper wave that gave up waiting for an LDS hand-over).  Synchronises the device."""
+        flags = ctypes.c_uint32(0)
+        _native.check(self.lib.cf2_device_errors(self._ctx, ctypes.byref(flags), int(clear)), "cf2_device_errors")
+        if flags.value:
+            raise _native.CF2Error(f"device error flags 0x{flags.value:x} (1: a helper wave's LDS hand-over timed out)")
+
     def invalidate(self):
         """Mark the cached snapshot (and the observations' owner) stale.  Needed after anything
         that changes the state without going through this object: replaying a hipGraph that

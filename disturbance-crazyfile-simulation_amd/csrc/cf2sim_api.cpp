@@ -257,6 +257,16 @@ int cf2_destroy(cf2_ctx* ctx) {
     return CF2_OK;
 }
 
+int cf2_device_errors(cf2_ctx* ctx, uint32_t* flags_out, int clear) {
+    if (!ctx || !flags_out) return CF2_ERR_INVALID_ARG;
+    // synchronous: waits for the kernels issued so far (all streams of the device)
+    hipError_t e = hipDeviceSynchronize();
+    uint32_t* dev = &ctx->tab_dev->dev_err;
+    if (e == hipSuccess) e = hipMemcpy(flags_out, dev, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && clear && *flags_out) e = hipMemset(dev, 0, sizeof(uint32_t));
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
 int cf2_layout_get(const cf2_ctx* ctx, cf2_layout* o) {
     if (!ctx || !o) return CF2_ERR_INVALID_ARG;
     memset(o, 0, sizeof(*o));

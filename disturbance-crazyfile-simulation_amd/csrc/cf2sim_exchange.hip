@@ -607,7 +607,7 @@ extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb,
         const float* act = act_dev[k % nact];
         st = cf2_step_packed(ctx, act, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr,
                              scr_next, cap, es);
-        if (st == CF2_ERR_UNSUPPORTED) {      // larger contexts: the env-step, then the pack, in order
+        if (st == CF2_ERR_UNSUPPORTED) {      // a shape without the fused pack: the env-step, then the pack
             st = cf2_step(ctx, act, nullptr, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, nullptr,
                           es);
             if (st == CF2_OK) st = cf2_obs_pack(x->obs[q], x->done[q], x->n, x->ol, cap, pk, scr, scr_next, es);

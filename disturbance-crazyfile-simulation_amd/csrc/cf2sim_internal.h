@@ -123,7 +123,9 @@ struct KTables {
     float init_xyz[3], pos_lim, angle_lim, yaw_lim, vel_lim, rate_lim, yaw_rate_lim;
     float action_std, motor_std, hover_x, hover_action;
     float dr_lo[9], dr_hi[9];
+    uint32_t dev_err;           // CF2_DEVERR_* bits the kernels set (cf2_device_errors); 0 when uploaded
 };
+enum : uint32_t { CF2_DEVERR_HANDOVER = 1u };   // a helper wave gave up waiting for an LDS hand-over
 
 struct StepIO {
     float* sf;          // internal AoSoA state (state_bytes(N))
@@ -143,8 +145,8 @@ int hip_fail(hipError_t e);
 // fills P.rb_* for the kernel instances P dispatches to, on the current device
 hipError_t query_occupancy(KParams& P);
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s);
-// the env-step with the delta exchange's pack of its observations fused in (step_kernel_small's
-// epilogue); hipErrorNotSupported above SMALL_N_MAX envs (the caller then packs separately)
+// the env-step with the delta exchange's pack of its observations fused in (the step kernels'
+// epilogues)
 hipError_t launch_step_packed(const KParams& P, const StepIO& io, const PackIO& pio, hipStream_t s);
 // The collect loop's policy half, fused behind the env-step (collect_kernel): the actor-critic
 // forward on the new observations (packed bf16x3 fragments of cf2_policy_pack, obs_dim 34)

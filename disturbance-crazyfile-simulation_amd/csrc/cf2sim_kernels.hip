@@ -448,16 +448,18 @@ __device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, u
 // has no fence semantics the compiler could move memory operations around.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // A one-way hand-over between waves of a block without a block barrier: the producer's lane 0
-// sets an LDS flag after the wave's LDS writes; consumers poll it (bounded: a flag never set ends
-// the wait with stale data, which the parity tests would show, instead of a hung grid).
+// sets an LDS flag after the wave's LDS writes; consumers poll it (bounded, so a flag never set
+// cannot hang the grid: the wait then records CF2_DEVERR_HANDOVER in the context's device error
+// word, which cf2_device_errors reports, and BatchedCrazyflieEnv.check_device_errors raises on).
 __device__ __forceinline__ void lds_flag_set(uint32_t* f) {
     __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_flag_wait(uint32_t* f) {
+__device__ __forceinline__ void lds_flag_wait(uint32_t* f, const KTables* tab) {
     for (uint32_t it = 0; it < (1u << 22); ++it) {
         if (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) return;
         __builtin_amdgcn_s_sleep(1);
     }
+    atomicOr(const_cast<uint32_t*>(&tab->dev_err), (uint32_t)CF2_DEVERR_HANDOVER);
 }
 
 // One wave's part of the small-N kernel's write-out of its 64 obs rows: the float4 chunks that touch
@@ -1848,6 +1850,61 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
     write_obs_rows(io.obs + (size_t)base * OD, s_obs, P.N - base < B ? P.N - base : B, B, OD, tid, B);
 }
 
+// The delta exchange's pack fused into the large-N env-step (cf2_step_packed above 32 768 envs):
+// after block_epilogue the block's 256 rows are final in s_obs (reset rows hold the reset
+// observation), so every thread writes its share of the block's o_k run, and each wave (one 64-env
+// pack block) its two bitmap words, its block-table word and its resets' side entries.
+template <uint32_t OL, uint32_t OD, uint32_t B>
+__device__ __forceinline__ void pack_epilogue_block(const PackIO& X, uint32_t n, uint32_t base, uint32_t tid,
+                                                    bool do_reset, const float* s_obs) {
+    typedef float f4x __attribute__((ext_vector_type(4)));
+    const PackLayout L{n, OL, X.cap};
+    uint32_t* pk = X.pk;
+    const uint32_t lane = tid & 63u, wbase = base + (tid & ~63u);
+    const uint64_t m = __ballot(do_reset);
+    uint32_t first = 0u;
+    if (lane == 0 && m) first = pack_alloc(L, X.scratch, (uint32_t)__popcll(m));
+    if (blockIdx.x == 0) {
+        if (tid == 0) { pk[0] = 0u; pk[1] = n; pk[2] = OL; pk[3] = X.cap; }
+        if (X.next_scratch)
+            for (uint32_t k = tid; k < PACK_SCRATCH_WORDS; k += B) X.next_scratch[k] = 0u;
+    }
+    const uint32_t nvalid = n - base < B ? n - base : B;
+    float* dst = reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * OL;
+    if (nvalid == B && ((uintptr_t)dst & 15u) == 0) {
+        f4x* d4 = reinterpret_cast<f4x*>(dst);
+        for (uint32_t c = tid; c < B * OL / 4u; c += B) {
+            f4x v;
+#pragma unroll
+            for (uint32_t e = 0; e < 4u; ++e) {
+                const uint32_t f = 4u * c + e, r = f / OL;
+                v[e] = s_obs[r * OD + OL + 4u + (f - r * OL)];
+            }
+            d4[c] = v;
+        }
+    } else {
+        for (uint32_t f = tid; f < nvalid * OL; f += B) {
+            const uint32_t r = f / OL;
+            dst[f] = s_obs[r * OD + OL + 4u + (f - r * OL)];
+        }
+    }
+    if (wbase < n) {
+        uint32_t* bits = pk + L.bits();
+        if (lane == 0) bits[wbase / 32u] = (uint32_t)m;
+        if (lane == 1 && wbase + 32u < n) bits[wbase / 32u + 1u] = (uint32_t)(m >> 32);
+        first = __shfl(first, 0);
+        if (lane == 0) pk[L.btab() + wbase / XB_PACK] = first;
+        if (do_reset && first != PACK_DROPPED) {
+            uint32_t* e = pk + L.side() + (first + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) * L.entry();
+            e[0] = base + tid;
+            const float* row = s_obs + tid * OD;
+            float* ef = reinterpret_cast<float*>(e + 1);
+#pragma unroll
+            for (uint32_t k = 0; k < OL + 4u; ++k) ef[k] = row[k];     // o_0 and A (= A_0)
+        }
+    }
+}
+
 // Launch shape of the large-N env kernels: 256-thread blocks of 256 envs (= the auto-reset
 // compaction group), 3 waves per SIMD (<= 168 VGPRs, <= 53 KB LDS per block); resets drawn and run
 // in chunks of 32
@@ -1859,7 +1916,7 @@ constexpr uint32_t STEP_BLOCK = 256, STEP_MIN_WAVES = 3, RESET_CHUNK = 32;
 // scattered SoA accesses cost no extra HBM traffic (a separate reset kernel pays ~60 B per
 // 4-byte field access for them).
 template <bool NOISE, bool DR, int PHYS, int SPEC, int ST_AUX = 0>
-__global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io) {
+__global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) step_kernel(KParams P0, StepIO io, PackIO X) {
     const KParams P = shape_view<SPEC>(P0);
     // Issue priority: the blocks that start only after the first residency round (the partial
     // last round at 262 144 envs) run mostly alone on their SIMDs and end the kernel; their waves
@@ -1891,6 +1948,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) step_kernel(KParam
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
+    if (X.pk) pack_epilogue_block<NOISE ? 13u : 17u, (uint32_t)OD, B>(X, P.N, base, tid, do_reset, s_obs);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
     if (uint64_t* r = timing_row())
@@ -2199,7 +2257,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
         }
         reset_prework();
         if (wave >= 2) {
-            lds_flag_wait(s_mask + 2);
+            lds_flag_wait(s_mask + 2, P.tab);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 H.p[k] = s_pose[k * 64 + lane];
@@ -2742,7 +2800,7 @@ __device__ __forceinline__ void small_roll_helper_step(const KParams& P, const K
             float ngs[9];
             held_noise(P, gr, wave == 2 ? 32u : 40u, hn, ngs);
             if (wave == PARAMS_WAVE) params();
-            lds_flag_wait(L.mask + 2);
+            lds_flag_wait(L.mask + 2, P.tab);
             const float* kin = L.kin + lane;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -3114,17 +3172,16 @@ static hipError_t launch_step_t(const KParams& P, const StepIO& io, hipStream_t 
         hipLaunchKernelGGL((step_kernel_small<NOISE, DR, PHYS, SPEC>), dim3((P.N + 63u) / 64u), dim3(256), 0, s, P, io, X);
         return hipGetLastError();
     }
-    if (X.pk) return hipErrorNotSupported;     // the fused pack is step_kernel_small's
     const dim3 grid((P.N + STEP_BLOCK - 1) / STEP_BLOCK), block(STEP_BLOCK);
     KParams Pl = P;
     Pl.late_block = P.rb_step;
     // the env state plus the step's I/O no longer fit the 256 MB Infinity Cache between env-steps
     // (P.nt_state, cf2_create): stream the state stores past it (nt), HBM-bound regime
     if (P.nt_state) {
-        hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC, 2>), grid, block, 0, s, Pl, io);
+        hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC, 2>), grid, block, 0, s, Pl, io, X);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, Pl, io);
+    hipLaunchKernelGGL((step_kernel<NOISE, DR, PHYS, SPEC>), grid, block, 0, s, Pl, io, X);
     return hipGetLastError();
 }
 template <bool NOISE, bool DR, int PHYS, int SPEC>
@@ -3306,7 +3363,6 @@ extern "C" int cf2_debug_timing_buffer(uint64_t* dev) {
 hipError_t query_occupancy(KParams& P) { CF2_DISPATCH(occupancy_t, P); }
 hipError_t launch_step(const KParams& P, const StepIO& io, hipStream_t s) { CF2_DISPATCH(launch_step_t, P, io, s); }
 hipError_t launch_step_packed(const KParams& P, const StepIO& io, const PackIO& pio, hipStream_t s) {
-    if (P.N > SMALL_N_MAX) return hipErrorNotSupported;
     CF2_DISPATCH(launch_step_t, P, io, s, pio);
 }
 hipError_t launch_rollout(const KParams& P, const StepIO& io, uint32_t K, uint32_t act_stride, hipStream_t s) {

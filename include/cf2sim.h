@@ -191,6 +191,11 @@ typedef struct cf2_layout {
 typedef struct cf2_ctx cf2_ctx;
 
 int  cf2_abi_version(void);
+/* Errors the kernels of ctx recorded on the device (synchronises the device): bit 1 = a helper
+ * wave of the small-N kernels gave up waiting for the LDS hand-over of the reset pose (its reset
+ * rows would be built from a stale pose; never observed).  clear != 0 resets the word.  The
+ * kernels never trap: they record and finish, and the host decides. */
+int  cf2_device_errors(cf2_ctx* ctx, uint32_t* flags_out, int clear);
 size_t cf2_config_sizeof(void);     /* lets FFI callers check their struct mirror */
 const char* cf2_status_string(int status);
 int  cf2_last_hip_error(void);
@@ -362,12 +367,12 @@ int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev,
 size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t cap);
 int  cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
                   uint32_t* packed_dev, uint32_t* scratch_dev, uint32_t* next_scratch_dev, void* stream);
-/* The env-step (cf2_step's outputs, no final_obs) with the pack of its observations fused in:
- * step_kernel_small writes packed_dev (cf2_obs_packed_words(N, OL, cap) words) as cf2_obs_pack
- * would, from the rows it has in LDS, so no pack launch re-reads them.  scratch_dev: this buffer's
- * side-slot counters (PACK_SCRATCH_WORDS = 288 words), zeroed by the previous pack; next_scratch_dev: the counters the next pack uses, zeroed here (or
- * NULL).  N <= 32 768 envs (the 8-GPU node shard); larger contexts return CF2_ERR_UNSUPPORTED and
- * launch nothing (call cf2_step and cf2_obs_pack). */
+/* The env-step (cf2_step's outputs, no final_obs) with the pack of its observations fused in: the
+ * env kernel writes packed_dev (cf2_obs_packed_words(N, OL, cap) words) as cf2_obs_pack would, from
+ * the rows it has in LDS, so no pack launch re-reads them (step_kernel_small's wave 2 at N <= 32 768,
+ * every thread of step_kernel's blocks above).  scratch_dev: this buffer's side-slot counters
+ * (PACK_SCRATCH_WORDS = 288 words), zeroed by the previous pack; next_scratch_dev: the counters the
+ * next pack uses, zeroed here (or NULL). */
 int  cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
                      uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* packed_dev, uint32_t* scratch_dev,
                      uint32_t* next_scratch_dev, uint32_t cap, void* stream);
@@ -398,7 +403,7 @@ int  cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride,
  * caller issued on env_stream into obs / reset of `region` (after cf2_xchg_wait_free(x, region,
  * env_stream)); packs it on env_stream.  cf2_xchg_run: env-steps k0 .. k0 + nb - 1 of ctx (nb <=
  * kmax; actions of step k at act_dev[k % nact]) issued back to back on env_stream with their pack
- * fused in (cf2_step_packed; larger contexts pack after each env-step), then the batch's exchange at
+ * fused in (cf2_step_packed), then the batch's exchange at
  * capacity cap; pred_host (pinned, npred x world words, or NULL) receives the look-ahead ring after
  * the batch's consume.  cf2_xchg_env_step: cf2_xchg_run of one step.  cf2_xchg_wait(x, stream): a
  * stream waits until every exchange issued so far is complete.  RCCL failures return CF2_ERR_HIP. */

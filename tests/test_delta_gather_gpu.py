@@ -182,7 +182,7 @@ def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
         twin.reset()
         ptrs = [ring[r][rank * n:(rank + 1) * n].data_ptr() for r in range(8)]
         k = 0
-        for G in [16, 3, 5, 8] + [16] * ((T - 48) // 16) + [9, 7]:
+        for G in [16, 3, 5, 8] + [16] * ((T - 48) // 16) + [9, 7] if T == 240 else [16, 3, 5, 8] + [16] * ((T - 32) // 16):
             for s in range(G):
                 twin.step_raw(ptrs[(k + s) % 8])
                 resets += int(gather_rows(twin.done, sizes=[n] * world).sum())
@@ -256,6 +256,14 @@ def test_delta_exchange_one_rccl_rank_batched_run(gpu, tmp_path):
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "run"), nprocs=1, join=True)
     _check(out, "native", min_checked=16)
+
+
+def test_delta_exchange_one_rccl_rank_batched_run_large_shard(gpu, tmp_path):
+    """The same above 32 768 envs: the pack fused into step_kernel (256-env blocks, 4 pack blocks
+    each, a ragged last block) instead of step_kernel_small."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(1, _port(), out, "nccl", 40000, 120, "run"), nprocs=1, join=True)
+    _check(out, "native", min_checked=8)
 
 
 def test_delta_exchange_one_rccl_rank_torch_path(gpu, tmp_path):

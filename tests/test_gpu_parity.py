@@ -66,6 +66,7 @@ def _run_pair(env_id, kw, n, T, prec, seed=3, stop_at_done=False):
         np.testing.assert_array_equal(g_i["truncated"].cpu().numpy().astype(bool) & ~(g_d != r_d), r_i["truncated"] & ~(g_d != r_d))
     gsf, gsi = env.get_state()
     rsf, rsi = ref.get_state()
+    env.check_device_errors()          # no helper wave gave up on an LDS hand-over
     env.close()
     ref.close()
     return np.array(errs), done_mismatch, rew_err, (gsf.cpu().numpy(), gsi.cpu().numpy()), (rsf, rsi)

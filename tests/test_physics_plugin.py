@@ -136,3 +136,76 @@ def test_plugin_rejects_mismatched_drone_and_bad_inputs(gpu):
         drone.env.step(torch.zeros(8, 4, device="cuda"))
     simple.close()
     drone.close()
+
+
+@pytest.mark.gpu
+def test_prop_spin_up_reaction_is_the_rotors_angular_momentum(gpu):
+    """Known answer for the prop joints' spin dynamics in the Bullet sub-step (a7: bullet3's
+    btMultiBody behind bc.stepSimulation(), envs/physics.py:249; the reference spins the prop joints
+    with setJointMotorControl2(targetVelocity = x_i * 100), envs/agents.py:323-328).  Vs PyBullet this
+    stays unpinned; this checks the kernel against angular-momentum conservation instead of against
+    the builder's own restatement.
+
+    From rest (identity attitude, zero velocity and body rates, all four motors in the same state,
+    the props already spinning), one cf2_physics_step whose action changes the motor targets
+    unevenly.  About the yaw axis the body and its four rotors (inertia Ip each, joint axes
+    a = (-1, +1, -1, +1), joint speeds w_j = prop_speed_gain * x_j) hold
+        L_z = (Izz + 4 Ip) wz + Ip * sum_j a_j w_j,
+    which changes only by the external yaw-torque impulse tau dt (the mixer's yaw torque: the same
+    in a run with Ip = 0, whose rotors carry no momentum).  With the prop mass set to 0 (so the
+    locked props add only Ip to the composite inertia) and no damping torque at zero rates:
+        (Izz + 4 Ip) wz(Ip) = Izz wz(0) - Ip * sum_j a_j (w_j' - w_j).
+    The gyroscopic coupling w x L is zero at zero body rates; the motor states after the sub-step
+    (w_j') are read back from the kernel."""
+    import torch
+    import cf2sim.physics as phoenix_physics
+    from cf2sim.physics import BatchedDrone
+    n = 64
+    env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
+    rng = np.random.default_rng(4)
+    a = np.full((n, 4), 0.1, np.float32)
+    a[:, 0] = rng.uniform(-0.9, 0.9, n).astype(np.float32)      # motor 0's target differs, per drone
+    res = {}
+    for ip in ("urdf", 0.0):
+        cfg = build_config(env_id, n, seed=1, auto_reset=False, max_episode_steps=0, latency=0.0,
+                           motor_thrust_noise=0.0, observation_noise=0, domain_randomization=-1)
+        ip_val = float(cfg.prop_inertia) if ip == "urdf" else 0.0
+        cfg.prop_inertia = ip_val
+        cfg.prop_mass = 0.0
+        drone = BatchedDrone(config=cfg, env_id=env_id)
+        phys = phoenix_physics.PyBulletPhysics(drone, None, time_step=None)
+        drone.reset()
+        env, L = drone.env, drone.env.layout
+        sf, si = env.get_state()
+        sf[L.f_pos:L.f_pos + 3] = torch.tensor([0.0, 0.0, 1.0], device=sf.device)[:, None]
+        sf[L.f_quat:L.f_quat + 4] = torch.tensor([0.0, 0.0, 0.0, 1.0], device=sf.device)[:, None]
+        sf[L.f_vel:L.f_vel + 3] = 0.0
+        sf[L.f_omega:L.f_omega + 3] = 0.0
+        sf[L.f_motor:L.f_motor + 4] = 0.5
+        sf[L.f_motor_lo:L.f_motor_lo + 4] = 0.0
+        sf[L.f_ou:L.f_ou + 4] = 0.0
+        si[L.i_flags] |= 1 << 7                      # a sub-step ran since the reset: the props spin
+        env.set_state(sf, si)
+        x_prev = env.get_state()[0][L.f_motor:L.f_motor + 4].cpu().numpy().astype(np.float64)
+        phys.step_forward(torch.from_numpy(a).cuda())
+        sf2, _ = env.get_state()
+        x_new = sf2[L.f_motor:L.f_motor + 4].cpu().numpy().astype(np.float64)
+        wz = sf2[L.f_omega + 2].cpu().numpy().astype(np.float64)
+        izz = float(np.float32(cfg.izz))
+        kq = float(np.float32(cfg.prop_speed_gain))
+        res[ip] = (wz, x_prev, x_new, izz, kq, float(np.float32(ip_val)))
+        env.check_device_errors()
+        drone.close()
+    wz_a, xp, xn, izz, kq, ip = res["urdf"]
+    wz_b, xp_b, xn_b, _, _, _ = res[0.0]
+    assert ip > 0 and kq > 0
+    np.testing.assert_array_equal(xn, xn_b)          # the same motor states: the same thrusts and yaw torque
+    ax = np.array([-1.0, 1.0, -1.0, 1.0])
+    dsp = kq * ((xn - xp) * ax[:, None]).sum(0)     # change of sum_j a_j w_j
+    assert np.abs(dsp).min() > 1.0                   # the rotors' momentum changes in every drone
+    lhs = (izz + 4 * ip) * wz_a
+    rhs = izz * wz_b - ip * dsp
+    reaction = ip * np.abs(dsp)
+    assert np.all(np.abs(lhs - rhs) <= 2e-3 * reaction), (np.abs(lhs - rhs) / reaction).max()
+    # and the reaction is a visible share of the yaw-rate response
+    assert np.all(np.abs(wz_a - wz_b) > 1e-2 * reaction / izz)

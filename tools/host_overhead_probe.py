@@ -63,7 +63,8 @@ def main():
         with torch.cuda.stream(comm):
             pass
     t("stream_context", ctx)
-    t("pack_obs_checked", lambda: pack_obs(env.obs, env.done, cap, out=send))
+    scr = torch.zeros(2, 288, dtype=torch.int32, device=dev)
+    t("pack_obs_checked", lambda: pack_obs(env.obs, env.done, cap, out=send, scratch=scr[0], next_scratch=scr[1]))
 
     def ag():
         with torch.cuda.stream(comm):
@@ -72,17 +73,22 @@ def main():
     t("all_gather_sync", lambda: dist.all_gather_into_tensor(recv, send))
     pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=0)
     pipe.start(env.obs)
-    ag_ = torch.rand(8, n, 4, device=dev)
 
     def full_step():
         buf = pipe.buffer()
         env.step_raw(acts[0].data_ptr(), obs_ptr=buf.data_ptr(), done_ptr=pipe.done_buffer().data_ptr())
-        pipe.publish(ag_[1], ag_[0])
+        pipe.publish()
     t("delta_step_eager_total", full_step)
     pipe.drain()
-    if pipe.exchange == "native":         # the env-step and its exchange as one C call
-        ap, a1, a0 = acts[0].data_ptr(), ag_[1].data_ptr(), ag_[0].data_ptr()
-        t("delta_step_one_call", lambda: pipe.step_and_publish(env, ap, a1, a0))
+    if pipe.exchange == "native":         # the env-step and its exchange as one C call; a batch of 16
+        ap = acts[0].data_ptr()
+        t("delta_step_one_call", lambda: pipe.step_and_publish(env, ap))
+        pipe.drain()
+        ptrs = [acts[r].data_ptr() for r in range(8)]
+        pipe.run(env, ptrs, (-pipe.k) % pipe.unit)
+        t0 = time.perf_counter()
+        pipe.run(env, ptrs, R - R % pipe.unit)
+        out["delta_step_batched_run_host"] = (time.perf_counter() - t0) * 1e6 / (R - R % pipe.unit)
         pipe.drain()
     pipe.close()
     print(json.dumps({k: round(v, 2) for k, v in out.items()}))
