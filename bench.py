@@ -16,20 +16,17 @@ streams from HBM every step, as under a training loop's fresh action and rollout
 
 Multi-GPU: one process per GPU.  Under torchrun the ranks come from the environment; with
 `--gpus N` and no launcher, bench.py starts its own N ranks as child processes before anything
-touches the GPU (the role of the reference's mpi_fork, utils/mpi_tools.py:47-99).  The default
-workload is BASELINE's metric config: 262 144 envs over the whole job (--global-envs), each
-rank stepping its contiguous global-id shard (32 768 envs per GPU at N = 8; "scaling":
-"strong").  Envs are independent, so the physics needs no collective; at N > 1 the reported line
-is the north-star variant with the per-step RCCL all-gather of the observation slab over xGMI
-(--gather-obs, default on at N > 1), pipelined with the next env-step.  By default the exchange
-moves deltas (--gather-mode delta, cf2sim.dist: o_k of every env, a reset bitmap and the reset
-rows' first halves; every rank keeps what it gathered and advances the envs' ages, and any row of
-the [262144, 34] slab is materialised bit-identically on request from those buffers and the
-actions, which every rank holds), 2.36x fewer xGMI bytes than the full rows (--gather-mode full).
-Over RCCL the timed env-steps run back to back with the exchange's pack fused into the env-step
-kernel, and each batch of 16 steps is all-gathered and consumed on the exchange stream while the
-next batch steps (PipelinedObsGather.run / cf2_xchg_run).  The same shards without the gather ("no_gather") and 262 144 envs per GPU
-("weak_scaling") are extra keys of the line.
+touches the GPU (the role of the reference's mpi_fork, utils/mpi_tools.py:47-99).  The envs are
+independent (no collective for the physics), so every rank steps BASELINE's
+262 144-env workload on its own global ids with no data-path collective ("scaling": "weak"; value =
+all ranks' env-steps / the max over ranks of the timed region).  Extra keys of the line:
+"strong_scaling" (the 262 144 envs split over the ranks, 32 768 per GPU at N = 8) and "gather", the
+north star's optional per-step RCCL all-gather of the observations over xGMI for those split envs
+(--gather-obs, default on at N > 1): delta rows (o_k of every env, a reset bitmap and the reset
+rows' first halves; every rank advances the envs' ages and materialises any rows bit-identically
+on request), 2.36x fewer xGMI bytes than the full rows (--gather-mode full), with the env-steps
+back to back (the pack fused into the env-step kernel) and one all-gather + consume per batch of
+16 env-steps on the library's own RCCL communicator (PipelinedObsGather.run / cf2_xchg_run).
 """
 from __future__ import annotations
 
@@ -251,18 +248,25 @@ def parse_args(argv=None):
     # env-steps 50-250); after ~1000 env-steps the reset rate is stationary (tools/reset_rate.py)
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=1000)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak (default): every rank steps BASELINE's 262 144 envs (its own global ids), no data-path "
+                         "collective; strong: --global-envs split over the ranks")
     ap.add_argument("--global-envs", type=int, default=METRIC_GLOBAL_ENVS,
-                    help="envs over the whole job (BASELINE's metric config); each rank steps its contiguous shard")
+                    help="--scaling strong: envs over the whole job, each rank stepping its contiguous shard")
     ap.add_argument("--envs-per-gpu", type=int, default=None,
-                    help="weak scaling instead: this many envs on every rank (overrides --global-envs)")
+                    help="weak scaling with this many envs on every rank (default 262 144)")
     ap.add_argument("--gather-obs", dest="gather_obs", action="store_true", default=None,
-                    help="per-step RCCL all-gather of the obs slab (default: on at N > 1)")
+                    help="also time the north star's per-step RCCL all-gather of the observations over the 262 144 envs "
+                         "split across the ranks (the line's gather key; default: on at N > 1; at N = 1 under a "
+                         "launcher: one RCCL rank)")
     ap.add_argument("--no-gather-obs", dest="gather_obs", action="store_false")
     ap.add_argument("--gather-mode", choices=("delta", "full"), default="delta",
                     help="delta: o_k + reset side slab, rows materialised on request (default); full: the rows")
-    ap.add_argument("--weak-envs", type=int, default=262144,
-                    help="N > 1: the weak_scaling key times this many envs per rank; 0 = skip")
-    ap.add_argument("--weak-steps", type=int, default=1000)
+    ap.add_argument("--gather-steps", type=int, default=2000, help="env-steps the gather key times")
+    ap.add_argument("--gather-envs", type=int, default=METRIC_GLOBAL_ENVS,
+                    help="envs over the whole job in the gather key (split over the ranks)")
+    ap.add_argument("--strong-steps", type=int, default=1000,
+                    help="N > 1: the strong_scaling key times 262 144 envs split over the ranks; 0 = skip")
     ap.add_argument("--oc-envs", type=int, default=1 << 20,
                     help="N = 1: the out-of-cache line steps this many envs (working set far beyond the 256 MB "
                          "Infinity Cache, so state traffic is HBM traffic); 0 = skip")
@@ -315,6 +319,104 @@ def working_set_bytes(env, ring: int) -> int:
     return n * 480 + ring * n * 16 + n * (4 * od + 4 + 1 + 1 + 4 + 4)
 
 
+def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks) -> dict:
+    """The north star's per-step all-gather of the observations ("RCCL all-gather over xGMI only for
+    the returned observation tensor"): --gather-envs (262 144) envs split over the ranks, every
+    env-step's observations made available on every rank (cf2sim.dist.PipelinedObsGather: the delta
+    rows, 2.36x fewer bytes than the full rows; over RCCL the native exchange, env-steps back to back
+    with the pack fused in and one all-gather + consume per batch of 16).  Timed like the headline:
+    barrier + synchronize on both sides of exactly --gather-steps env-steps, max over ranks.  The
+    rows of the last step, materialised on every rank, must equal a full all-gather of them."""
+    import torch
+    import torch.distributed as dist
+    from cf2sim.dist import PipelinedObsGather, delta_supported, gather_rows, shard_range
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    off, n = shard_range(args.gather_envs, rank, world)
+    shards = [shard_range(args.gather_envs, r, world)[1] for r in range(world)]
+    if len(set(shards)) != 1:
+        return {"skipped": f"ragged shards {sorted(set(shards))}"}
+    env = BatchedCrazyflieEnv(args.env_id, n, seed=args.seed, env_id_offset=off, device=dev, **env_kw)
+    bind_synthetic_tables(env, dev)
+    env.reset()
+    ring = args.action_ring
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321)
+    # the job's actions, identical on every rank (a receiver builds every env's history slots from
+    # them, as the policy that computed them would); a rank steps its rows [off, off + n)
+    acts_g = torch.rand(ring, args.gather_envs, 4, device=dev, generator=g) * 2 - 1
+    acts = acts_g[:, off:off + n]
+    act_p = [acts[r].data_ptr() for r in range(ring)]
+    delta = args.gather_mode == "delta" and delta_supported(env.cfg)
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps))
+    native = delta and pipe.exchange == "native"
+    if delta:
+        pipe.start(env.obs)
+
+    def steps_of(steps):
+        if native:
+            pipe.run(env, act_p, steps)
+            return
+        for _ in range(steps):
+            k = pipe.k
+            b = pipe.buffer()
+            if delta:
+                env.step_raw(act_p[k % ring], obs_ptr=b.data_ptr(), done_ptr=pipe.done_buffer().data_ptr())
+            else:
+                env.step_raw(act_p[k % ring], obs_ptr=b.data_ptr())
+            pipe.publish()
+
+    steps_of(args.warmup)
+    pipe.drain()
+    barrier_sync()
+    t0 = time.perf_counter()
+    steps_of(args.gather_steps)
+    pipe.drain()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0)
+    rows_check = None
+    if delta:
+        # rows on request: the whole [gather_envs, D] slab of the last timed step, materialised from
+        # the gathered buffers and the actions, must equal a full all-gather of that step's rows
+        kl = pipe.k - 1
+        a3 = [acts_g[max(kl - d, 0) % ring] for d in range(3)]
+        full = gather_rows(pipe.obs[pipe._where[kl][0]], sizes=shards)     # the obs buffer step kl wrote
+        rows = pipe.rows(*a3)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(rows, full))
+        r0_, r1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0_.record()
+        for _ in range(10):
+            pipe.rows(*a3, out=rows)
+        r1_.record()
+        torch.cuda.synchronize()
+        rows_check = {"step": kl, "rows": args.gather_envs, "equal_to_full_gather": same,
+                      "us_all_rows": r0_.elapsed_time(r1_) * 1e3 / 10}
+        if not same:
+            raise SystemExit("bench.py: the exchanged rows differ from the full all-gather")
+        del full, rows
+    per_rank = pipe.bytes_per_rank_per_step
+    rx = (world - 1) * per_rank                       # bytes this rank receives per step
+    ms = el / args.gather_steps * 1e3
+    out = {"value": args.gather_envs * args.gather_steps / el, "unit": "env-steps/s", "ms_per_step": ms,
+           "steps": args.gather_steps, "global_envs": args.gather_envs, "envs_per_gpu": n, "scaling": "strong",
+           "mode": ("delta rows (o_k + reset bitmap + side slab of the crash budget + predicted time-outs); "
+                    "every rank advances the ages, rows on request" if delta else "full rows"),
+           "exchange": pipe.exchange,
+           "launch": (f"env-steps back to back with the pack fused in, one all-gather + consume per batch of "
+                      f"{pipe.unit} (cf2_xchg_run)" if native else "per-step publish"),
+           "bytes_per_rank_per_step": per_rank, "bytes_in_per_rank_per_step": rx,
+           "full_rows_bytes_per_rank_per_step": n * env.obs_dim * 4,
+           "rx_GBs_per_rank": rx / (ms * 1e-3) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
+           "link_bound_us_per_step": (rx / (world - 1) / (XGMI_PEAK_GBS / 7) * 1e6) if world > 1 else 0.0,
+           "overflows": pipe.overflows(), "rows_on_request": rows_check}
+    env.check_device_errors()
+    pipe.drain()
+    pipe.close()
+    env.close()
+    return out
+
+
 def main(argv=None):
     args = parse_args(argv)
     launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
@@ -354,13 +456,18 @@ def main(argv=None):
 
     from cf2sim.vec_env import BatchedCrazyflieEnv
 
-    if args.envs_per_gpu:
-        n, off, scaling = args.envs_per_gpu, rank * args.envs_per_gpu, "weak"
-        shards = [n] * world
-    else:
+    # the timed workload: BASELINE's metric config (262 144 envs, C4 gust) on every GPU.  The envs
+    # are independent (no collective for the physics), so at N > 1 every rank
+    # steps its own 262 144 global ids with no data-path collective ("scaling": "weak"; --scaling
+    # strong splits the 262 144 over the ranks instead).  The north star's optional per-step
+    # all-gather of the observations is its own measured object of the line ("gather", below).
+    if args.scaling == "strong" and not args.envs_per_gpu:
         off, n = shard_range(args.global_envs, rank, world)
-        scaling = "strong"
         shards = [shard_range(args.global_envs, r, world)[1] for r in range(world)]
+        scaling = "strong"
+    else:
+        n = args.envs_per_gpu or METRIC_GLOBAL_ENVS
+        off, shards, scaling = rank * n, [n] * world, "weak"
     global_envs = sum(shards)
     gather = (world > 1) if args.gather_obs is None else bool(args.gather_obs)
     gather = gather and use_pg
@@ -382,71 +489,17 @@ def main(argv=None):
     env.reset()
     ring = args.action_ring
     g = torch.Generator(device=dev)
-    g.manual_seed(1234)
-    # the job's actions, identical on every rank (the delta exchange rebuilds every env's history
-    # rows from them, as a policy that computed them would); a rank steps its rows [off, off + n)
-    acts_g = torch.rand(ring, global_envs, 4, device=dev, generator=g) * 2 - 1
-    acts = acts_g[:, off:off + n]
+    g.manual_seed(1234 + rank)
+    acts = torch.rand(ring, n, 4, device=dev, generator=g) * 2 - 1
     stream = torch.cuda.current_stream()
-
-    from cf2sim.dist import delta_supported
-    pipe = None
-    gather_mode = None
-    delta = gather and args.gather_mode == "delta"
-    if gather and args.graph:
-        raise SystemExit("bench.py: --graph is for the env-step alone (no --gather-obs)")
-    if delta and (len(set(shards)) != 1 or not delta_supported(env.cfg) or args.envs_per_gpu):
-        delta = False
-    if gather:
-        if len(set(shards)) == 1:
-            pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps))
-            if delta:
-                pipe.start(env.obs)
-                gather_mode = (f"pipelined delta all-gather (o_k + reset bitmap + side slab of "
-                               f"{pipe.cap} resets per rank + predicted time-outs; every rank advances the ages, "
-                               f"rows on request; side stream; {pipe.exchange} exchange)")
-            else:
-                gather_mode = "pipelined all_gather_into_tensor of the rows (2 obs buffers, side stream)"
-        else:
-            gather_mode = "ragged shards: synchronous padded all_gather"
-    kk = [0]                               # env-steps taken (the delta exchange needs a_{k-1})
-    # per-step host work kept small (at the node shard an env-step is ~10 us of GPU time): the
-    # action ring's addresses and views resolved once
+    # per-step host work kept small: the action ring's addresses resolved once
     act_p = [acts[r].data_ptr() for r in range(ring)]
-    act_g = [acts_g[r] for r in range(ring)]
-    pipe_p = None
-    if pipe is not None:
-        pipe_p = ([b.data_ptr() for b in pipe.obs], [b.data_ptr() for b in pipe.done] if delta else None)
-    # the native exchange: env-steps back to back (the pack fused in), one all-gather + consume per
-    # batch of 16 (cf2_xchg_run); the actions of step k are slab k % ring, as in the eager loop
-    native_x = pipe is not None and delta and pipe.exchange == "native"
 
-    def one_step(k, with_gather):
-        j = kk[0]
-        kk[0] += 1
-        r = j % ring
-        if with_gather and pipe is not None:
-            b = pipe.k % pipe.depth
-            pipe.buffer()                  # waits (on the device) until the exchange that read it is done
-            if delta:
-                env.step_raw(act_p[r], obs_ptr=pipe_p[0][b], done_ptr=pipe_p[1][b])
-            else:
-                env.step_raw(act_p[r], obs_ptr=pipe_p[0][b])
-            pipe.publish()
-        else:
-            env.step_raw(act_p[r])
-            if with_gather:
-                env.gather_observations()
+    def steps_of(steps):
+        for k in range(steps):
+            env.step_raw(act_p[k % ring])
 
-    def steps_of(steps, with_gather):
-        if with_gather and native_x:
-            pipe.run(env, act_p, steps)
-            kk[0] += steps
-        else:
-            for k in range(steps):
-                one_step(k, with_gather)
-
-    def run(steps, with_gather, graph=None):
+    def run(steps, graph=None):
         """exactly `steps` env-steps between barrier + synchronize; returns the max-over-ranks wall
         time and this rank's HIP-event time on the launch stream"""
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -457,18 +510,14 @@ def main(argv=None):
             for g_ in graph:
                 g_.replay()
         else:
-            steps_of(steps, with_gather)
-        if with_gather and pipe is not None:
-            pipe.drain()
+            steps_of(steps)
         e1.record(stream)
         torch.cuda.synchronize()
         if use_pg:
             dist.barrier()
         return max_over_ranks(time.perf_counter() - t0), e0.elapsed_time(e1)
 
-    steps_of(args.warmup, gather)
-    if pipe is not None:
-        pipe.drain()
+    steps_of(args.warmup)
     torch.cuda.synchronize()
 
     def capture(steps):
@@ -477,83 +526,44 @@ def main(argv=None):
         g_ = torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g_, stream=s):
-                for k in range(steps):
-                    one_step(k, gather)
-                if pipe is not None:
-                    pipe.drain()
+                steps_of(steps)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         return g_
 
-    graph = None
-    if args.graph:
-        graph = [capture(args.steps)]
+    graph = [capture(args.steps)] if args.graph else None
 
     # ---- timed region: exactly K steps between barrier + synchronize, max over ranks ----
-    elapsed, ev_ms = run(args.steps, gather, graph)
+    elapsed, ev_ms = run(args.steps, graph)
     kern_ms = ev_ms / args.steps
-    rows_check = None
-    if gather and delta and pipe is not None:
-        # rows on request: the whole [global_envs, D] slab of the last timed step, materialised from
-        # the gathered buffers and the actions, must equal a full all-gather of that step's rows
-        from cf2sim.dist import gather_rows
-        kl = pipe.k - 1
-        a3 = [acts_g[max(kl - d, 0) % ring] for d in range(3)]
-        full = gather_rows(pipe.obs[kl % pipe.depth], sizes=shards)
-        rows = pipe.rows(*a3)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(rows, full))
-        r0_, r1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        r0_.record(stream)
-        for _ in range(10):
-            pipe.rows(*a3, out=rows)
-        r1_.record(stream)
-        torch.cuda.synchronize()
-        rows_check = {"step": kl, "rows": global_envs, "equal_to_full_gather": same,
-                      "us_all_rows": r0_.elapsed_time(r1_) * 1e3 / 10}
-        if not same:
-            raise SystemExit("bench.py: the exchanged rows differ from the full all-gather")
-        del full, rows
-    if gather:
-        # the timed region also holds the all-gathers: time the step kernel alone here
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
-        torch.cuda.synchronize()
-        for k in range(50):
-            ev[k][0].record(stream)
-            env.step_raw(acts[k % ring].data_ptr())
-            ev[k][1].record(stream)
-        torch.cuda.synchronize()
-        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / 50
 
-    no_gather = None
+    gather_info = None
     if gather:
-        el2, ev2 = run(args.steps, False)
-        no_gather = {"value": global_envs * args.steps / el2, "unit": "env-steps/s",
-                     "ms_per_step": el2 / args.steps * 1e3, "kernel_ms_per_launch": ev2 / args.steps}
+        gather_info = exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks)
 
-    weak = None
-    if world > 1 and not args.envs_per_gpu and args.weak_envs > 0:
-        # weak scaling: a fixed 262 144 envs per GPU (no gather); max over ranks as above
-        wn = args.weak_envs
-        wenv = BatchedCrazyflieEnv(args.env_id, wn, seed=args.seed, env_id_offset=rank * wn, device=dev, **env_kw)
-        bind_synthetic_tables(wenv, dev)
-        wenv.reset()
-        wacts = torch.rand(ring, wn, 4, device=dev, generator=g) * 2 - 1
-        for k in range(200):
-            wenv.step_raw(wacts[k % ring].data_ptr())
+    strong = None
+    if world > 1 and scaling == "weak" and args.strong_steps > 0:
+        # the same 262 144 envs split over the ranks (32 768 per GPU at N = 8), no collective
+        so, sn = shard_range(METRIC_GLOBAL_ENVS, rank, world)
+        senv = BatchedCrazyflieEnv(args.env_id, sn, seed=args.seed, env_id_offset=so, device=dev, **env_kw)
+        bind_synthetic_tables(senv, dev)
+        senv.reset()
+        sacts = torch.rand(ring, sn, 4, device=dev, generator=g) * 2 - 1
+        sp = [sacts[r].data_ptr() for r in range(ring)]
+        for k in range(args.warmup):
+            senv.step_raw(sp[k % ring])
         barrier_sync()
         t0 = time.perf_counter()
-        for k in range(args.weak_steps):
-            wenv.step_raw(wacts[k % ring].data_ptr())
+        for k in range(args.strong_steps):
+            senv.step_raw(sp[k % ring])
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        wel = max_over_ranks(time.perf_counter() - t0)
-        weak = {"envs_per_gpu": wn, "global_envs": wn * world, "steps": args.weak_steps, "gather_obs": False,
-                "value": wn * world * args.weak_steps / wel, "unit": "env-steps/s",
-                "ms_per_step": wel / args.weak_steps * 1e3}
-        wenv.close()
-        del wacts
+        dist.barrier()
+        sel = max_over_ranks(time.perf_counter() - t0)
+        strong = {"envs_per_gpu": sn, "global_envs": METRIC_GLOBAL_ENVS, "steps": args.strong_steps,
+                  "gather_obs": False, "value": METRIC_GLOBAL_ENVS * args.strong_steps / sel, "unit": "env-steps/s",
+                  "ms_per_step": sel / args.strong_steps * 1e3}
+        senv.close()
+        del sacts
 
     fused = None
     if world == 1 and args.rollout_k > 0:
@@ -703,6 +713,7 @@ def main(argv=None):
                      "hbm_frac": bytes_per_env_step(env) * n / (sus * 1e-6) / 1e9 / HBM_PEAK_GBS}
         del sacts
 
+    from cf2sim.dist import delta_supported
     exchange = None
     if world == 1 and args.exchange_probe and n == METRIC_GLOBAL_ENVS and delta_supported(env.cfg):
         # the delta obs exchange of the 8-GPU shape on one GPU: 8 shards of this step's real rows
@@ -739,7 +750,7 @@ def main(argv=None):
             consume_obs(send, W8, n8, ol, cap, age)
         ev[2].record(stream)
         for _ in range(reps):
-            obs_rows(send, cap, prev_pk, cap, W8, n8, ol, age, acts_g[2], acts_g[1], acts_g[0], out=out_rows)
+            obs_rows(send, cap, prev_pk, cap, W8, n8, ol, age, acts[2], acts[1], acts[0], out=out_rows)
         ev[3].record(stream)
         torch.cuda.synchronize()
         pack_us = ev[0].elapsed_time(ev[1]) * 1e3 / (reps * W8)
@@ -819,23 +830,6 @@ def main(argv=None):
     achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(f"{args.env_id}:N={n}")
     wset = working_set_bytes(env, ring)
-    gather_info = None
-    if gather:
-        per_rank = pipe.bytes_per_rank_per_step if pipe is not None else n * env.obs_dim * 4
-        rx = (world - 1) * per_rank                       # bytes this rank receives per step
-        gather_info = {"mode": gather_mode, "bytes_in_per_rank_per_step": rx, "total_bytes_per_step": world * per_rank,
-                       "full_rows_bytes_in_per_rank_per_step": (global_envs - n) * env.obs_dim * 4,
-                       "overflows": pipe.overflows() if pipe is not None else 0,
-                       "rx_GBs_per_rank": rx / (elapsed / args.steps) / 1e9, "xgmi_peak_GBs": XGMI_PEAK_GBS,
-                       "rx_frac_of_xgmi": rx / (elapsed / args.steps) / 1e9 / XGMI_PEAK_GBS,
-                       "launch": (f"env-steps back to back with the pack fused in, one all-gather + consume per "
-                                  f"batch of {pipe.unit} (cf2_xchg_run)" if native_x else "eager per-step launches"),
-                       "exchange": pipe.exchange if pipe is not None else "padded all_gather",
-                       "rows_on_request": rows_check}
-        if pipe is not None:
-            pipe.drain()
-            pipe.close()
-
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -859,7 +853,8 @@ def main(argv=None):
             "config": {"workload": f"{args.env_id} ({describe(env.cfg)}), {global_envs} envs over {world} GPU(s)"
                                    f" ({n} per GPU)",
                        "envs_per_gpu": n, "global_envs": global_envs, "aggregate_phy_steps": 2,
-                       "parallelism": f"env-shard x{world}", "gather_obs": bool(gather),
+                       "parallelism": f"env-shard x{world}, no data-path collective",
+                       "gather_obs": bool(gather),
                        "graph": bool(args.graph)},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS,
@@ -874,8 +869,7 @@ def main(argv=None):
                          "out_of_cache": out_of_cache},
             "cpu_baseline": cpu,
             "gather": gather_info,
-            "no_gather": no_gather,
-            "weak_scaling": weak,
+            "strong_scaling": strong,
             "fused_rollout": fused,
             "collect": collect_line,
             "streaming_actions": streaming,

@@ -1,11 +1,13 @@
 """bench.py's multi-rank measurement path on a GPU box.
 
 - `bench.py --gpus 2` without a launcher starts its own two ranks (CF2_BENCH_BACKEND=gloo: both
-  ranks share the one MI355X of the test box) on BASELINE's metric config, 262 144 envs over the
-  job, and prints one line with n_gpus = world_size = 2, the per-step observation all-gather on,
-  and the no-gather and weak-scaling keys.
-- Under torchrun with one rank and --gather-obs, the RCCL ("nccl") pipelined all-gather runs
-  (PipelinedObsGather on its side stream), the path the 8-GPU run takes.
+  ranks share the one MI355X of the test box), each stepping BASELINE's metric config (262 144
+  envs) with no collective, and prints one line with n_gpus = world_size = 2, "scaling": "weak",
+  the strong-scaling key and the gather key (the observation exchange over the 262 144 envs split
+  across the ranks).
+- Under torchrun with one rank and --gather-obs, the RCCL ("nccl") native exchange runs (batches
+  of env-steps with the pack fused in, one all-gather + consume each), the path the 8-GPU run
+  takes; its rows equal a full all-gather.
 - PipelinedObsGather's output equals the observations the env-step wrote, step for step."""
 import json
 import os
@@ -19,7 +21,8 @@ import torch
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = ["--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--rollout-k", "0", "--streaming-ring", "0",
-         "--oc-envs", "0", "--weak-steps", "20"]
+         "--oc-envs", "0", "--strong-steps", "20", "--gather-steps", "40", "--collect-steps", "0",
+         "--exchange-probe", "0"]
 
 
 def _env():
@@ -46,27 +49,30 @@ def test_bench_self_launches_two_ranks(gpu):
     assert p.returncode == 0, p.stderr[-3000:]
     d = _line(p.stdout)
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
-    assert d["config"]["global_envs"] == 262144 and d["config"]["envs_per_gpu"] == 131072
-    assert d["config"]["gather_obs"] is True and d["scaling"] == "strong"
-    assert d["value"] > 0 and d["no_gather"]["value"] > 0
-    assert d["weak_scaling"]["global_envs"] == 2 * 262144 and d["weak_scaling"]["value"] > 0
-    # the delta exchange (default): 2.3x fewer bytes than the rows, no side-slab overflow
+    assert d["config"]["global_envs"] == 2 * 262144 and d["config"]["envs_per_gpu"] == 262144
+    assert d["scaling"] == "weak" and d["value"] > 0 and d["config"]["gather_obs"] is True
+    assert d["strong_scaling"]["global_envs"] == 262144 and d["strong_scaling"]["value"] > 0
+    # the delta exchange (default) of the 262 144 envs split over the ranks: 2.3x fewer bytes than
+    # the rows, no side-slab overflow, the rows on request equal to a full all-gather
     gi = d["gather"]
-    assert gi["mode"].startswith("pipelined delta")
-    assert gi["full_rows_bytes_in_per_rank_per_step"] == 131072 * 34 * 4
-    assert gi["bytes_in_per_rank_per_step"] * 2.3 <= gi["full_rows_bytes_in_per_rank_per_step"]
-    assert gi["overflows"] == 0
+    assert gi["mode"].startswith("delta rows") and gi["exchange"] == "gloo" and gi["envs_per_gpu"] == 131072
+    assert gi["full_rows_bytes_per_rank_per_step"] == 131072 * 34 * 4
+    assert gi["bytes_per_rank_per_step"] * 2.3 <= gi["full_rows_bytes_per_rank_per_step"]
+    assert gi["overflows"] == 0 and gi["rows_on_request"]["equal_to_full_gather"] is True
 
 
 def test_bench_rccl_gather_path_one_rank(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--gather-obs",
-           "--global-envs", "32768", *SHORT]
+           "--gather-envs", "32768", *SHORT]
     p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _line(p.stdout)
     assert d["backend"] == "nccl" and d["world_size"] == 1 and d["config"]["gather_obs"] is True
-    assert d["gather"]["mode"].startswith("pipelined delta") and d["value"] > 0 and d["gather"]["overflows"] == 0
+    gi = d["gather"]
+    assert gi["mode"].startswith("delta rows") and gi["exchange"] == "native" and d["value"] > 0
+    assert gi["overflows"] == 0 and gi["rows_on_request"]["equal_to_full_gather"] is True
+    assert "cf2_xchg_run" in gi["launch"]
 
 
 def _pipe_worker(rank, world, port, out):

@@ -80,7 +80,10 @@ def test_metric_config_shards(world):
 
 def test_bench_defaults_are_the_metric_config():
     a = bench.parse_args([])
-    assert a.global_envs == 262144 and a.envs_per_gpu is None
+    # every rank steps BASELINE's 262 144 envs, no data-path collective; the north
+    # star's all-gather splits the 262 144 over the ranks in its own key
+    assert a.scaling == "weak" and a.envs_per_gpu is None and a.gather_envs == 262144
+    assert a.global_envs == 262144 and bench.parse_args(["--scaling", "strong"]).scaling == "strong"
     assert a.gather_obs is None          # on at N > 1, off at N = 1
     assert a.steps == 10000 and a.warmup == 1000
     assert bench.parse_args(["--no-gather-obs"]).gather_obs is False
