@@ -210,6 +210,7 @@ __global__ void __launch_bounds__(XB) obs_rows_kernel(const uint32_t* __restrict
                                                       float* __restrict__ out) {
     constexpr uint32_t OD = 2u * (OL + 4u);
     __shared__ __align__(16) float s_rows[XB * OD];
+    __shared__ __align__(16) float s_ok[XB * OL], s_op[XB * OL];
     const uint32_t tid = threadIdx.x, base = blockIdx.x * XB;
     const uint32_t cnt = nrows - base < XB ? nrows - base : XB;
     const bool live = tid < cnt;
@@ -218,12 +219,27 @@ __global__ void __launch_bounds__(XB) obs_rows_kernel(const uint32_t* __restrict
     const uint32_t* pk = pk_all + (size_t)r * stride;
     const float* okp = reinterpret_cast<const float*>(pk + L.o_slab()) + (size_t)li * OL;
     const float* opp = reinterpret_cast<const float*>(pk_prev_all + (size_t)r * stride_prev + Lp.o_slab()) + (size_t)li * OL;
+    // the block's o_k and o_{k-1} runs staged through LDS with coalesced loads when its rows sit in
+    // one rank (a thread's own 13-float run would take 13 loads 52 B apart)
+    const uint32_t g0 = row0 + base, rf = g0 / L.n;
+    const bool staged = (g0 + cnt - 1u) / L.n == rf;
+    if (staged) {
+        const uint32_t li0 = g0 - rf * L.n;
+        const float* ok0 = reinterpret_cast<const float*>(pk_all + (size_t)rf * stride + L.o_slab()) + (size_t)li0 * OL;
+        const float* op0 =
+            reinterpret_cast<const float*>(pk_prev_all + (size_t)rf * stride_prev + Lp.o_slab()) + (size_t)li0 * OL;
+        rows_to_lds(s_ok, ok0, cnt * OL, ((uintptr_t)ok0 & 15u) == 0);
+        rows_to_lds(s_op, op0, cnt * OL, ((uintptr_t)op0 & 15u) == 0);
+    }
+    __syncthreads();
+    const float* okv = staged ? s_ok + tid * OL : okp;
+    const float* opv = staged ? s_op + tid * OL : opp;
     const bool rs = (pk[L.bits() + li / 32u] >> (li % 32u)) & 1u;
     const uint32_t a = age[i];
     float* row = s_rows + tid * OD;
     if (live) {
 #pragma unroll
-        for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = okp[k];
+        for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = okv[k];
         if (rs) {
             const uint32_t slot = pack_slot(pk, L, li);
             if (slot == PACK_DROPPED) {     // the side slab had no room for its block's resets
@@ -244,7 +260,7 @@ __global__ void __launch_bounds__(XB) obs_rows_kernel(const uint32_t* __restrict
             const float4 a0 = a >= 3u ? reinterpret_cast<const float4*>(a_km2)[i] : ak;
             const float4 h1 = a == 1u ? ak : a1;
 #pragma unroll
-            for (uint32_t k = 0; k < OL; ++k) row[k] = opp[k];
+            for (uint32_t k = 0; k < OL; ++k) row[k] = opv[k];
             row[OL] = a0.x; row[OL + 1u] = a0.y; row[OL + 2u] = a0.z; row[OL + 3u] = a0.w;
             row[2u * OL + 4u] = h1.x; row[2u * OL + 5u] = h1.y; row[2u * OL + 6u] = h1.z; row[2u * OL + 7u] = h1.w;
         }

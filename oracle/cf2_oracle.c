@@ -298,10 +298,12 @@ static void apply_action(const orc_ctx* X, orc_env* E, const REAL a[4], const RE
         REAL noisy;
         if (c->use_motor_dynamics) {
             REAL rot = R_SQRT(tn);
-#ifdef ORACLE_F32
+#if defined(ORACLE_F32) && !defined(ORACLE_REF_MOTOR)
             /* the HIP kernel's form: x += B (rot - x) with x kept as an unevaluated pair x + xl
              * (TwoSum), so the 5 ms recurrence does not accumulate fp32 rounding.  Equal to
-             * A x + B rot for A = 1 - B (agents.py:288); see DESIGN.md section 5. */
+             * A x + B rot for A = 1 - B (agents.py:288); see DESIGN.md section 5.  The fp64 build
+             * and the f32ref build (ORACLE_REF_MOTOR: fp32 in the reference's own form) keep
+             * A x + B rot literally. */
             {
                 REAL inc = E->B[j] * ((rot - E->x[j]) - E->xl[j]);
                 REAL sum = E->x[j] + inc, bb = sum - E->x[j];                       /* TwoSum */

@@ -135,6 +135,41 @@ def test_closed_loop_state_within_1e4_rel_over_240_steps(gpu):
     assert comp.max() < 1e-4, comp.max(1)
 
 
+def test_kernel_no_further_from_fp64_than_the_reference_algebra_in_fp32(gpu):
+    """The fp32 suite above compares the kernel with an fp32 restatement that carries the kernel's
+    own compensated motor recurrence; here the comparison is also made with the reference's own
+    algebra in fp32 (oracle f32ref: x = A x + B u, envs/agents.py:287-288, rounded every sub-step).
+    Closed loop over 240 env-steps (a PD controller on each side's own observation), the
+    reference-default config: the kernel's state is at least as close to the fp64 restatement as
+    the literal fp32 transcription of the reference is, and within 1e-3 of that transcription."""
+    env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
+    kw = dict(observation_noise=0, domain_randomization=-1, motor_thrust_noise=0)
+    n, T, seed = 256, 240, 11
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env = BatchedCrazyflieEnv(env_id, n, seed=seed, **kw)
+    cfg = build_config(env_id, n, seed=seed, **kw)
+    ref64, ref32 = O.OracleEnv(cfg, "f64"), O.OracleEnv(cfg, "f32ref")
+    sl = slice(21, 34)
+    go, r64, r32 = env.reset().cpu().numpy(), ref64.reset(), ref32.reset()
+    alive = np.ones(n, bool)
+    for _ in range(T):
+        go = env.step(torch.from_numpy(pd_actions(go[:, sl], cfg.hover_action)).cuda())[0].cpu().numpy()
+        r64, _, d64, _ = ref64.step(pd_actions(r64[:, sl], cfg.hover_action))
+        r32, _, d32, _ = ref32.step(pd_actions(r32[:, sl], cfg.hover_action))
+        alive &= ~d64 & ~d32
+    g = env.get_state()[0].cpu().numpy()[:13].astype(np.float64)
+    s64, s32 = ref64.get_state()[0][:13], ref32.get_state()[0][:13]
+    env.close()
+    ref64.close()
+    ref32.close()
+    assert alive.sum() >= n // 2
+    def worst(a, b):
+        return max(float(v.max()) for v in state_rel_err(a[:, alive], b[:, alive]).values())
+    e_kernel, e_ref32, e_pair = worst(g, s64), worst(s32, s64), worst(g, s32)
+    assert e_kernel <= 1.2 * e_ref32 + 1e-7, (e_kernel, e_ref32)
+    assert e_pair < 1e-3, e_pair
+
+
 def test_closed_loop_noisy_dr_state_within_1e4_rel_over_240_steps(gpu):
     """The same target on the reference-default config (sensor noise, 10 % DR, motor-thrust OU
     noise, latency): the PD loop acts on the noisy observation; both sides draw the same Philox
