@@ -9,7 +9,7 @@ NENV=${2:-262144}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc -o pmc -- python3 bench.py --steps 30 --warmup 300 --no-cpu-baseline --collect-steps 0 --rollout-k 32 --streaming-ring 0 --oc-envs 0 --exchange-probe 0 --two-streams 0 --global-envs $NENV > $OUT/bench.log 2>&1 || { echo "pmc pass failed"; tail -5 $OUT/bench.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc -o pmc -- python3 bench.py --steps 30 --warmup 300 --no-cpu-baseline --collect-steps 0 --rollout-k 32 --streaming-ring 0 --oc-envs 0 --exchange-probe 0 --two-streams 0 --envs-per-gpu $NENV > $OUT/bench.log 2>&1 || { echo "pmc pass failed"; tail -5 $OUT/bench.log; exit 1; }
 # the fused collect step (cf2_collect_step) on the same workload, from its own per-launch benchmark
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_collect -o pmc -- python3 tools/collect_bench.py --envs $NENV --steps 64 --warmup 300 > $OUT/collect.log 2>&1 || { echo "collect pmc pass failed"; tail -5 $OUT/collect.log; exit 1; }
 # the matrix-core side of the fused collect kernel: MFMA-busy cycles (MI355X_MICROARCH.md: counts cycles,
