@@ -720,7 +720,7 @@ def main(argv=None):
         # and done flags packed as the ranks would (cf2_obs_pack, 32 768 rows each), then a rank's
         # per-step consume of all 262 144 envs (cf2_obs_consume: the ages) and, on request, the
         # materialisation of all 262 144 rows (cf2_obs_rows), timed with HIP events on this stream
-        from cf2sim.dist import consume_obs, default_cap, obs_rows, pack_obs, packed_words
+        from cf2sim.dist import PACK_SCRATCH_WORDS, consume_obs, default_cap, obs_rows, pack_obs, packed_words
         W8, n8, ol = 8, n // 8, env.obs_dim // 2 - 4
         cap = default_cap(n8)
         words = packed_words(n8, ol, cap)
@@ -732,7 +732,7 @@ def main(argv=None):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         reps = 20
 
-        scr = torch.zeros(W8 + 1, 288, dtype=torch.int32, device=dev)
+        scr = torch.zeros(W8 + 1, PACK_SCRATCH_WORDS, dtype=torch.int32, device=dev)
 
         def pack_all(dst):
             for r in range(W8):

@@ -75,8 +75,8 @@ def run_ranks(plan, timeout: float | None = None) -> int:
 # for the gloo rehearsal of the multi-rank path; both produce the same rows bit for bit) ----
 
 PACK_BLOCK = 64       # envs per pack block: one block-table word each (the side slot of the block's first reset)
-PACK_DROPPED = -1     # block-table word (int32 view of 0xFFFFFFFF): the block's resets got no side slot
-PACK_SCRATCH_WORDS = 288   # side-slot counters of a pack (csrc/cf2sim_pack.h), past the largest packed buffer
+PACK_DROPPED = -1     # block-table word (int32 view of 0xFFFFFFFF): the block's resets past its quota got no slot
+PACK_SCRATCH_WORDS = 32    # the spill counter of a pack (csrc/cf2sim_pack.h), past the largest packed buffer
 ZERO_AHEAD = 8        # a consume zeroes the look-ahead rows of the 8 steps after its own
 NO_WATCH = 0xFFFFFFFF
 PRED_BATCH = 4        # eager exchange: the time-out count ring is copied to the host every 4 env-steps
@@ -161,10 +161,12 @@ def pack_obs(obs, reset, cap: int, out=None, scratch=None, next_scratch=None):
     bits[:pb.size] = pb
     out[4 + n * ol:4 + n * ol + nb] = torch.from_numpy(bits.view(np.int32))
     out[1], out[2], out[3] = n, ol, cap
-    # block table: each 64-env block's resets take consecutive slots (blocks in order here; the GPU
-    # hands slots out per XCD region, so only the slots differ, not the rows); a block that does not
-    # fit is dropped
+    # side slots (csrc/cf2sim_pack.h): each 64-env block owns `quota` slots for its first resets; the
+    # excess takes consecutive slots of the spill area (blocks in order here; the GPU's atomic hands
+    # them out in arrival order, so only the slots differ, not the rows), or is dropped
     nblk = (n + PACK_BLOCK - 1) // PACK_BLOCK
+    q = pack_quota(n, cap)
+    spill_base = nblk * q
     cnt = torch.zeros(nblk, dtype=torch.int64)
     idx = torch.nonzero(r).flatten()
     cnt.index_add_(0, idx // PACK_BLOCK, torch.ones_like(idx))
@@ -172,22 +174,36 @@ def pack_obs(obs, reset, cap: int, out=None, scratch=None, next_scratch=None):
     side, used = _side(n, ol), 0
     for b in torch.nonzero(cnt).flatten().tolist():
         c = int(cnt[b])
-        if used + c > cap:
-            btab[b] = PACK_DROPPED
-            continue
-        btab[b] = used
+        first = 0
+        if c > q:
+            if used + c - q > cap - spill_base:
+                first = PACK_DROPPED
+            else:
+                first = spill_base + used
+                used += c - q
+        btab[b] = first
         for s_, i in enumerate(idx[(idx // PACK_BLOCK) == b].tolist()):
-            e = side + (used + s_) * (ol + 5)
+            if s_ < q:
+                slot = b * q + s_
+            elif first == PACK_DROPPED:
+                continue
+            else:
+                slot = first + s_ - q
+            e = side + slot * (ol + 5)
             out[e] = i
             f[e + 1:e + 1 + ol + 4] = obs[i, :ol + 4]
-        used += c
     out[4 + n * ol + nb:4 + n * ol + nb + nblk] = btab.to(torch.int32)
     return out
 
 
+def pack_quota(n: int, cap: int) -> int:
+    """Side slots each 64-env pack block owns (PackLayout::quota): min(cap // blocks, 64)."""
+    return min(int(cap) // ((int(n) + PACK_BLOCK - 1) // PACK_BLOCK), PACK_BLOCK)
+
+
 def _slots(pk, n: int, ol: int, rs):
-    """Side slot of every env (valid where rs; PACK_DROPPED where its block got none) from the block
-    table and the bitmap (cf2sim_pack.h pack_slot)."""
+    """Side slot of every env (valid where rs; PACK_DROPPED where it got none) from its rank among its
+    block's resets, the block's quota and the block table (cf2sim_pack.h pack_slot)."""
     import torch
     nb = (n + 31) // 32
     nblk = (n + PACK_BLOCK - 1) // PACK_BLOCK
@@ -198,7 +214,9 @@ def _slots(pk, n: int, ol: int, rs):
     start[1:] = c[torch.arange(1, nblk) * PACK_BLOCK - 1]
     within = c - rs.to(torch.int64) - start[blk]
     first = btab[blk]
-    return torch.where(first == PACK_DROPPED, torch.full_like(first, PACK_DROPPED), first + within)
+    q = pack_quota(n, int(pk[3]))
+    spill = torch.where(first == PACK_DROPPED, torch.full_like(first, PACK_DROPPED), first + within - q)
+    return torch.where(within < q, blk * q + within, spill)
 
 
 def consume_obs(recv, world: int, n: int, ol: int, cap: int, age, overflow=None, watch_age: int = NO_WATCH,
@@ -621,9 +639,12 @@ class PipelinedObsGather:
             if ev is not None:
                 ev.synchronize()
             lo = max(e - self.npred + ZERO_AHEAD + 1, 0)
+            # one vectorised max over ranks per copy: a torch op per step cost ~3 us of host time
+            # each, ~170 us per batch of 16 (tools/run_host_probe.py), more than the batch's launches
+            mx = buf.numpy().max(axis=1).tolist()
             for t in range(lo, e + 1):
                 if t not in self._counts:
-                    self._counts[t] = int(buf[t % self.npred].max())
+                    self._counts[t] = mx[t % self.npred]
             for t in [t for t in self._counts if t < lo - self.npred]:
                 del self._counts[t]
             break
@@ -658,12 +679,20 @@ class PipelinedObsGather:
             # the count ring to the host every PRED_BATCH steps (read lookahead steps later)
             buf = self._next_pool()
             if self.pred.is_cuda:
-                s = self._stream()
+                # on a side stream behind the exchange: the env stream does not wait for it, and the
+                # native copy (device stores into the pinned buffer) does not hold this thread
+                s = self._side_stream()
                 if self._xchg is not None:
-                    self._lib.cf2_xchg_wait(self._xchg, s.cuda_stream)
-                elif self.comm is not None:
-                    s.wait_event(self._ev_end)
-                buf.copy_(self.pred, non_blocking=True)
+                    from . import _native
+                    _native.check(self._lib.cf2_xchg_pred_to_host(self._xchg, buf.data_ptr(), s.cuda_stream),
+                                  "cf2_xchg_pred_to_host")
+                else:
+                    if self.comm is not None:
+                        s.wait_event(self._ev_end)
+                    else:
+                        s.wait_stream(self._stream())
+                    with torch.cuda.stream(s):
+                        buf.copy_(self.pred, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(s)
             else:
@@ -770,7 +799,13 @@ class PipelinedObsGather:
             raise ValueError("run: at least one action buffer")
         arr = (ctypes.c_void_p * nact)(*act_ptrs)
         rew, trunc, cost, level = env._raw_step_outputs()
-        s = self._stream()
+        # the batches run on a stream of the exchange's own, ordered after the caller's stream and
+        # before it again on return.  Issued on the null stream (torch's default) each batch's first
+        # env-step waited for the previous batch's whole exchange (17.2 us per env-step at 32 768
+        # envs, 14.3 on a pool stream: tools/xchg_run_probe.py --own-stream, gpurun_out/r05k)
+        cur = self._stream()
+        s = self._run_stream()
+        s.wait_stream(cur)
         w = self.watch != NO_WATCH
         done = 0
         while done < steps:
@@ -792,7 +827,14 @@ class PipelinedObsGather:
                 self._copies.append((k0 + nb - 1, buf, ev))
             self._after(k0, nb, cap, q, copied=True)
             done += nb
+        cur.wait_stream(s)
         return self.k - 1
+
+    def _run_stream(self):
+        import torch
+        if getattr(self, "_rs", None) is None:
+            self._rs = torch.cuda.Stream(device=self.device)
+        return self._rs
 
     def _side_stream(self):
         import torch

@@ -25,9 +25,9 @@
 // where a_k is the action of the env-step that produced the row and o_{k-1} is o_k of step k - 1.
 // The receiver tracks age from the bitmaps (exact: reset or not is always known).  A rank with more
 // resets than its side slab holds in one step (an overflow) marks the 64-env pack blocks whose
-// resets got no slot (PACK_DROPPED in the block table): exactly those reset rows get NaN in their
-// o_0 / A parts and every dropped block is counted; their o_k parts and all other rows stay exact,
-// and the following steps are exact again.
+// resets past their quota got no spill slot (PACK_DROPPED in the block table): exactly those reset
+// rows get NaN in their o_0 / A parts and every such block is counted; their o_k parts and all other
+// rows stay exact, and the following steps are exact again.
 // The capacity may change from step to step (the caller sizes the all-gather): TimeLimit
 // truncations are predictable, so the receiver counts, per rank, the envs whose age reaches
 // max_steps - L this step -- at most that many time out L steps later (fewer if they crash first)
@@ -81,8 +81,8 @@ __device__ __forceinline__ void lds_to_rows(float* g, const float* s, uint32_t c
 
 // Sender: one thread per env of this rank (OL: 13 with sensor noise, 17 without).  The block's obs
 // rows are read coalesced into LDS, o_k extracted into an LDS stage and written as one contiguous
-// run of the o_k slab; the reset bitmap comes from wave ballots; each wave is one pack block and
-// takes its resets' side slots with one pack_alloc (cf2sim_pack.h).  next_scratch: the counters of
+// run of the o_k slab; the reset bitmap comes from wave ballots; each wave is one pack block, whose
+// resets past its quota take spill slots with one pack_alloc (cf2sim_pack.h).  next_scratch: the counters of
 // the buffer the next pack on this stream uses (zeroed here; this pack's were zeroed by the last).
 template <uint32_t OL>
 __global__ void __launch_bounds__(XB) obs_pack_kernel(const float* __restrict__ obs, const uint8_t* __restrict__ reset,
@@ -119,8 +119,9 @@ __global__ void __launch_bounds__(XB) obs_pack_kernel(const float* __restrict__ 
 #pragma unroll
         for (uint32_t k = 0; k < OL; ++k) s_o[tid * OL + k] = row[OL + 4u + k];
     }
-    if (r && first != PACK_DROPPED) {
-        uint32_t* e = pk + L.side() + (first + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) * L.entry();
+    const uint32_t slot = pack_entry_slot(L, wbase / XB_PACK, (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), first);
+    if (r && slot != PACK_DROPPED) {
+        uint32_t* e = pk + L.side() + slot * L.entry();
         e[0] = i;
         float* ef = reinterpret_cast<float*>(e + 1);
 #pragma unroll
@@ -198,8 +199,8 @@ __global__ void __launch_bounds__(256) obs_consume_kernel(ConsumeSteps S, uint32
 // buffers of step k (pk_all, capacity L.cap, rank r's at r * stride) and k - 1 (pk_prev_all, Lp.cap,
 // stride_prev), the ages after step
 // k's consume and the actions of steps k, k - 1, k - 2 ([world n, 4] each).  Each thread builds its
-// row in LDS, the block writes them out coalesced.  A reset row finds its side entry through the
-// block table and the bitmap (pack_slot: a pack block's slots are consecutive and in env order).
+// row in LDS, the block writes them out coalesced.  A reset row finds its side entry from its rank
+// among its pack block's resets (the bitmap) and the block table (pack_slot).
 template <uint32_t OL>
 __global__ void __launch_bounds__(XB) obs_rows_kernel(const uint32_t* __restrict__ pk_all, PackLayout L, uint32_t stride,
                                                       const uint32_t* __restrict__ pk_prev_all, PackLayout Lp,
@@ -242,7 +243,7 @@ __global__ void __launch_bounds__(XB) obs_rows_kernel(const uint32_t* __restrict
         for (uint32_t k = 0; k < OL; ++k) row[OL + 4u + k] = okv[k];
         if (rs) {
             const uint32_t slot = pack_slot(pk, L, li);
-            if (slot == PACK_DROPPED) {     // the side slab had no room for its block's resets
+            if (slot == PACK_DROPPED) {     // past its block's quota, and the spill area was full
 #pragma unroll
                 for (uint32_t k = 0; k < OL + 4u; ++k) row[k] = __builtin_nanf("");
 #pragma unroll
@@ -295,6 +296,29 @@ extern "C" int cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint
         hipLaunchKernelGGL(obs_pack_kernel<17>, dim3((n + XB - 1) / XB), dim3(XB), 0, (hipStream_t)stream, obs_dev,
                            reset_dev, L, packed_dev, scratch_dev, next_scratch_dev);
     const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+// The look-ahead ring to the host: one block of lanes storing into the pinned host buffer through
+// its device mapping.  hipMemcpyAsync device -> pinned host held the calling thread until the copy
+// had run (ROCm 7 on MI355X: the next batch's first env-step started 18 us after the exchange's end,
+// gpurun_out/r05f trace), which serialised each batch behind the previous exchange; kernel stores
+// to the mapped buffer leave the host thread free.
+__global__ void __launch_bounds__(256) words_to_host_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
+                                                             uint32_t n) {
+    for (uint32_t i = threadIdx.x; i < n; i += 256u) dst[i] = src[i];
+}
+
+static int words_to_host(const uint32_t* src_dev, uint32_t* dst_host, uint32_t n, hipStream_t st) {
+    void* dp = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dp, dst_host, 0);
+    if (e != hipSuccess || !dp) {                 // not a mapped pinned buffer: the runtime's copy
+        (void)hipGetLastError();
+        e = hipMemcpyAsync(dst_host, src_dev, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+        return e == hipSuccess ? CF2_OK : hip_fail(e);
+    }
+    hipLaunchKernelGGL(words_to_host_kernel, dim3(1), dim3(256), 0, st, src_dev, (uint32_t*)dp, n);
+    e = hipGetLastError();
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
@@ -558,9 +582,8 @@ static int xchg_exchange(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint
     int st = xchg_consume(x, k0, nb, q, cap);
     if (st != CF2_OK) return st;
     if (pred_host && x->pred) {
-        e = hipMemcpyAsync(pred_host, x->pred, (size_t)x->npred * x->world * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           x->xs);
-        if (e != hipSuccess) return hip_fail(e);
+        st = words_to_host(x->pred, pred_host, x->npred * x->world, x->xs);
+        if (st != CF2_OK) return st;
     }
     e = hipEventRecord(x->end, x->xs);
     if (e != hipSuccess) return hip_fail(e);
@@ -600,6 +623,16 @@ extern "C" int cf2_xchg_wait(cf2_xchg* x, void* stream) {
     if (!x->end_rec) return CF2_OK;
     const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->end, 0);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
+}
+
+extern "C" int cf2_xchg_pred_to_host(cf2_xchg* x, uint32_t* pred_host, void* stream) {
+    if (!x || !x->registered || !x->pred || !pred_host) return CF2_ERR_INVALID_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    if (x->end_rec) {
+        const hipError_t e = hipStreamWaitEvent(st, x->end, 0);
+        if (e != hipSuccess) return hip_fail(e);
+    }
+    return words_to_host(x->pred, pred_host, x->npred * x->world, st);
 }
 
 extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,

@@ -6,17 +6,19 @@
 //   [0] 0 (reserved)   [1] n   [2] OL   [3] cap
 //   [4, 4 + n OL)                       o_k rows
 //   [.., + ceil(n / 32))                reset bitmap, env i = bit i % 32 of word i / 32
-//   [.., + ceil(n / 64))                block table: per 64-env pack block, the side slot of its first
-//                                       reset (its resets hold consecutive slots, in env order), or
-//                                       PACK_DROPPED when the side slab had no room for them
+//   [.., + ceil(n / 64))                block table: per 64-env pack block, the first spill slot of its
+//                                       resets past its quota (or PACK_DROPPED: the spill area had no
+//                                       room for them; 0 when the block has no more than its quota)
 //   [.., + cap (OL + 5))                side entries: local env index, o_0[OL], A[4]
-// Side slots are handed out per pack block (never per env): from 16 384 envs on, 3/4 of the capacity
-// as 8 regions, one per XCD, each counted by an atomic of its own (hardware XCC_ID), and the rest as
-// a shared spill region with one more counter, used when the block's XCD region is full (then the
-// other XCDs' regions); below that one shared region.  One counter for all
-// blocks serialised at the memory-side atomic unit (~35 ns per atomic on one address: 19.5 us for
-// the 512 per-wave atomics of a 32 768-env pack, round 4), eight of them split that queue.
-// The counters live in a per-buffer scratch area that is never sent (PACK_SCRATCH_WORDS after the
+// Side slots: the first nblk * quota slots belong to the pack blocks, quota = min(cap / nblk, 64)
+// consecutive slots each, taken by the block's first quota resets in env order with no atomic; the
+// rest of the capacity is a shared spill area, where a block with more resets than its quota takes
+// the excess as consecutive slots with one atomic on a counter.  At the default capacity (7.5 % of
+// the shard: quota 4) 88 % of the blocks of the steady 4.1 % reset rate need no atomic.  Every block
+// taking its slots from one counter serialised at the memory-side atomic unit (~35 ns per atomic on
+// one address: 19.5 us for a 32 768-env pack, round 4); eight per-XCD counters (round 5) still cost
+// the fused step ~2 us at 32 768 envs.
+// The counter lives in a per-buffer scratch area that is never sent (PACK_SCRATCH_WORDS after the
 // largest packed buffer); a pack zeroes the scratch of the buffer the next pack on its stream uses.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -25,9 +27,8 @@
 namespace cf2 {
 
 constexpr uint32_t XB_PACK = 64;                  // envs per pack block (one block-table word each)
-constexpr uint32_t PACK_DROPPED = 0xFFFFFFFFu;     // block-table value: the block's resets got no slot
-constexpr uint32_t PACK_XCDS = 8, PACK_CTR_STRIDE = 32;     // counters 128 B apart
-constexpr uint32_t PACK_SCRATCH_WORDS = (PACK_XCDS + 1) * PACK_CTR_STRIDE;
+constexpr uint32_t PACK_DROPPED = 0xFFFFFFFFu;     // block-table value: its resets past the quota got no slot
+constexpr uint32_t PACK_SCRATCH_WORDS = 32;     // the spill counter (one 128-B line)
 
 struct PackLayout {
     uint32_t n, ol, cap;
@@ -38,16 +39,12 @@ struct PackLayout {
     __host__ __device__ uint32_t side() const { return btab() + (n + XB_PACK - 1u) / XB_PACK; }
     __host__ __device__ uint32_t entry() const { return ol + 5u; }
     __host__ __device__ uint32_t words() const { return (side() + cap * entry() + 3u) & ~3u; }
-    // side slots per XCD region (3/4 of the capacity over the 8 regions) and of the spill region.
-    // Below 256 pack blocks (16 384 envs) there are few atomics to split, and regions would waste
-    // room (a small launch does not spread its blocks over all XCDs): one shared region then.
-    __host__ __device__ uint32_t region() const { return n >= 256u * XB_PACK ? (cap * 3u) / (4u * PACK_XCDS) : 0u; }
-    __host__ __device__ uint32_t spill() const { return cap - PACK_XCDS * region(); }
+    __host__ __device__ uint32_t nblk() const { return (n + XB_PACK - 1u) / XB_PACK; }
+    // side slots each pack block owns, then the start and size of the shared spill area
+    __host__ __device__ uint32_t quota() const { const uint32_t q = cap / nblk(); return q < XB_PACK ? q : XB_PACK; }
+    __host__ __device__ uint32_t spill_base() const { return nblk() * quota(); }
+    __host__ __device__ uint32_t spill() const { return cap - spill_base(); }
 };
-
-__device__ __forceinline__ uint32_t pack_xcc_id() {
-    return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & (PACK_XCDS - 1u);     // HW_REG XCC_ID
-}
 
 // The exchange's pack fused into the env-step (cf2_step_packed): where step_kernel_small writes the
 // packed buffer of its envs besides their observation rows
@@ -58,36 +55,33 @@ struct PackIO {
     uint32_t cap;
 };
 
-// The first side slot of a pack block with c > 0 resets (one thread calls it), or PACK_DROPPED:
-// the block's XCD region, else the spill region, else the other XCDs' regions (a failed attempt
-// leaves that counter past its region, so the region's remaining slots stay unused: the side slab
-// overflows only within a few blocks' resets of full).
+// The block-table word of a pack block with c resets (one thread calls it): 0 when they fit the
+// block's quota, else the first of c - quota consecutive spill slots, or PACK_DROPPED when the spill
+// area has no room for them (a failed attempt leaves the counter past the area, so it overflows
+// only within one block's excess of full).
 __device__ __forceinline__ uint32_t pack_alloc(const PackLayout& L, uint32_t* scratch, uint32_t c) {
-    const uint32_t x = pack_xcc_id(), r = L.region();
-    if (r >= c) {
-        const uint32_t old = atomicAdd(scratch + x * PACK_CTR_STRIDE, c);
-        if (old + c <= r) return x * r + old;
-    }
-    const uint32_t old = atomicAdd(scratch + PACK_XCDS * PACK_CTR_STRIDE, c);
-    if (old + c <= L.spill()) return PACK_XCDS * r + old;
-    if (r >= c) {
-        for (uint32_t t = 1; t < PACK_XCDS; ++t) {
-            const uint32_t y = (x + t) & (PACK_XCDS - 1u);
-            const uint32_t o = atomicAdd(scratch + y * PACK_CTR_STRIDE, c);
-            if (o + c <= r) return y * r + o;
-        }
-    }
-    return PACK_DROPPED;
+    const uint32_t q = L.quota();
+    if (c <= q) return 0u;
+    const uint32_t e = c - q, old = atomicAdd(scratch, e);
+    return old + e <= L.spill() ? L.spill_base() + old : PACK_DROPPED;
+}
+
+// The side slot of the reset of rank `rank` (resets before it in its pack block) in block blk, whose
+// block-table word is `first`, or PACK_DROPPED
+__host__ __device__ __forceinline__ uint32_t pack_entry_slot(const PackLayout& L, uint32_t blk, uint32_t rank,
+                                                             uint32_t first) {
+    const uint32_t q = L.quota();
+    if (rank < q) return blk * q + rank;
+    return first == PACK_DROPPED ? PACK_DROPPED : first + (rank - q);
 }
 
 // The side slot of local env li (a reset env) from the block table and the bitmap, or PACK_DROPPED.
 __device__ __forceinline__ uint32_t pack_slot(const uint32_t* pk, const PackLayout& L, uint32_t li) {
-    const uint32_t b = li / XB_PACK, first = pk[L.btab() + b];
-    if (first == PACK_DROPPED) return PACK_DROPPED;
-    const uint32_t w0 = b * (XB_PACK / 32u), wl = li / 32u;
-    uint32_t slot = first;
-    for (uint32_t w = w0; w < wl; ++w) slot += (uint32_t)__popc(pk[L.bits() + w]);
-    return slot + (uint32_t)__popc(pk[L.bits() + wl] & ((1u << (li % 32u)) - 1u));
+    const uint32_t b = li / XB_PACK, w0 = b * (XB_PACK / 32u), wl = li / 32u;
+    uint32_t rank = 0;
+    for (uint32_t w = w0; w < wl; ++w) rank += (uint32_t)__popc(pk[L.bits() + w]);
+    rank += (uint32_t)__popc(pk[L.bits() + wl] & ((1u << (li % 32u)) - 1u));
+    return pack_entry_slot(L, b, rank, pk[L.btab() + b]);
 }
 
 }  // namespace cf2

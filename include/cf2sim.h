@@ -406,7 +406,11 @@ int  cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride,
  * fused in (cf2_step_packed), then the batch's exchange at
  * capacity cap; pred_host (pinned, npred x world words, or NULL) receives the look-ahead ring after
  * the batch's consume.  cf2_xchg_env_step: cf2_xchg_run of one step.  cf2_xchg_wait(x, stream): a
- * stream waits until every exchange issued so far is complete.  RCCL failures return CF2_ERR_HIP. */
+ * stream waits until every exchange issued so far is complete.  cf2_xchg_pred_to_host(x, pred_host,
+ * stream): the same wait, then the look-ahead ring to pred_host.  Both ring copies are device stores
+ * into the pinned buffer's mapping (a kernel on the stream), which never hold the calling thread;
+ * memory that is not mapped pinned memory falls back to hipMemcpyAsync.  RCCL failures return
+ * CF2_ERR_HIP. */
 typedef struct cf2_xchg cf2_xchg;
 int  cf2_xchg_bind(const char* rccl_path);
 int  cf2_xchg_unique_id(uint8_t* id_out, size_t id_len);
@@ -421,6 +425,7 @@ int  cf2_xchg_register(cf2_xchg* x, uint32_t n, uint32_t obs_len, uint32_t watch
 int  cf2_xchg_publish(cf2_xchg* x, uint64_t k, uint32_t cap, uint32_t region, void* env_stream);
 int  cf2_xchg_wait_free(cf2_xchg* x, uint32_t region, void* stream);
 int  cf2_xchg_wait(cf2_xchg* x, void* stream);
+int  cf2_xchg_pred_to_host(cf2_xchg* x, uint32_t* pred_host, void* stream);
 int  cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
                   const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
                   float* level_dev, uint32_t* pred_host, void* env_stream);

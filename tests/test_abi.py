@@ -128,7 +128,7 @@ def test_obs_exchange_error_paths(lib):
     assert lib.cf2_obs_pack(None, None, 8, 13, 1, None, None, None, None) == -1
     assert lib.cf2_step_packed(*([None] * 11), 1, None) == -1
     w = lib.cf2_obs_packed_words(32768, 13, 32768)
-    assert lib.cf2_xchg_send_words(32768, 13, 2, 16) == 2 * 16 * (w + 288)
+    assert lib.cf2_xchg_send_words(32768, 13, 2, 16) == 2 * 16 * (w + 32)
     assert lib.cf2_xchg_recv_words(32768, 13, 8, 2, 16) == 2 * 8 * 16 * w
     assert lib.cf2_xchg_send_words(32768, 13, 1, 16) == 0 and lib.cf2_xchg_recv_words(32768, 13, 8, 2, 65) == 0
     assert lib.cf2_obs_consume(None, 1, 8, 13, 1, None, None, 0, None, None, None) == -1
@@ -139,4 +139,5 @@ def test_obs_exchange_error_paths(lib):
     assert lib.cf2_xchg_create(idb, 128, 1, 0, 1, ctypes.byref(h)) == -1
     assert lib.cf2_xchg_create(idb, 128, 1, 0, 9, ctypes.byref(h)) == -1
     assert lib.cf2_xchg_publish(None, 0, 1, 0, None) == -1 and lib.cf2_xchg_wait(None, None) == -1
+    assert lib.cf2_xchg_pred_to_host(None, None, None) == -1
     assert lib.cf2_xchg_run(None, None, 0, 8, 1, 0, None, 1, None, None, None, None, None, None) == -1

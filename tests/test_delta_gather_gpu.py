@@ -88,11 +88,12 @@ def test_kernels_equal_torch_ops(gpu, world, n, ol, cap):
 
 
 def test_overflow_nans_exactly_the_reset_rows_that_got_no_slot(gpu):
-    """A rank with more resets than its side slab: the reset rows of exactly the 64-env blocks its
-    packed buffer marks dropped have NaN in o_0 / A, their o_k parts and every other row (that
-    rank's, its other reset rows, the other rank's) are exactly the rows the history rules give,
-    and the overflow count is the number of dropped blocks."""
-    from cf2sim.dist import PACK_BLOCK, PACK_DROPPED, consume_obs, obs_rows, pack_obs, packed_words
+    """A rank with more resets than its side slab: in exactly the 64-env blocks its packed buffer
+    marks dropped, the reset rows past the block's quota have NaN in o_0 / A; their o_k parts and
+    every other row (the dropped blocks' first `quota` resets, that rank's other reset rows, the
+    other rank's) are exactly the rows the history rules give, and the overflow count is the number
+    of dropped blocks."""
+    from cf2sim.dist import PACK_BLOCK, PACK_DROPPED, consume_obs, obs_rows, pack_obs, pack_quota, packed_words
     world, n, ol = 2, 3000, 13
     od = 2 * (ol + 4)
     prev, cur, _, age, acts = _synthetic(world, n, ol, seed=9)
@@ -133,8 +134,17 @@ def test_overflow_nans_exactly_the_reset_rows_that_got_no_slot(gpu):
     rs = reset.bool()
     exp[rs, :ol + 4] = cur[rs, :ol + 4]
     exp[rs, 2 * ol + 4:] = cur[rs, ol:ol + 4]
-    lost = rs & dropped_env
+    # a dropped block keeps its first `quota` resets (their own slots); only the excess is lost
+    rank = torch.zeros(world * n, dtype=torch.int64)
+    for b0 in range(0, world * n, n):
+        for s0 in range(b0, b0 + n, PACK_BLOCK):
+            blk = rs[s0:min(s0 + PACK_BLOCK, b0 + n)].to(torch.int64)
+            rank[s0:s0 + blk.numel()] = torch.cumsum(blk, 0) - blk
+    q = pack_quota(n, cap)
+    assert q == 2
+    lost = rs & dropped_env & (rank >= q)
     assert 0 < int(lost.sum()) < int(rs[:n].sum()), "some, not all, of rank 0's reset rows are lost"
+    assert not bool((rs & dropped_env & (rank < q)).logical_and(torch.isnan(rows).any(1)).any())
     nan_part = torch.zeros(world * n, od, dtype=torch.bool)
     nan_part[lost, :ol + 4] = True
     nan_part[lost, 2 * ol + 4:] = True
@@ -283,7 +293,7 @@ def test_operands_the_kernels_would_overrun_are_rejected(gpu):
     """Host-side checks before the launch: a uint8 age vector (half the bytes the kernel indexes),
     short rows / packed buffers, or a pack whose next counters are its own raise ValueError instead
     of faulting on the device."""
-    from cf2sim.dist import consume_obs, obs_rows, pack_obs, packed_words
+    from cf2sim.dist import PACK_SCRATCH_WORDS, consume_obs, obs_rows, pack_obs, packed_words
     n, ol, cap = 256, 13, 16
     od = 2 * (ol + 4)
     prev = torch.zeros(n, od, device=gpu)
@@ -301,6 +311,6 @@ def test_operands_the_kernels_would_overrun_are_rejected(gpu):
         obs_rows(pk[: packed_words(n, ol, cap) // 2], cap, pk, cap, 1, n, ol, good_age, a, a, a)
     with pytest.raises(ValueError):
         pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap, out=torch.zeros(8, dtype=torch.int32, device=gpu))
-    scr = torch.zeros(288, dtype=torch.int32, device=gpu)
+    scr = torch.zeros(PACK_SCRATCH_WORDS, dtype=torch.int32, device=gpu)
     with pytest.raises(ValueError):
         pack_obs(prev, torch.zeros(n, dtype=torch.uint8, device=gpu), cap, out=pk, scratch=scr, next_scratch=scr)

@@ -125,6 +125,55 @@ def test_full_size_hj_adversary_slices(gpu):
     full.close()
 
 
+def test_full_size_hj_adversary_resynchronised_every_step(gpu):
+    """The strict form of the test above, with no env exempt.  Before every env-step the
+    restatement's slices are loaded with the kernel's own state (cf2_get_state ->
+    OracleEnv.set_state), so each step starts both sides from identical bits and only one step's
+    rounding can separate them; a tie in the HJ branch would then need the state within ~1 ulp of a
+    grid midpoint.  Every env of every slice: observation within 2e-5 mixed abs/rel, done and
+    disturbance level exact, at the full size and over 30 env-steps with resets."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    from test_gpu_parity import _synthetic_tables
+    env_id, T = "DroneHoverBulletFreeEnvWithRandomHJAdversary-v0", 30
+    V = _synthetic_tables(tuple(range(3)), seed=1)
+    table_of_level = [lv % 3 for lv in range(21)]
+    full = BatchedCrazyflieEnv(env_id, N, seed=5)
+    full.bind_hj_tables(torch.from_numpy(V).cuda(), table_of_level)
+    refs = []
+    for k in SLICES:
+        r = O.OracleEnv(build_config(env_id, SLICE, seed=5, env_id_offset=k), precision="f32")
+        r.bind_tables(V, table_of_level)
+        refs.append(r)
+    full.reset()
+    for r in refs:
+        r.reset()
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(12)
+    worst, resets = 0.0, 0
+    for t in range(T):
+        gsf, gsi = full.get_state()
+        gsf, gsi = gsf.cpu().numpy(), gsi.cpu().numpy()
+        for k, r in zip(SLICES, refs):
+            r.set_state(np.ascontiguousarray(gsf[:, k:k + SLICE]), np.ascontiguousarray(gsi[:, k:k + SLICE]))
+        a = ((torch.rand(N, 4, device="cuda", generator=gen) * 2 - 1) * 0.25 + 0.1111).contiguous()
+        g_o, _, g_d, g_i = full.step(a)
+        g_o, g_d = g_o.cpu().numpy(), g_d.cpu().numpy().astype(bool)
+        lv = g_i["disturbance_level"].cpu().numpy()
+        a_np = a.cpu().numpy()
+        for k, r in zip(SLICES, refs):
+            r_o, _, r_d, r_i = r.step(a_np[k:k + SLICE])
+            worst = max(worst, _nerr(g_o[k:k + SLICE], r_o))
+            np.testing.assert_array_equal(g_d[k:k + SLICE], r_d)
+            np.testing.assert_allclose(lv[k:k + SLICE], r_i["level"], atol=1e-6)
+            resets += int(r_d.sum())
+    assert worst < 2e-5, worst
+    assert resets > 0
+    full.check_device_errors()
+    full.close()
+    for r in refs:
+        r.close()
+
+
 def test_maximum_env_count(gpu):
     """CF2_MAX_ENVS_PER_CTX (2^23 envs, 4 GB of state in one context): the largest grid steps
     with finite outputs, and its first and last 256 envs equal the fp32 restatement run on those

@@ -377,3 +377,33 @@ def test_downwash_formations_long_horizon_closed_loop(gpu):
             assert float((e < 5e-4).mean()) >= 0.93, (t, float((e < 5e-4).mean()))
     env.close()
     ref.close()
+
+
+def test_downwash_formations_resynchronised_every_step(gpu):
+    """The strict form of the long-horizon test above, with no drone exempt: the same 240
+    closed-loop env-steps, but before every env-step the restatement is loaded with the kernel's
+    own state (cf2_get_state -> OracleEnv.set_state), so the chaotic wake crossings cannot
+    accumulate ulp differences and each step is compared from identical bits.  Every drone of every
+    env-step: observation within 2e-5 mixed abs/rel, done exact."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    env_id, n, T = "DroneHoverBulletFreeEnvWithDownwash-v0", 512, 240
+    env = BatchedCrazyflieEnv(env_id, n, seed=3)
+    cfg = build_config(env_id, n, seed=3)
+    ref = O.OracleEnv(cfg, precision="f32")
+    go = env.reset().cpu().numpy()
+    ref.reset()
+    worst, dones = 0.0, 0
+    for t in range(T):
+        gsf, gsi = env.get_state()
+        ref.set_state(gsf.cpu().numpy(), gsi.cpu().numpy())
+        a = pd_actions(go[:, 17:30], cfg.hover_action)
+        g_o, _, g_d, _ = env.step(torch.from_numpy(a).cuda())
+        r_o, _, r_d, _ = ref.step(a)
+        go = g_o.cpu().numpy()
+        worst = max(worst, float((np.abs(go - r_o) / (1 + np.abs(r_o))).max()))
+        np.testing.assert_array_equal(g_d.cpu().numpy().astype(bool), r_d)
+        dones += int(r_d.sum())
+    assert worst < 2e-5, worst
+    env.check_device_errors()
+    env.close()
+    ref.close()

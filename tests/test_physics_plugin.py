@@ -164,7 +164,8 @@ def test_prop_spin_up_reaction_is_the_rotors_angular_momentum(gpu):
     env_id = "DroneHoverBulletFreeEnvWithoutAdversary-v0"
     rng = np.random.default_rng(4)
     a = np.full((n, 4), 0.1, np.float32)
-    a[:, 0] = rng.uniform(-0.9, 0.9, n).astype(np.float32)      # motor 0's target differs, per drone
+    # motor 0's target differs from the other three's (0.1) by 0.4-1.0, per drone
+    a[:, 0] = (rng.choice([-1.0, 1.0], n) * rng.uniform(0.5, 0.9, n)).astype(np.float32)
     res = {}
     for ip in ("urdf", 0.0):
         cfg = build_config(env_id, n, seed=1, auto_reset=False, max_episode_steps=0, latency=0.0,
@@ -202,7 +203,7 @@ def test_prop_spin_up_reaction_is_the_rotors_angular_momentum(gpu):
     np.testing.assert_array_equal(xn, xn_b)          # the same motor states: the same thrusts and yaw torque
     ax = np.array([-1.0, 1.0, -1.0, 1.0])
     dsp = kq * ((xn - xp) * ax[:, None]).sum(0)     # change of sum_j a_j w_j
-    assert np.abs(dsp).min() > 1.0                   # the rotors' momentum changes in every drone
+    assert np.abs(dsp).min() > 0.5                   # the rotors' momentum changes in every drone
     lhs = (izz + 4 * ip) * wz_a
     rhs = izz * wz_b - ip * dsp
     reaction = ip * np.abs(dsp)

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=600)
     ap.add_argument("--unit", type=int, default=16)
     ap.add_argument("--env-id", default="DroneHoverBulletFreeEnvWithGust-v0")
+    ap.add_argument("--own-stream", action="store_true", help="run on a pool stream, not the null stream")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -31,6 +32,8 @@ def main():
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", device_id=dev)
     n = args.envs
+    if args.own_stream:
+        torch.cuda.set_stream(torch.cuda.Stream())
     env = BatchedCrazyflieEnv(args.env_id, n, seed=0, device=dev)
     env.reset()
     g = torch.Generator(device=dev)
@@ -73,6 +76,12 @@ def main():
     # align to the unit, then warm up
     batched((-pipe.k) % args.unit + args.warmup)
     res["run_us"], res["run_gpu_us"] = timed(batched, args.steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pipe.run(env, ptrs, args.steps)        # the host's issue time alone (the GPU catches up after)
+    res["run_host_issue_us"] = (time.perf_counter() - t0) * 1e6 / args.steps
+    pipe.drain()
+    torch.cuda.synchronize()
     res["overflows"] = pipe.overflows()
     res["bytes_per_rank_per_step"] = pipe.bytes_per_rank_per_step
     # rows on request: all rows of the last step
