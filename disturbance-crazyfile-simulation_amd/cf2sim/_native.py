@@ -99,7 +99,7 @@ def load() -> ctypes.CDLL:
     lib.cf2_obs_packed_words.restype = ctypes.c_size_t
     lib.cf2_obs_packed_words.argtypes = [u32, u32, u32]
     lib.cf2_obs_pack.argtypes = [vp, vp, u32, u32, u32, vp, vp, vp, vp]
-    lib.cf2_step_packed.argtypes = [vp] * 11 + [u32, vp]
+    lib.cf2_step_packed.argtypes = [vp] * 10 + [u32, vp]
     lib.cf2_xchg_send_words.restype = ctypes.c_size_t
     lib.cf2_xchg_send_words.argtypes = [u32, u32, u32, u32]
     lib.cf2_xchg_recv_words.restype = ctypes.c_size_t

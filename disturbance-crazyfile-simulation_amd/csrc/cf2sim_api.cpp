@@ -354,9 +354,9 @@ int cf2_step(cf2_ctx* ctx, const float* act_dev, const float* dstb_dev, float* o
 
 int cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
                     uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* packed_dev, uint32_t* scratch_dev,
-                    uint32_t* next_scratch_dev, uint32_t cap, void* stream) {
+                    uint32_t cap, void* stream) {
     if (!ctx || !act_dev || !obs_dev || !rew_dev || !done_dev || !packed_dev || !scratch_dev) return CF2_ERR_INVALID_ARG;
-    if (cap > ctx->P.N || scratch_dev == next_scratch_dev) return CF2_ERR_INVALID_ARG;
+    if (cap > ctx->P.N) return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_EXTERNAL) return CF2_ERR_INVALID_ARG;
     if (ctx->cfg.disturbance == CF2_DSTB_HJ && !ctx->P.V) return CF2_ERR_NO_TABLE;
     if (ctx->P.ground_effect) return CF2_ERR_UNSUPPORTED;
@@ -364,7 +364,7 @@ int cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* r
         ((uintptr_t)scratch_dev & 3u) != 0)
         return CF2_ERR_INVALID_ARG;
     StepIO io{ctx->sf, act_dev, nullptr, obs_dev, rew_dev, done_dev, trunc_dev, cost_dev, level_dev, nullptr};
-    const PackIO pio{packed_dev, scratch_dev, next_scratch_dev, cap};
+    const PackIO pio{packed_dev, scratch_dev, cap};
     const hipError_t e = launch_step_packed(ctx->P, io, pio, (hipStream_t)stream);
     if (e == hipErrorNotSupported) return CF2_ERR_UNSUPPORTED;
     return e == hipSuccess ? CF2_OK : hip_fail(e);

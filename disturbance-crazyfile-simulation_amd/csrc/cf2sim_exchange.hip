@@ -309,6 +309,21 @@ __global__ void __launch_bounds__(256) words_to_host_kernel(const uint32_t* __re
     for (uint32_t i = threadIdx.x; i < n; i += 256u) dst[i] = src[i];
 }
 
+// A batch's packed buffers before its env-steps (cf2_xchg_run): each buffer's header words and
+// zeroed spill counters (the fused pack leaves both to its caller, cf2sim_kernels.hip), and the
+// counter of the next region's first buffer, which a per-step publish after the batch counts in
+__global__ void __launch_bounds__(256) pack_prep_kernel(uint32_t* __restrict__ send, uint32_t words, uint32_t nb,
+                                                         uint32_t n, uint32_t ol, uint32_t cap,
+                                                         uint32_t* __restrict__ scratch, uint32_t* __restrict__ next0) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t k = t; k < nb * PACK_SCRATCH_WORDS; k += 256u) scratch[k] = 0u;
+    if (t < PACK_SCRATCH_WORDS) next0[t] = 0u;
+    if (t < nb) {
+        uint32_t* h = send + (size_t)t * words;
+        h[0] = 0u; h[1] = n; h[2] = ol; h[3] = cap;
+    }
+}
+
 static int words_to_host(const uint32_t* src_dev, uint32_t* dst_host, uint32_t n, hipStream_t st) {
     void* dp = nullptr;
     hipError_t e = hipHostGetDevicePointer(&dp, dst_host, 0);
@@ -470,6 +485,7 @@ extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world,
     // (at equal priority it shared the env stream's queue: r05d trace)
     int lo_prio = 0, hi_prio = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    // (a low or the default priority measured the same per env-step: gpurun_out/r05o)
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->xs, hipStreamNonBlocking, hi_prio);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
     for (uint32_t k = 0; e == hipSuccess && k < depth; ++k)
@@ -646,20 +662,23 @@ extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb,
     const hipStream_t es = (hipStream_t)env_stream;
     int st = xchg_take_region(x, region, es);
     if (st != CF2_OK) return st;
-    const uint32_t q = region, qn = (uint32_t)(x->next_region % x->depth);
+    const uint32_t q = region;
     const uint32_t words = PackLayout{x->n, x->ol, cap}.words();
+    hipLaunchKernelGGL(pack_prep_kernel, dim3(1), dim3(256), 0, es, xchg_send(x, q), words, nb, x->n, x->ol, cap,
+                       xchg_scratch(x, q, 0), xchg_scratch(x, (uint32_t)(x->next_region % x->depth), 0));
+    const hipError_t pe = hipGetLastError();
+    if (pe != hipSuccess) return hip_fail(pe);
     for (uint32_t s = 0; s < nb; ++s) {
         const uint64_t k = k0 + s;
         uint32_t* pk = xchg_send(x, q) + (size_t)s * words;
         uint32_t* scr = xchg_scratch(x, q, s);
-        uint32_t* scr_next = s + 1 < nb ? xchg_scratch(x, q, s + 1) : xchg_scratch(x, qn, 0);
         const float* act = act_dev[k % nact];
-        st = cf2_step_packed(ctx, act, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr,
-                             scr_next, cap, es);
+        st = cf2_step_packed(ctx, act, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr, cap,
+                             es);
         if (st == CF2_ERR_UNSUPPORTED) {      // a shape without the fused pack: the env-step, then the pack
             st = cf2_step(ctx, act, nullptr, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, nullptr,
                           es);
-            if (st == CF2_OK) st = cf2_obs_pack(x->obs[q], x->done[q], x->n, x->ol, cap, pk, scr, scr_next, es);
+            if (st == CF2_OK) st = cf2_obs_pack(x->obs[q], x->done[q], x->n, x->ol, cap, pk, scr, nullptr, es);
         }
         if (st != CF2_OK) return st;
     }

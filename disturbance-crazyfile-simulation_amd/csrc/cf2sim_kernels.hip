@@ -1864,11 +1864,6 @@ __device__ __forceinline__ void pack_epilogue_block(const PackIO& X, uint32_t n,
     const uint64_t m = __ballot(do_reset);
     uint32_t first = 0u;
     if (lane == 0 && m) first = pack_alloc(L, X.scratch, (uint32_t)__popcll(m));
-    if (blockIdx.x == 0) {
-        if (tid == 0) { pk[0] = 0u; pk[1] = n; pk[2] = OL; pk[3] = X.cap; }
-        if (X.next_scratch)
-            for (uint32_t k = tid; k < PACK_SCRATCH_WORDS; k += B) X.next_scratch[k] = 0u;
-    }
     const uint32_t nvalid = n - base < B ? n - base : B;
     float* dst = reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * OL;
     if (nvalid == B && ((uintptr_t)dst & 15u) == 0) {
@@ -2100,49 +2095,37 @@ enum { SEED_SMALL = 10 };   // per finished env, wave 0 -> waves 1-3: final body
 enum { C2_WORDS = 9 };      // per env, wave 3 -> wave 2: the second reset sensor call's gyro normals
 
 // The delta exchange's pack fused into the small-N env-step (cf2_step_packed; the layout and the
-// side-slot allocation are cf2sim_pack.h's, the standalone form is obs_pack_kernel), in two parts:
-// * pack_env_wave: the env wave, as soon as its rows are in LDS (s_obs) and before the block
-//   barrier, writes the block's bitmap words and the o_k words of its rows that did not reset (one
-//   coalesced dword store per 64 words of the block's o_k run), off the block's tail;
-// * pack_epilogue: wave 2, once the reset rows are final (s_rrow), writes their o_k words, the
-//   block's table word and their side entries.
-// The packed buffer is then ready for the all-gather when the env-step kernel ends: no pack kernel,
-// no re-read of the observation rows.  A block with more resets than its quota asks for spill slots
-// (pack_alloc, a memory-side atomic) as soon as it knows its resets, so the atomic's round trip
-// overlaps the reset tail.
+// side-slot allocation are cf2sim_pack.h's, the standalone form is obs_pack_kernel): wave 2, once the
+// reset rows are final (s_rrow; the other rows are final in s_obs at the block barrier), writes the
+// block's bitmap words and block-table word, each lane its row's o_k (13 or 17 dword stores, the
+// wave's together a contiguous run) and, for a reset row, its side entry.  The packed buffer is then
+// ready for the all-gather when the env-step kernel ends: no pack kernel, no re-read of the
+// observation rows.  A block with more resets than its quota asks for spill slots (pack_alloc, a
+// memory-side atomic) right after the block barrier, so the atomic's round trip overlaps the reset
+// tail.  The header words and the zeroing of the next pack's counter are the caller's (cf2_xchg_run
+// does both for a whole batch in one small launch): as little as a block-0 store of the header in
+// this kernel slowed even the unpacked env-step from 9.5 to 10.6-11.0 us at 32 768 envs, and a
+// word-interleaved o_k run (one coalesced store per 64 words, ~1000 more instructions) did the same
+// (tools/pack_cost_probe.py with ablation builds, gpurun_out/r05r-r05x): the small kernel's env wave
+// is sensitive to code anywhere in the kernel.
 template <uint32_t OL, uint32_t OD>
-__device__ __forceinline__ void pack_env_wave(const PackIO& X, uint32_t n, uint32_t base, uint32_t nvalid,
-                                              uint64_t mask, const float* s_obs, uint32_t lane) {
+__device__ __forceinline__ void pack_epilogue(const PackIO& X, uint32_t n, uint32_t base, uint32_t nvalid,
+                                              uint64_t mask, const float* s_obs, const float* s_rrow, uint32_t lane,
+                                              uint32_t first) {
     const PackLayout L{n, OL, X.cap};
     uint32_t* pk = X.pk;
-    if (blockIdx.x == 0) {
-        if (lane == 0) { pk[0] = 0u; pk[1] = n; pk[2] = OL; pk[3] = X.cap; }
-        if (X.next_scratch)
-            for (uint32_t k = lane; k < PACK_SCRATCH_WORDS; k += 64u) X.next_scratch[k] = 0u;
-    }
-    float* dst = reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)base * OL;
-#pragma unroll
-    for (uint32_t j = 0; j < OL; ++j) {
-        const uint32_t f = lane + 64u * j, r = f / OL;
-        if (f < nvalid * OL && !((mask >> r) & 1ull)) dst[f] = s_obs[r * OD + OL + 4u + (f - r * OL)];
-    }
     uint32_t* bits = pk + L.bits();
     if (lane == 0) bits[base / 32u] = (uint32_t)mask;
     if (lane == 1 && base + 32u < n) bits[base / 32u + 1u] = (uint32_t)(mask >> 32);
-}
-
-template <uint32_t OL, uint32_t OD>
-__device__ __forceinline__ void pack_epilogue(const PackIO& X, uint32_t n, uint32_t base, uint64_t mask,
-                                              const float* s_rrow, uint32_t lane, uint32_t first) {
-    const PackLayout L{n, OL, X.cap};
-    uint32_t* pk = X.pk;
     first = __shfl(first, 0);          // lane 0's pack_alloc, issued right after the block barrier
     if (lane == 0) pk[L.btab() + base / XB_PACK] = first;
-    if (!((mask >> lane) & 1ull)) return;
-    const float* row = s_rrow + lane * OD;
+    if (lane >= nvalid) return;
+    const bool rs = (mask >> lane) & 1ull;
+    const float* row = (rs ? s_rrow : s_obs) + lane * OD;
     float* ok = reinterpret_cast<float*>(pk + L.o_slab()) + (size_t)(base + lane) * OL;
 #pragma unroll
-    for (uint32_t k = 0; k < OL; ++k) ok[k] = row[OL + 4u + k];      // the reset row's o_k
+    for (uint32_t k = 0; k < OL; ++k) ok[k] = row[OL + 4u + k];
+    if (!rs) return;
     const uint32_t slot = pack_entry_slot(L, base / XB_PACK, (uint32_t)__popcll(mask & ((1ull << lane) - 1ull)), first);
     if (slot == PACK_DROPPED) return;
     uint32_t* e = pk + L.side() + slot * L.entry();
@@ -2235,7 +2218,6 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
             do_reset = step_env<NOISE, DR, PHYS, true, HD>(P, io, i, s_obs + lane * OD, rs, s_hjgrid, s_draw + lane);
         const uint64_t m = __ballot(do_reset);
         if (lane == 0) { s_mask[0] = (uint32_t)m; s_mask[1] = (uint32_t)(m >> 32); }
-        if (X.pk) pack_env_wave<OL, OD>(X, P.N, base, P.N - base < 64u ? P.N - base : 64u, m, s_obs, lane);
         if (do_reset) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { s_seed[k * 64 + lane] = rs.wb[k]; s_seed[(3 + k) * 64 + lane] = rs.bias[k]; }
@@ -2387,7 +2369,7 @@ __device__ __forceinline__ uint64_t small_body(const KParams& P0, const StepIO& 
     if (wave == 0) write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, false);
     else if (wave == 2) {
         write_obs_rows_part<OD>(io.obs + (size_t)base * OD, s_obs, s_rrow, mask, nvalid, lane, true);
-        if (X.pk) pack_epilogue<OL, OD>(X, P.N, base, mask, s_rrow, lane, pk_first);
+        if (X.pk) pack_epilogue<OL, OD>(X, P.N, base, nvalid, mask, s_obs, s_rrow, lane, pk_first);
     }
     TSTAMP(12);  // rows written
 #ifdef CF2_TIMING

@@ -19,7 +19,8 @@
 // one address: 19.5 us for a 32 768-env pack, round 4); eight per-XCD counters (round 5) still cost
 // the fused step ~2 us at 32 768 envs.
 // The counter lives in a per-buffer scratch area that is never sent (PACK_SCRATCH_WORDS after the
-// largest packed buffer); a pack zeroes the scratch of the buffer the next pack on its stream uses.
+// largest packed buffer).  The standalone pack zeroes the scratch of the buffer the next pack on its
+// stream uses; the env-step's fused pack leaves that (and the header words) to its caller.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -50,8 +51,7 @@ struct PackLayout {
 // packed buffer of its envs besides their observation rows
 struct PackIO {
     uint32_t* pk;              // packed buffer (null: no pack)
-    uint32_t* scratch;         // this buffer's side-slot counters (zeroed by the previous pack)
-    uint32_t* next_scratch;    // the counters of the buffer the next pack uses (zeroed here), or null
+    uint32_t* scratch;         // this buffer's spill counter (zeroed before the env-step)
     uint32_t cap;
 };
 

@@ -362,20 +362,21 @@ int  cf2_gae(uint32_t T, uint32_t n, const float* rew_dev, const float* val_dev,
  * csrc/cf2sim_pack.h); a block whose resets find no room in the side slab (an overflow) is marked
  * dropped: exactly its reset rows have NaN in their o_0 / A parts, *overflow_dev counts the dropped
  * blocks, every other row and all o_k parts stay exact, and later steps are exact again.  A pack
- * counts side slots in scratch_dev (PACK_SCRATCH_WORDS = 288 words, zeroed before the pack) and
- * zeroes next_scratch_dev (the counters of the next pack on its stream; or NULL). */
+ * counts spill slots in scratch_dev (PACK_SCRATCH_WORDS = 32 words, zeroed before the pack) and
+ * zeroes next_scratch_dev (the counter of the next pack on its stream; or NULL). */
 size_t cf2_obs_packed_words(uint32_t n, uint32_t obs_len, uint32_t cap);
 int  cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, uint32_t obs_len, uint32_t cap,
                   uint32_t* packed_dev, uint32_t* scratch_dev, uint32_t* next_scratch_dev, void* stream);
 /* The env-step (cf2_step's outputs, no final_obs) with the pack of its observations fused in: the
  * env kernel writes packed_dev (cf2_obs_packed_words(N, OL, cap) words) as cf2_obs_pack would, from
  * the rows it has in LDS, so no pack launch re-reads them (step_kernel_small's wave 2 at N <= 32 768,
- * every thread of step_kernel's blocks above).  scratch_dev: this buffer's side-slot counters
- * (PACK_SCRATCH_WORDS = 288 words), zeroed by the previous pack; next_scratch_dev: the counters the
- * next pack uses, zeroed here (or NULL). */
+ * every thread of step_kernel's blocks above), except the 4 header words, which it leaves as they
+ * are.  scratch_dev: this buffer's spill counter (PACK_SCRATCH_WORDS = 32 words), zeroed by the
+ * caller before the call (cf2_xchg_run writes a batch's headers and zeroes its counters in one
+ * launch). */
 int  cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
                      uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* packed_dev, uint32_t* scratch_dev,
-                     uint32_t* next_scratch_dev, uint32_t cap, void* stream);
+                     uint32_t cap, void* stream);
 int  cf2_obs_consume(const uint32_t* packed_all_dev, uint32_t world, uint32_t n, uint32_t obs_len, uint32_t cap,
                      uint16_t* age_dev, uint32_t* overflow_dev, uint32_t watch_age, uint32_t* pred_dev,
                      uint32_t* pred_next_dev, void* stream);

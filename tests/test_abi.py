@@ -126,7 +126,7 @@ def test_obs_exchange_error_paths(lib):
     assert lib.cf2_obs_packed_words(0, 13, 0) == 0 and lib.cf2_obs_packed_words(8, 12, 1) == 0
     assert lib.cf2_obs_packed_words(8, 13, 9) == 0                      # cap > n
     assert lib.cf2_obs_pack(None, None, 8, 13, 1, None, None, None, None) == -1
-    assert lib.cf2_step_packed(*([None] * 11), 1, None) == -1
+    assert lib.cf2_step_packed(*([None] * 10), 1, None) == -1
     w = lib.cf2_obs_packed_words(32768, 13, 32768)
     assert lib.cf2_xchg_send_words(32768, 13, 2, 16) == 2 * 16 * (w + 32)
     assert lib.cf2_xchg_recv_words(32768, 13, 8, 2, 16) == 2 * 8 * 16 * w

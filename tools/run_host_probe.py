@@ -81,7 +81,7 @@ def main():
     scr = torch.zeros(2, PACK_SCRATCH_WORDS, dtype=torch.int32, device=dev)
     res["step_packed_ctypes"] = host(lambda: lib.cf2_step_packed(
         env._ctx, ptrs[0], env.obs.data_ptr(), rew, env.done.data_ptr(), trunc, cost, level, pk.data_ptr(),
-        scr[0].data_ptr(), scr[1].data_ptr(), 64, sp), K)
+        scr[0].data_ptr(), 64, sp), K)
 
     pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=int(env.cfg.max_episode_steps))
     pipe.start(env.obs)

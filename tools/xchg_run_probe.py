@@ -23,6 +23,10 @@ def main():
     ap.add_argument("--unit", type=int, default=16)
     ap.add_argument("--env-id", default="DroneHoverBulletFreeEnvWithGust-v0")
     ap.add_argument("--own-stream", action="store_true", help="run on a pool stream, not the null stream")
+    ap.add_argument("--depth", type=int, default=2)
+    ap.add_argument("--lookahead", type=int, default=None)
+    ap.add_argument("--no-watch", action="store_true", help="no time-out look-ahead (no count copies)")
+    ap.add_argument("--skip-eager", action="store_true")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -40,7 +44,8 @@ def main():
     g.manual_seed(1)
     ring = torch.rand(8, n, 4, device=dev, generator=g) * 2 - 1
     ptrs = [ring[r].data_ptr() for r in range(8)]
-    res = {"envs": n, "steps": args.steps, "unit": args.unit}
+    res = {"envs": n, "steps": args.steps, "unit": args.unit, "depth": args.depth, "lookahead": args.lookahead,
+           "watch": not args.no_watch}
 
     def timed(fn, steps):
         torch.cuda.synchronize()
@@ -58,8 +63,8 @@ def main():
     plain(args.warmup)
     res["env_step_us"], _ = timed(plain, args.steps)
 
-    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=int(env.cfg.max_episode_steps),
-                              unit=args.unit)
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, depth=args.depth, lookahead=args.lookahead,
+                              max_steps=0 if args.no_watch else int(env.cfg.max_episode_steps), unit=args.unit)
     pipe.start(env.obs)
     res["exchange"] = pipe.exchange
 
@@ -67,8 +72,9 @@ def main():
         for _ in range(steps):
             pipe.step_and_publish(env, ptrs[pipe.k % 8])
         pipe.drain()
-    eager(args.warmup)
-    res["eager_us"], _ = timed(eager, args.steps)
+    if not args.skip_eager:
+        eager(args.warmup)
+        res["eager_us"], _ = timed(eager, args.steps)
 
     def batched(steps):
         pipe.run(env, ptrs, steps)
