@@ -201,7 +201,7 @@ def pack_quota(n: int, cap: int) -> int:
     return min(int(cap) // ((int(n) + PACK_BLOCK - 1) // PACK_BLOCK), PACK_BLOCK)
 
 
-def _slots(pk, n: int, ol: int, rs):
+def _slots(pk, n: int, ol: int, cap: int, rs):
     """Side slot of every env (valid where rs; PACK_DROPPED where it got none) from its rank among its
     block's resets, the block's quota and the block table (cf2sim_pack.h pack_slot)."""
     import torch
@@ -214,7 +214,7 @@ def _slots(pk, n: int, ol: int, rs):
     start[1:] = c[torch.arange(1, nblk) * PACK_BLOCK - 1]
     within = c - rs.to(torch.int64) - start[blk]
     first = btab[blk]
-    q = pack_quota(n, int(pk[3]))
+    q = pack_quota(n, cap)
     spill = torch.where(first == PACK_DROPPED, torch.full_like(first, PACK_DROPPED), first + within - q)
     return torch.where(within < q, blk * q + within, spill)
 
@@ -314,7 +314,7 @@ def obs_rows(recv, cap: int, recv_prev, cap_prev: int, world: int, n: int, ol: i
         o[:, ol:ol + 4] = torch.where((a >= 3)[:, None], act_prev2[sl], act[sl])
         o[:, ol + 4:2 * ol + 4] = f[4:4 + n * ol].view(n, ol)
         o[:, 2 * ol + 4:] = torch.where((a == 1)[:, None], act[sl], act_prev[sl])
-        sl_ = _slots(pk, n, ol, rs)
+        sl_ = _slots(pk, n, ol, cap, rs)
         drop = rs & (sl_ == PACK_DROPPED)
         o[drop, :ol + 4] = nan
         o[drop, 2 * ol + 4:] = nan

@@ -145,6 +145,8 @@ struct ConsumeSteps {
     uint32_t words[CONSUME_MAX];           // their per-rank stride
     uint32_t* pred[CONSUME_MAX];           // [world] look-ahead counts of each step, or null
     uint32_t* zero[CONSUME_MAX];           // [world] rows to zero, or null
+    uint32_t* scratch;                     // the batch's spill counters to zero (its packs are done), or null
+    uint32_t scratch_words;
     uint32_t steps;
 };
 // (the step loops are unrolled: a dynamically indexed by-value kernel argument would be copied to
@@ -159,6 +161,8 @@ __global__ void __launch_bounds__(256) obs_consume_kernel(ConsumeSteps S, uint32
         for (uint32_t z = 0; z < CONSUME_MAX; ++z)
             if (S.zero[z]) S.zero[z][tid] = 0u;
     }
+    if (blockIdx.x == 0 && S.scratch)
+        for (uint32_t k = tid; k < S.scratch_words; k += 256u) S.scratch[k] = 0u;
     const bool live = i < total;
     const uint32_t ic = live ? i : total - 1u;
     const uint32_t r = ic / L.n, li = ic - r * L.n;
@@ -307,21 +311,6 @@ extern "C" int cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint
 __global__ void __launch_bounds__(256) words_to_host_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
                                                              uint32_t n) {
     for (uint32_t i = threadIdx.x; i < n; i += 256u) dst[i] = src[i];
-}
-
-// A batch's packed buffers before its env-steps (cf2_xchg_run): each buffer's header words and
-// zeroed spill counters (the fused pack leaves both to its caller, cf2sim_kernels.hip), and the
-// counter of the next region's first buffer, which a per-step publish after the batch counts in
-__global__ void __launch_bounds__(256) pack_prep_kernel(uint32_t* __restrict__ send, uint32_t words, uint32_t nb,
-                                                         uint32_t n, uint32_t ol, uint32_t cap,
-                                                         uint32_t* __restrict__ scratch, uint32_t* __restrict__ next0) {
-    const uint32_t t = threadIdx.x;
-    for (uint32_t k = t; k < nb * PACK_SCRATCH_WORDS; k += 256u) scratch[k] = 0u;
-    if (t < PACK_SCRATCH_WORDS) next0[t] = 0u;
-    if (t < nb) {
-        uint32_t* h = send + (size_t)t * words;
-        h[0] = 0u; h[1] = n; h[2] = ol; h[3] = cap;
-    }
 }
 
 static int words_to_host(const uint32_t* src_dev, uint32_t* dst_host, uint32_t n, hipStream_t st) {
@@ -574,6 +563,10 @@ static int xchg_consume(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint3
             S.words[s] = nb * words;                    // rank stride of the batch's [world][nb][words] layout
             if (x->pred) S.pred[s] = x->pred + (size_t)((k0 + s0 + s) % x->npred) * x->world;
         }
+        if (s0 == 0) {          // the batch's packs are done: zero its spill counters for the region's next use
+            S.scratch = xchg_scratch(x, q, 0);
+            S.scratch_words = nb * PACK_SCRATCH_WORDS;
+        }
         const uint64_t k1 = k0 + s0 + S.steps - 1;
         if (x->pred)
             for (uint32_t z = 0; z < CONSUME_MAX; ++z) S.zero[z] = x->pred + (size_t)((k1 + 1 + z) % x->npred) * x->world;
@@ -593,10 +586,10 @@ static int xchg_exchange(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint
     const size_t words = PackLayout{x->n, x->ol, cap}.words();
     if (g_rccl.all_gather(xchg_send(x, q), xchg_recv(x, q), nb * words, ncclUint32, x->comm, x->xs) != ncclSuccess)
         return CF2_ERR_HIP;
-    e = hipEventRecord(x->free_[q], x->xs);
-    if (e != hipSuccess) return hip_fail(e);
     int st = xchg_consume(x, k0, nb, q, cap);
     if (st != CF2_OK) return st;
+    e = hipEventRecord(x->free_[q], x->xs);     // the region's buffers are read and its counters zeroed
+    if (e != hipSuccess) return hip_fail(e);
     if (pred_host && x->pred) {
         st = words_to_host(x->pred, pred_host, x->npred * x->world, x->xs);
         if (st != CF2_OK) return st;
@@ -622,7 +615,7 @@ extern "C" int cf2_xchg_publish(cf2_xchg* x, uint64_t k, uint32_t cap, uint32_t 
     ++x->next_region;
     // the caller's env-step wrote obs / done of the region (after cf2_xchg_wait_free): pack it here
     int st = cf2_obs_pack(x->obs[region], x->done[region], x->n, x->ol, cap, xchg_send(x, region),
-                          xchg_scratch(x, region, 0), xchg_scratch(x, (uint32_t)(x->next_region % x->depth), 0), es);
+                          xchg_scratch(x, region, 0), nullptr, es);
     if (st != CF2_OK) return st;
     return xchg_exchange(x, k, 1, region, cap, es, nullptr);
 }
@@ -664,10 +657,6 @@ extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb,
     if (st != CF2_OK) return st;
     const uint32_t q = region;
     const uint32_t words = PackLayout{x->n, x->ol, cap}.words();
-    hipLaunchKernelGGL(pack_prep_kernel, dim3(1), dim3(256), 0, es, xchg_send(x, q), words, nb, x->n, x->ol, cap,
-                       xchg_scratch(x, q, 0), xchg_scratch(x, (uint32_t)(x->next_region % x->depth), 0));
-    const hipError_t pe = hipGetLastError();
-    if (pe != hipSuccess) return hip_fail(pe);
     for (uint32_t s = 0; s < nb; ++s) {
         const uint64_t k = k0 + s;
         uint32_t* pk = xchg_send(x, q) + (size_t)s * words;

@@ -2102,9 +2102,10 @@ enum { C2_WORDS = 9 };      // per env, wave 3 -> wave 2: the second reset senso
 // ready for the all-gather when the env-step kernel ends: no pack kernel, no re-read of the
 // observation rows.  A block with more resets than its quota asks for spill slots (pack_alloc, a
 // memory-side atomic) right after the block barrier, so the atomic's round trip overlaps the reset
-// tail.  The header words and the zeroing of the next pack's counter are the caller's (cf2_xchg_run
-// does both for a whole batch in one small launch): as little as a block-0 store of the header in
-// this kernel slowed even the unpacked env-step from 9.5 to 10.6-11.0 us at 32 768 envs, and a
+// tail.  The informational header words are not written and the zeroing of the counter is the
+// caller's (cf2_xchg_* zeroes a batch's counters in its consume): as little as a block-0 store of
+// the header in this kernel slowed even the unpacked env-step from 9.5 to 10.6-11.0 us at 32 768
+// envs, and a
 // word-interleaved o_k run (one coalesced store per 64 words, ~1000 more instructions) did the same
 // (tools/pack_cost_probe.py with ablation builds, gpurun_out/r05r-r05x): the small kernel's env wave
 // is sensitive to code anywhere in the kernel.

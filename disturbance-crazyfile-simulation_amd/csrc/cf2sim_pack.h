@@ -3,7 +3,8 @@
 // epilogue (cf2sim_kernels.hip, step_kernel_small).
 //
 // One rank's packed buffer (32-bit words, 16-B multiple):
-//   [0] 0 (reserved)   [1] n   [2] OL   [3] cap
+//   [0] 0 (reserved)   [1] n   [2] OL   [3] cap     (informational: no receiver reads them; the
+//                                                    env-step's fused pack does not write them)
 //   [4, 4 + n OL)                       o_k rows
 //   [.., + ceil(n / 32))                reset bitmap, env i = bit i % 32 of word i / 32
 //   [.., + ceil(n / 64))                block table: per 64-env pack block, the first spill slot of its
@@ -20,7 +21,7 @@
 // the fused step ~2 us at 32 768 envs.
 // The counter lives in a per-buffer scratch area that is never sent (PACK_SCRATCH_WORDS after the
 // largest packed buffer).  The standalone pack zeroes the scratch of the buffer the next pack on its
-// stream uses; the env-step's fused pack leaves that (and the header words) to its caller.
+// stream uses; cf2_xchg_* zeroes a batch's counters in its consume, once the batch's packs are done.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -370,10 +370,10 @@ int  cf2_obs_pack(const float* obs_dev, const uint8_t* reset_dev, uint32_t n, ui
 /* The env-step (cf2_step's outputs, no final_obs) with the pack of its observations fused in: the
  * env kernel writes packed_dev (cf2_obs_packed_words(N, OL, cap) words) as cf2_obs_pack would, from
  * the rows it has in LDS, so no pack launch re-reads them (step_kernel_small's wave 2 at N <= 32 768,
- * every thread of step_kernel's blocks above), except the 4 header words, which it leaves as they
- * are.  scratch_dev: this buffer's spill counter (PACK_SCRATCH_WORDS = 32 words), zeroed by the
- * caller before the call (cf2_xchg_run writes a batch's headers and zeroes its counters in one
- * launch). */
+ * every thread of step_kernel's blocks above), except the 4 informational header words, which it
+ * leaves as they are (no receiver reads them).  scratch_dev: this buffer's spill counter
+ * (PACK_SCRATCH_WORDS = 32 words), zeroed by the caller before the call (cf2_xchg_* zeroes a
+ * batch's counters in the batch's consume, after its packs). */
 int  cf2_step_packed(cf2_ctx* ctx, const float* act_dev, float* obs_dev, float* rew_dev, uint8_t* done_dev,
                      uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* packed_dev, uint32_t* scratch_dev,
                      uint32_t cap, void* stream);
