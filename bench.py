@@ -758,15 +758,53 @@ def main(argv=None):
         rows_us = ev[2].elapsed_time(ev[3]) * 1e3 / reps
         full_b, delta_b = n8 * env.obs_dim * 4, words * 4
         rows_b = n * (4 * env.obs_dim + 4 * ol + 12 * 4 + 2) + W8 * delta_b
+        # the exchange path packs inside the env-step (cf2_step_packed): one node-shard context, its
+        # env-step with and without the fused pack, alternating blocks of launches
+        shard = BatchedCrazyflieEnv(args.env_id, n8, seed=args.seed + 1, device=dev, **env_kw)
+        shard.reset()
+        srew, strunc, scost, slevel = shard._raw_step_outputs()
+        spk = torch.zeros(words, dtype=torch.int32, device=dev)
+        sscr = torch.zeros(PACK_SCRATCH_WORDS, dtype=torch.int32, device=dev)
+        sact = [a[:n8].contiguous() for a in acts]
+        sp = stream.cuda_stream
+        lib = shard.lib
+
+        def shard_steps(packed: bool, k: int):
+            for j in range(k):
+                a = sact[j % len(sact)].data_ptr()
+                if packed:
+                    st = lib.cf2_step_packed(shard._ctx, a, shard.obs.data_ptr(), srew, shard.done.data_ptr(), strunc,
+                                             scost, slevel, spk.data_ptr(), sscr.data_ptr(), cap, sp)
+                else:
+                    st = lib.cf2_step(shard._ctx, a, None, shard.obs.data_ptr(), srew, shard.done.data_ptr(), strunc,
+                                      scost, slevel, None, sp)
+                if st != 0:
+                    raise RuntimeError(f"node-shard probe: status {st}")
+        shard_steps(False, 200)
+        best = {False: float("inf"), True: float("inf")}
+        for _ in range(4):
+            for packed in (False, True):
+                sscr.zero_()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                shard_steps(packed, 200)
+                e1.record(stream)
+                e1.synchronize()
+                best[packed] = min(best[packed], e0.elapsed_time(e1) * 1e3 / 200)
+        shard.check_device_errors()
+        shard.close()
         exchange = {"shape": f"8 ranks x {n8} envs", "cap_per_rank": cap, "bytes_per_rank_per_step": delta_b,
                     "full_rows_bytes_per_rank_per_step": full_b, "reduction": full_b / delta_b,
                     "link_bound_us_8gpu": delta_b / 153e9 * 1e6, "link_bound_us_8gpu_full_rows": full_b / 153e9 * 1e6,
-                    "pack_us_per_rank": pack_us, "consume_us_all_envs": consume_us,
+                    "node_shard_step_us": best[False], "node_shard_step_packed_us": best[True],
+                    "standalone_pack_us_per_rank": pack_us, "consume_us_all_envs": consume_us,
                     "consume_algorithmic_bytes": n * 4 + W8 * ((n8 + 31) // 32) * 4,
                     "rows_on_request_us_all_rows": rows_us, "rows_algorithmic_bytes": rows_b,
                     "rows_GBs": rows_b / (rows_us * 1e-6) / 1e9,
                     "note": "link bound: each GPU receives one packed buffer from each of 7 peers over its 7 xGMI links "
-                            "(~153 GB/s each) in parallel; per step a receiver only advances the envs' ages (consume); "
+                            "(~153 GB/s each) in parallel; the exchange path packs inside the env-step "
+                            "(node_shard_step_packed_us vs node_shard_step_us; the standalone pack kernel is the "
+                            "per-step publish's); per step a receiver only advances the envs' ages (consume); "
                             "rows are materialised on request"}
         del send, prev_pk, rows, out_rows
 
