@@ -145,6 +145,9 @@ def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
                       f"(2048 envs x 600 env-steps, {dt1:.1f} s)"}
 
 
+GATHER_TIMEOUT_S = 180      # the gather key's watchdog (bench.py measures it last at N > 1)
+
+
 def step_kernel_key() -> str:
     """Content key of the step kernel's build (kernel source, headers, flags: cf2sim.build), so a
     traffic measurement stays valid across rebuilds that do not touch the step kernel."""
@@ -537,10 +540,6 @@ def main(argv=None):
     elapsed, ev_ms = run(args.steps, graph)
     kern_ms = ev_ms / args.steps
 
-    gather_info = None
-    if gather:
-        gather_info = exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks)
-
     strong = None
     if world > 1 and scaling == "weak" and args.strong_steps > 0:
         # the same 262 144 envs split over the ranks (32 768 per GPU at N = 8), no collective
@@ -868,6 +867,7 @@ def main(argv=None):
     achieved_gbs = bytes_per * n / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(f"{args.env_id}:N={n}")
     wset = working_set_bytes(env, ring)
+    line = None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -906,7 +906,7 @@ def main(argv=None):
                          "cache_resident": wset < INFINITY_CACHE_BYTES,
                          "out_of_cache": out_of_cache},
             "cpu_baseline": cpu,
-            "gather": gather_info,
+            "gather": None,
             "strong_scaling": strong,
             "fused_rollout": fused,
             "collect": collect_line,
@@ -914,6 +914,27 @@ def main(argv=None):
             "two_streams": two_streams,
             "delta_exchange": exchange,
         }
+    if gather:
+        # measured last, under a watchdog: the line above is complete without it, and a rank that
+        # fails or stalls inside the exchange's collectives must not cost the line
+        import threading
+
+        def stalled():
+            if line is not None:
+                line["gather"] = {"error": f"no result after {GATHER_TIMEOUT_S} s"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+        dog = threading.Timer(GATHER_TIMEOUT_S, stalled)
+        dog.daemon = True
+        dog.start()
+        try:
+            gather_info = exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks)
+        except Exception as e:          # every rank reports; a stall on the others ends at the watchdog
+            gather_info = {"error": repr(e)[:300]}
+        dog.cancel()
+        if line is not None:
+            line["gather"] = gather_info
+    if line is not None:
         print(json.dumps(line), flush=True)
     env.check_device_errors()
     env.close()
