@@ -28,7 +28,7 @@ class _Timed:
 
     def __getattr__(self, name):
         f = getattr(self._lib, name)
-        if name != "cf2_xchg_run":
+        if name not in ("cf2_xchg_run", "cf2_xchg_env_step"):
             return f
 
         def timed(*a):
@@ -101,6 +101,24 @@ def main():
     res["run_python_per_step"] = (t_run - proxy.t) * 1e6 / K
     res["run_wall_per_step"] = t_wall * 1e6 / K
     pipe._lib = proxy._lib
+    # the eager path: one step_and_publish per env-step (a policy in the loop)
+    pipe.run(env, ptrs, (-pipe.k) % pipe.unit)
+    for _ in range(100):
+        pipe.step_and_publish(env, ptrs[pipe.k % 8])
+    pipe.drain()
+    torch.cuda.synchronize()
+    proxy2 = _Timed(pipe._lib)
+    pipe._lib = proxy2
+    t0 = time.perf_counter()
+    for _ in range(K // 4):
+        pipe.step_and_publish(env, ptrs[pipe.k % 8])
+    t_e = time.perf_counter() - t0
+    pipe.drain()
+    torch.cuda.synchronize()
+    res["eager_call_per_step"] = proxy2.t * 1e6 / (K // 4)
+    res["eager_python_per_step"] = (t_e - proxy2.t) * 1e6 / (K // 4)
+    res["eager_wall_per_step"] = (time.perf_counter() - t0) * 1e6 / (K // 4)
+    pipe._lib = proxy2._lib
     import cProfile
     import io
     import pstats
