@@ -413,6 +413,7 @@ class PipelinedObsGather:
                              "buffers of that step and the one before)")
         self.group = group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         self.nccl = dist.get_backend(group) == "nccl"
         sizes = exchange_sizes(n, group)
         if len(set(sizes)) != 1:
@@ -462,6 +463,7 @@ class PipelinedObsGather:
         self._where = {}                     # step -> (region, slot in its batch, batch size, capacity)
         self._region = 0                     # publishes / batches so far (their region: % depth)
         self._start_rows = None
+        self._batch = None                   # step(): [k0, nb, cap, region, steps issued] of the open batch
         if self.comm is not None:
             from . import _native
             self._lib = _native.load()
@@ -720,6 +722,7 @@ class PipelinedObsGather:
             return out
         if not self.started:
             raise RuntimeError("delta exchange: call start(reset observations) first")
+        self.flush()
         k, q = self.k, self._q()
         cap = self.step_cap(k)
         words = packed_words(self.n, self.ol, cap)
@@ -767,6 +770,7 @@ class PipelinedObsGather:
             raise RuntimeError("delta exchange: call start(reset observations) first")
         if env.num_envs != self.n or env.obs_dim != self.od:
             raise ValueError("step_and_publish: the env's shard does not match the exchange's layout")
+        self.flush()
         k, q = self.k, self._q()
         cap = self.step_cap(k)
         rew, trunc, cost, level = env._raw_step_outputs()
@@ -797,6 +801,7 @@ class PipelinedObsGather:
         nact = len(act_ptrs)
         if nact < 1:
             raise ValueError("run: at least one action buffer")
+        self.flush()
         arr = (ctypes.c_void_p * nact)(*act_ptrs)
         rew, trunc, cost, level = env._raw_step_outputs()
         # the batches run on a stream of the exchange's own, ordered after the caller's stream and
@@ -830,6 +835,76 @@ class PipelinedObsGather:
         cur.wait_stream(s)
         return self.k - 1
 
+    def step(self, env, act_ptr: int) -> int:
+        """Native exchange, a policy in the loop: env-step k of `env` (this rank's shard; act_ptr its
+        [n, 4] actions, e.g. the policy's output on local_obs() of the step before) with its pack
+        fused in, on the current stream.  The exchange runs per batch of `unit` steps aligned to
+        multiples of it (cf2_xchg_begin / cf2_xchg_step / cf2_xchg_end: the same launches as run(),
+        with the actions given one step at a time), so the gathered rows of a step are available
+        once its batch is exchanged: at the batch's end or at flush().  Collective: every rank calls
+        it for every env-step.  Returns k.  For the best overlap call it from a non-default stream
+        (on the null stream a batch's first env-step waits for the previous batch's exchange)."""
+        import torch
+        from . import _native
+        if self._xchg is None:
+            raise RuntimeError("step needs the native exchange (RCCL, delta=True)")
+        if not self.started:
+            raise RuntimeError("delta exchange: call start(reset observations) first")
+        if env.num_envs != self.n or env.obs_dim != self.od:
+            raise ValueError("step: the env's shard does not match the exchange's layout")
+        sp = torch.cuda.current_stream(self.device).cuda_stream
+        if self._batch is None:
+            k0, q = self.k, self._q()
+            nb = self.unit - k0 % self.unit
+            cap = max(self.step_cap(k) for k in range(k0, k0 + nb))
+            _native.check(self._lib.cf2_xchg_begin(self._xchg, cap, q, sp), "cf2_xchg_begin")
+            self._batch = [k0, nb, cap, q, 0]
+        b = self._batch
+        rew, trunc, cost, level = env._raw_step_outputs()
+        _native.check(self._lib.cf2_xchg_step(self._xchg, env._ctx, act_ptr, rew, trunc, cost, level, sp),
+                      "cf2_xchg_step")
+        b[4] += 1
+        k = b[0] + b[4] - 1
+        if b[4] == b[1]:
+            self.flush()
+        return k
+
+    def flush(self):
+        """Exchange the env-steps step() has issued since the last exchange (collective: every rank
+        calls it at the same step).  A no-op when there are none."""
+        import torch
+        b = self._batch
+        if b is None:
+            return
+        from . import _native
+        self._batch = None
+        k0, nb, cap, q, s = b
+        w = self.watch != NO_WATCH
+        buf = self._next_pool() if w else None
+        _native.check(self._lib.cf2_xchg_end(self._xchg, k0, buf.data_ptr() if w else None,
+                                             torch.cuda.current_stream(self.device).cuda_stream), "cf2_xchg_end")
+        if w:
+            ev = torch.cuda.Event()
+            self._lib.cf2_xchg_wait(self._xchg, self._side_stream().cuda_stream)
+            ev.record(self._side_stream())
+            self._copies.append((k0 + s - 1, buf, ev))
+        self._after(k0, s, cap, q, copied=True)
+
+    def local_obs(self):
+        """This rank's observation rows [n, D] of the latest env-step (step(), run(), step_and_publish
+        or the caller's env-step into buffer()), before or after their exchange: what a policy in the
+        loop acts on.  The done flags of that step: local_done()."""
+        if self._batch is not None:
+            return self.obs[self._batch[3]]
+        if self.k > 0:
+            return self.obs[self._where[self.k - 1][0]]
+        return self._start_rows[self.rank * self.n:(self.rank + 1) * self.n]
+
+    def local_done(self):
+        if self._batch is not None:
+            return self.done[self._batch[3]]
+        return self.done[self._where[self.k - 1][0]] if self.k > 0 else None
+
     def _run_stream(self):
         import torch
         if getattr(self, "_rs", None) is None:
@@ -850,6 +925,8 @@ class PipelinedObsGather:
         the next publish / run.  Before any step: the slab start() gathered."""
         if not self.delta:
             raise RuntimeError("rows() is for the delta exchange")
+        if self._batch is not None:
+            raise RuntimeError("rows(): step() has env-steps not yet exchanged; call flush() on every rank first")
         k = self.k - 1
         N = self.world * self.n
         nrows = N - row0 if nrows is None else int(nrows)

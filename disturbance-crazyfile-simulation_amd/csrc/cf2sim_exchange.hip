@@ -411,6 +411,9 @@ struct cf2_xchg {
     hipEvent_t end;                    // every exchange issued so far is complete
     bool free_rec[XCHG_MAX_DEPTH], end_rec;
     uint64_t next_region;
+    // a batch opened by cf2_xchg_begin and filled by cf2_xchg_step (actions given one env-step at a time)
+    bool open;
+    uint32_t open_region, open_cap, open_steps;
     // registered buffers
     bool registered;
     uint32_t n, ol, watch, npred, kmax;
@@ -609,7 +612,8 @@ static int xchg_take_region(cf2_xchg* x, uint32_t region, hipStream_t es) {
 }
 
 extern "C" int cf2_xchg_publish(cf2_xchg* x, uint64_t k, uint32_t cap, uint32_t region, void* env_stream) {
-    if (!x || !x->registered || !layout_ok(x->n, x->ol, cap) || region >= x->depth) return CF2_ERR_INVALID_ARG;
+    if (!x || !x->registered || x->open || !layout_ok(x->n, x->ol, cap) || region >= x->depth)
+        return CF2_ERR_INVALID_ARG;
     if (region != x->next_region % x->depth) return CF2_ERR_INVALID_ARG;
     const hipStream_t es = (hipStream_t)env_stream;
     ++x->next_region;
@@ -644,34 +648,57 @@ extern "C" int cf2_xchg_pred_to_host(cf2_xchg* x, uint32_t* pred_host, void* str
     return words_to_host(x->pred, pred_host, x->npred * x->world, st);
 }
 
+extern "C" int cf2_xchg_begin(cf2_xchg* x, uint32_t cap, uint32_t region, void* env_stream) {
+    if (!x || !x->registered || x->open || region >= x->depth || !layout_ok(x->n, x->ol, cap))
+        return CF2_ERR_INVALID_ARG;
+    const int st = xchg_take_region(x, region, (hipStream_t)env_stream);
+    if (st != CF2_OK) return st;
+    x->open = true;
+    x->open_region = region; x->open_cap = cap; x->open_steps = 0;
+    return CF2_OK;
+}
+
+extern "C" int cf2_xchg_step(cf2_xchg* x, cf2_ctx* ctx, const float* act_dev, float* rew_dev, uint8_t* trunc_dev,
+                             float* cost_dev, float* level_dev, void* env_stream) {
+    if (!x || !x->open || !ctx || !act_dev || ((uintptr_t)act_dev & 15u) || !rew_dev || x->open_steps >= x->kmax)
+        return CF2_ERR_INVALID_ARG;
+    const hipStream_t es = (hipStream_t)env_stream;
+    const uint32_t q = x->open_region, s = x->open_steps, cap = x->open_cap;
+    uint32_t* pk = xchg_send(x, q) + (size_t)s * PackLayout{x->n, x->ol, cap}.words();
+    uint32_t* scr = xchg_scratch(x, q, s);
+    int st = cf2_step_packed(ctx, act_dev, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr,
+                             cap, es);
+    if (st == CF2_ERR_UNSUPPORTED) {      // a shape without the fused pack: the env-step, then the pack
+        st = cf2_step(ctx, act_dev, nullptr, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, nullptr,
+                      es);
+        if (st == CF2_OK) st = cf2_obs_pack(x->obs[q], x->done[q], x->n, x->ol, cap, pk, scr, nullptr, es);
+    }
+    if (st == CF2_OK) ++x->open_steps;
+    return st;
+}
+
+extern "C" int cf2_xchg_end(cf2_xchg* x, uint64_t k0, uint32_t* pred_host, void* env_stream) {
+    if (!x || !x->open || x->open_steps == 0) return CF2_ERR_INVALID_ARG;
+    x->open = false;
+    return xchg_exchange(x, k0, x->open_steps, x->open_region, x->open_cap, (hipStream_t)env_stream, pred_host);
+}
+
 extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
                             const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev,
                             float* cost_dev, float* level_dev, uint32_t* pred_host, void* env_stream) {
-    if (!x || !x->registered || !ctx || !act_dev || nact == 0 || nb == 0 || nb > x->kmax || region >= x->depth ||
-        !layout_ok(x->n, x->ol, cap) || !rew_dev)
+    if (!x || !x->registered || x->open || !ctx || !act_dev || nact == 0 || nb == 0 || nb > x->kmax ||
+        region >= x->depth || !layout_ok(x->n, x->ol, cap) || !rew_dev)
         return CF2_ERR_INVALID_ARG;
     for (uint32_t a = 0; a < nact; ++a)
         if (!act_dev[a] || ((uintptr_t)act_dev[a] & 15u)) return CF2_ERR_INVALID_ARG;
-    const hipStream_t es = (hipStream_t)env_stream;
-    int st = xchg_take_region(x, region, es);
-    if (st != CF2_OK) return st;
-    const uint32_t q = region;
-    const uint32_t words = PackLayout{x->n, x->ol, cap}.words();
-    for (uint32_t s = 0; s < nb; ++s) {
-        const uint64_t k = k0 + s;
-        uint32_t* pk = xchg_send(x, q) + (size_t)s * words;
-        uint32_t* scr = xchg_scratch(x, q, s);
-        const float* act = act_dev[k % nact];
-        st = cf2_step_packed(ctx, act, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr, cap,
-                             es);
-        if (st == CF2_ERR_UNSUPPORTED) {      // a shape without the fused pack: the env-step, then the pack
-            st = cf2_step(ctx, act, nullptr, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, nullptr,
-                          es);
-            if (st == CF2_OK) st = cf2_obs_pack(x->obs[q], x->done[q], x->n, x->ol, cap, pk, scr, nullptr, es);
-        }
-        if (st != CF2_OK) return st;
+    int st = cf2_xchg_begin(x, cap, region, env_stream);
+    for (uint32_t s = 0; st == CF2_OK && s < nb; ++s)
+        st = cf2_xchg_step(x, ctx, act_dev[(k0 + s) % nact], rew_dev, trunc_dev, cost_dev, level_dev, env_stream);
+    if (st != CF2_OK) {
+        x->open = false;      // the region stays taken; the caller's count moved on with it
+        return st;
     }
-    return xchg_exchange(x, k0, nb, q, cap, es, pred_host);
+    return cf2_xchg_end(x, k0, pred_host, env_stream);
 }
 
 extern "C" int cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, uint32_t region,

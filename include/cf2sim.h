@@ -406,7 +406,11 @@ int  cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride,
  * kmax; actions of step k at act_dev[k % nact]) issued back to back on env_stream with their pack
  * fused in (cf2_step_packed), then the batch's exchange at
  * capacity cap; pred_host (pinned, npred x world words, or NULL) receives the look-ahead ring after
- * the batch's consume.  cf2_xchg_env_step: cf2_xchg_run of one step.  cf2_xchg_wait(x, stream): a
+ * the batch's consume.  cf2_xchg_env_step: cf2_xchg_run of one step.  The same batch with its
+ * actions given one env-step at a time (a policy in the loop, acting on each step's local rows):
+ * cf2_xchg_begin(x, cap, region, env_stream) opens it (takes the region), cf2_xchg_step(x, ctx, act,
+ * rew, trunc, cost, level, env_stream) issues its next env-step (up to kmax), cf2_xchg_end(x, k0,
+ * pred_host, env_stream) issues its exchange; cf2_xchg_run is begin + nb steps + end.  cf2_xchg_wait(x, stream): a
  * stream waits until every exchange issued so far is complete.  cf2_xchg_pred_to_host(x, pred_host,
  * stream): the same wait, then the look-ahead ring to pred_host.  Both ring copies are device stores
  * into the pinned buffer's mapping (a kernel on the stream), which never hold the calling thread;
@@ -430,6 +434,10 @@ int  cf2_xchg_pred_to_host(cf2_xchg* x, uint32_t* pred_host, void* stream);
 int  cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
                   const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
                   float* level_dev, uint32_t* pred_host, void* env_stream);
+int  cf2_xchg_begin(cf2_xchg* x, uint32_t cap, uint32_t region, void* env_stream);
+int  cf2_xchg_step(cf2_xchg* x, cf2_ctx* ctx, const float* act_dev, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
+                   float* level_dev, void* env_stream);
+int  cf2_xchg_end(cf2_xchg* x, uint64_t k0, uint32_t* pred_host, void* env_stream);
 int  cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, uint32_t region, const float* act_dev,
                        float* rew_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, void* env_stream);
 

@@ -140,4 +140,6 @@ def test_obs_exchange_error_paths(lib):
     assert lib.cf2_xchg_create(idb, 128, 1, 0, 9, ctypes.byref(h)) == -1
     assert lib.cf2_xchg_publish(None, 0, 1, 0, None) == -1 and lib.cf2_xchg_wait(None, None) == -1
     assert lib.cf2_xchg_pred_to_host(None, None, None) == -1
+    assert lib.cf2_xchg_begin(None, 1, 0, None) == -1 and lib.cf2_xchg_end(None, 0, None, None) == -1
+    assert lib.cf2_xchg_step(None, None, None, None, None, None, None, None) == -1
     assert lib.cf2_xchg_run(None, None, 0, 8, 1, 0, None, 1, None, None, None, None, None, None) == -1

@@ -205,6 +205,39 @@ def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
             if not torch.equal(rows, full):
                 bad.append(k - 1)
         twin.close()
+    elif exchange == "step":
+        # a policy in the loop: each action is computed from the local rows of the step before
+        # (pipe.local_obs()), the exchange runs per batch; rows checked at irregular flushes
+        twin = BatchedCrazyflieEnv(ENV_ID, n, seed=3, env_id_offset=rank * n, device=dev, max_episode_steps=41)
+        twin.reset()
+        side = torch.cuda.Stream(device=dev)          # steps issued from a pool stream, as step() advises
+        side.wait_stream(torch.cuda.current_stream())
+        taken = []
+        with torch.cuda.stream(side):
+            for k in range(T):
+                loc = pipe.local_obs()
+                if not torch.equal(loc, twin.obs if k > 0 else obs0):
+                    bad.append(("local", k))
+                a = (torch.tanh(3.0 * loc[:, 17:21]) * 0.5 + ring[k % 8][rank * n:(rank + 1) * n] * 0.5).contiguous()
+                taken.append(a)
+                twin.step_raw(a.data_ptr())
+                resets += int(twin.done.sum())
+                assert pipe.step(env, a.data_ptr()) == k
+                if k % 7 == 6 or k == T - 1:
+                    if k % 16 != 15:
+                        try:
+                            pipe.rows(a, a, a)
+                            bad.append(("rows before flush", k))
+                        except RuntimeError:
+                            pass
+                    pipe.flush()
+                    ga = [gather_rows(taken[max(k - d, 0)], sizes=[n] * world) for d in range(3)]
+                    rows = pipe.rows(*ga)
+                    checked += 1
+                    if not torch.equal(rows, gather_rows(twin.obs, sizes=[n] * world)):
+                        bad.append(k)
+        torch.cuda.current_stream().wait_stream(side)
+        twin.close()
     else:
         for k in range(T):
             a = acts[k]
@@ -266,6 +299,16 @@ def test_delta_exchange_one_rccl_rank_batched_run(gpu, tmp_path):
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "run"), nprocs=1, join=True)
     _check(out, "native", min_checked=16)
+
+
+def test_delta_exchange_one_rccl_rank_policy_in_the_loop(gpu, tmp_path):
+    """step(): the batch's env-steps issued one at a time, each action computed on the GPU from the
+    local rows of the step before (local_obs(), equal to an eagerly stepped twin's every step), the
+    exchange per batch of 16 or at irregular flush()es (every 7th step); rows() refuses to run over
+    un-exchanged steps, and after each flush the rows equal the full gather of the twin's."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(1, _port(), out, "nccl", 32768, 240, "step"), nprocs=1, join=True)
+    _check(out, "native", min_checked=30)
 
 
 def test_delta_exchange_one_rccl_rank_batched_run_large_shard(gpu, tmp_path):

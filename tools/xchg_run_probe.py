@@ -88,6 +88,22 @@ def main():
     res["run_host_issue_us"] = (time.perf_counter() - t0) * 1e6 / args.steps
     pipe.drain()
     torch.cuda.synchronize()
+    # a policy in the loop: step() per env-step (actions given one at a time), exchange per batch,
+    # issued from a pool stream
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    cnt = [0]
+
+    def stepped(steps):
+        with torch.cuda.stream(side):
+            for _ in range(steps):
+                pipe.step(env, ptrs[cnt[0] % 8])
+                cnt[0] += 1
+            pipe.flush()
+            pipe.drain()
+        torch.cuda.current_stream().wait_stream(side)
+    stepped((-pipe.k) % args.unit + args.warmup)
+    res["step_us"], _ = timed(stepped, args.steps)
     res["overflows"] = pipe.overflows()
     res["bytes_per_rank_per_step"] = pipe.bytes_per_rank_per_step
     # rows on request: all rows of the last step
