@@ -394,7 +394,7 @@ int  cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride,
  * together; depth 2..8 buffer regions).  cf2_xchg_register: the buffers, once: obs [n, 2 OL + 8] /
  * reset uint8 [n] per region (depth each), send (cf2_xchg_send_words, zeroed) and recv
  * (cf2_xchg_recv_words) for batches of up to kmax env-steps, age [world n], overflow, pred (the
- * look-ahead ring [npred][world], used when watch_age is on; npred >= 17).  Every publish / batch
+ * look-ahead ring [npred][world], used when watch_age is on; npred >= 33).  Every publish / batch
  * takes the next region (0, 1, ..., depth - 1, 0, ...; `region` must name it: the caller keeps the
  * count) and first makes env_stream wait for the all-gather that last read that region.  A batch of
  * nb steps at capacity cap leaves recv region q as [world][nb][cf2_obs_packed_words(n, OL, cap)]:
