@@ -311,6 +311,55 @@ def test_delta_exchange_one_rccl_rank_policy_in_the_loop(gpu, tmp_path):
     _check(out, "native", min_checked=30)
 
 
+def _batch_misuse(rank, world, port, out):
+    sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
+    os.environ["CF2SIM_EXCHANGE"] = "native"
+    import torch.distributed as dist
+    from cf2sim.dist import PipelinedObsGather
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    n = 4096
+    env = BatchedCrazyflieEnv(ENV_ID, n, seed=3, device=dev)
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=500)
+    pipe.start(env.reset().clone())
+    lib, x = pipe._lib, pipe._xchg
+    sp = torch.cuda.current_stream().cuda_stream
+    a = torch.zeros(n, 4, device=dev)
+    rew, trunc, cost, level = env._raw_step_outputs()
+    res = []
+    res.append(lib.cf2_xchg_step(x, env._ctx, a.data_ptr(), rew, trunc, cost, level, sp))   # no open batch
+    res.append(lib.cf2_xchg_end(x, 0, None, sp))                                            # no open batch
+    res.append(lib.cf2_xchg_begin(x, 64, 1, sp))                                            # not the next region
+    res.append(lib.cf2_xchg_begin(x, 64, 0, sp))                                            # ok
+    res.append(lib.cf2_xchg_begin(x, 64, 1, sp))                                            # already open
+    res.append(lib.cf2_xchg_end(x, 0, None, sp))                                            # open, but no step yet
+    res.append(lib.cf2_xchg_publish(x, 0, 64, 1, sp))                                       # a batch is open
+    res.append(lib.cf2_xchg_step(x, env._ctx, a.data_ptr() + 4, rew, trunc, cost, level, sp))   # misaligned actions
+    res.append(lib.cf2_xchg_step(x, env._ctx, a.data_ptr(), rew, trunc, cost, level, sp))   # ok
+    res.append(lib.cf2_xchg_end(x, 0, None, sp))                                            # ok: exchanges step 0
+    torch.cuda.synchronize()
+    pipe._lib = None
+    pipe._xchg = None
+    lib.cf2_xchg_destroy(x)
+    with open(out, "w") as f:
+        f.write(" ".join(str(r) for r in res))
+    dist.destroy_process_group()
+
+
+def test_batch_calls_reject_misuse(gpu, tmp_path):
+    """cf2_xchg_begin / cf2_xchg_step / cf2_xchg_end: a step or an end without an open batch, a
+    begin on the wrong region or while a batch is open, an end with no step, a publish while a
+    batch is open and misaligned actions return CF2_ERR_INVALID_ARG; the well-formed sequence
+    returns CF2_OK."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_batch_misuse, args=(1, _port(), out), nprocs=1, join=True)
+    got = [int(v) for v in open(out).read().split()]
+    assert got == [-1, -1, -1, 0, -1, -1, -1, -1, 0, 0], got
+
+
 def test_delta_exchange_one_rccl_rank_batched_run_large_shard(gpu, tmp_path):
     """The same above 32 768 envs: the pack fused into step_kernel (256-env blocks, 4 pack blocks
     each, a ragged last block) instead of step_kernel_small."""
