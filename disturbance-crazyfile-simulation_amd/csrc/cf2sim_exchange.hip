@@ -662,6 +662,8 @@ extern "C" int cf2_xchg_step(cf2_xchg* x, cf2_ctx* ctx, const float* act_dev, fl
                              float* cost_dev, float* level_dev, void* env_stream) {
     if (!x || !x->open || !ctx || !act_dev || ((uintptr_t)act_dev & 15u) || !rew_dev || x->open_steps >= x->kmax)
         return CF2_ERR_INVALID_ARG;
+    cf2_layout lay;      // the env-step writes n rows of obs_len into the registered buffers: they must match
+    if (cf2_layout_get(ctx, &lay) != CF2_OK || lay.num_envs != x->n || lay.obs_len != x->ol) return CF2_ERR_INVALID_ARG;
     const hipStream_t es = (hipStream_t)env_stream;
     const uint32_t q = x->open_region, s = x->open_steps, cap = x->open_cap;
     uint32_t* pk = xchg_send(x, q) + (size_t)s * PackLayout{x->n, x->ol, cap}.words();

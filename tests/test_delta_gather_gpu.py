@@ -338,6 +338,9 @@ def _batch_misuse(rank, world, port, out):
     res.append(lib.cf2_xchg_end(x, 0, None, sp))                                            # open, but no step yet
     res.append(lib.cf2_xchg_publish(x, 0, 64, 1, sp))                                       # a batch is open
     res.append(lib.cf2_xchg_step(x, env._ctx, a.data_ptr() + 4, rew, trunc, cost, level, sp))   # misaligned actions
+    other = BatchedCrazyflieEnv(ENV_ID, 2 * n, seed=3, device=dev)
+    res.append(lib.cf2_xchg_step(x, other._ctx, a.data_ptr(), rew, trunc, cost, level, sp))  # a shard of another size
+    other.close()
     res.append(lib.cf2_xchg_step(x, env._ctx, a.data_ptr(), rew, trunc, cost, level, sp))   # ok
     res.append(lib.cf2_xchg_end(x, 0, None, sp))                                            # ok: exchanges step 0
     torch.cuda.synchronize()
@@ -352,12 +355,13 @@ def _batch_misuse(rank, world, port, out):
 def test_batch_calls_reject_misuse(gpu, tmp_path):
     """cf2_xchg_begin / cf2_xchg_step / cf2_xchg_end: a step or an end without an open batch, a
     begin on the wrong region or while a batch is open, an end with no step, a publish while a
-    batch is open and misaligned actions return CF2_ERR_INVALID_ARG; the well-formed sequence
+    batch is open, misaligned actions and an env of another shard size return CF2_ERR_INVALID_ARG;
+    the well-formed sequence
     returns CF2_OK."""
     out = str(tmp_path / "r.txt")
     mp.spawn(_batch_misuse, args=(1, _port(), out), nprocs=1, join=True)
     got = [int(v) for v in open(out).read().split()]
-    assert got == [-1, -1, -1, 0, -1, -1, -1, -1, 0, 0], got
+    assert got == [-1, -1, -1, 0, -1, -1, -1, -1, -1, 0, 0], got
 
 
 def test_delta_exchange_one_rccl_rank_batched_run_large_shard(gpu, tmp_path):
