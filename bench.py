@@ -145,7 +145,7 @@ def cpu_baseline(n_envs=16384, steps=1000, seed=0, threads=None):
                       f"(2048 envs x 600 env-steps, {dt1:.1f} s)"}
 
 
-GATHER_TIMEOUT_S = 180      # the gather key's watchdog (bench.py measures it last at N > 1)
+GATHER_TIMEOUT_S = 120      # the gather key's watchdog (bench.py measures it last at N > 1)
 
 
 def step_kernel_key() -> str:
