@@ -89,6 +89,42 @@ def test_kernel_matches_fp32_restatement(gpu, env_id, kw):
     assert fe.max() < 5e-4, "state field errors (err, field): " + repr(top)
 
 
+@pytest.mark.parametrize("env_id,kw", CASES)
+def test_kernel_matches_fp32_restatement_resynchronised(gpu, env_id, kw):
+    """The strict form of the test above: before every env-step the restatement is loaded with the
+    kernel's own state (cf2_get_state -> OracleEnv.set_state), so each of the 120 env-steps is
+    compared from identical bits and no chaotic growth can hide behind the 5e-4 band: every
+    observation within 2e-5 mixed abs/rel, rewards within 1e-5 (relative to 1 + |r|), done and
+    truncation exact, across auto-resets."""
+    from cf2sim.vec_env import BatchedCrazyflieEnv
+    n, T, seed = 512, 120, 3
+    env = BatchedCrazyflieEnv(env_id, n, seed=seed, want_final_obs=True, **kw)
+    ref = O.OracleEnv(build_config(env_id, n, seed=seed, **kw), precision="f32")
+    env.reset()
+    ref.reset()
+    rng = np.random.default_rng(seed + 1)
+    worst_o = worst_r = 0.0
+    dones = 0
+    for t in range(T):
+        gsf, gsi = env.get_state()
+        ref.set_state(gsf.cpu().numpy(), gsi.cpu().numpy())
+        a = _actions(rng, n)
+        g_o, g_r, g_d, g_i = env.step(torch.from_numpy(a).cuda())
+        r_o, r_r, r_d, r_i = ref.step(a, want_final=True)
+        g_o, g_r = g_o.cpu().numpy(), g_r.cpu().numpy()
+        worst_o = max(worst_o, float((np.abs(g_o - r_o) / (1.0 + np.abs(r_o))).max()))
+        worst_r = max(worst_r, float((np.abs(g_r - r_r) / (1.0 + np.abs(r_r))).max()))
+        np.testing.assert_array_equal(g_d.cpu().numpy().astype(bool), r_d)
+        np.testing.assert_array_equal(g_i["truncated"].cpu().numpy().astype(bool), r_i["truncated"])
+        dones += int(r_d.sum())
+    env.check_device_errors()
+    env.close()
+    ref.close()
+    assert worst_o < 2e-5, worst_o
+    assert worst_r < 1e-5, worst_r
+    assert dones > 0
+
+
 @pytest.mark.parametrize("env_id,kw", CASES[:3])
 def test_kernel_tracks_fp64_restatement(gpu, env_id, kw):
     errs, dmis, rew_err, (gsf, gsi), (rsf, rsi) = _run_pair(env_id, kw, 512, 120, "f64")
