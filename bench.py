@@ -507,8 +507,8 @@ def main(argv=None):
         time and this rank's HIP-event time on the launch stream"""
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         barrier_sync()
+        e0.record(stream)         # before the clock starts: recording costs host time, not GPU time
         t0 = time.perf_counter()
-        e0.record(stream)
         if graph is not None:
             for g_ in graph:
                 g_.replay()
