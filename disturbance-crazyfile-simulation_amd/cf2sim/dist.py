@@ -894,6 +894,8 @@ class PipelinedObsGather:
         """This rank's observation rows [n, D] of the latest env-step (step(), run(), step_and_publish
         or the caller's env-step into buffer()), before or after their exchange: what a policy in the
         loop acts on.  The done flags of that step: local_done()."""
+        if not self.delta or not self.started:
+            raise RuntimeError("local_obs(): a delta exchange after start()")
         if self._batch is not None:
             return self.obs[self._batch[3]]
         if self.k > 0:
@@ -901,6 +903,8 @@ class PipelinedObsGather:
         return self._start_rows[self.rank * self.n:(self.rank + 1) * self.n]
 
     def local_done(self):
+        if not self.delta or not self.started:
+            raise RuntimeError("local_done(): a delta exchange after start()")
         if self._batch is not None:
             return self.done[self._batch[3]]
         return self.done[self._where[self.k - 1][0]] if self.k > 0 else None
