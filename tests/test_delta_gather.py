@@ -197,6 +197,14 @@ def test_exchange_rejects_depth_one_and_short_lookahead():
         p = PipelinedObsGather(64, 34, "cpu", delta=True, max_steps=100)
         assert p.unit == 16 and p.L == 48 and p.depth == 2 and p.kmax == 1 and p.exchange == "gloo"
         assert p.npred == p.L + 17 and p.watch == 52
+        # the batched and per-step-batch calls need the native (RCCL) exchange; local rows need start()
+        with pytest.raises(RuntimeError):
+            p.step(None, 0)
+        with pytest.raises(RuntimeError):
+            p.run(None, [0], 16)
+        with pytest.raises(RuntimeError):
+            p.local_obs()
+        p.flush()                                    # no open batch: a no-op
     finally:
         dist.destroy_process_group()
 
