@@ -760,6 +760,7 @@ def main(argv=None):
         # the exchange path packs inside the env-step (cf2_step_packed): one node-shard context, its
         # env-step with and without the fused pack, alternating blocks of launches
         shard = BatchedCrazyflieEnv(args.env_id, n8, seed=args.seed + 1, device=dev, **env_kw)
+        bind_synthetic_tables(shard, dev)
         shard.reset()
         srew, strunc, scost, slevel = shard._raw_step_outputs()
         spk = torch.zeros(words, dtype=torch.int32, device=dev)

@@ -5,9 +5,10 @@ set -o pipefail
 OUT=${1:-gpurun_out/all_configs.jsonl}
 cd "$GRAFT_REPO_ROOT"
 : > "$OUT"
+: > "$OUT.err"
 run() {   # label, bench args...
   local label=$1; shift
-  timeout -k 10 180 python bench.py --steps 2000 --warmup 1000 --no-cpu-baseline --rollout-k 32 --streaming-ring 0 --oc-envs 0 "$@" 2>/dev/null |
+  timeout -k 10 180 python bench.py --steps 2000 --warmup 1000 --no-cpu-baseline --rollout-k 32 --streaming-ring 0 --oc-envs 0 "$@" 2>>"$OUT.err" |
     python -c "import json,sys; d=json.loads(sys.stdin.read()); d['label']='$label'; print(json.dumps(d))" >> "$OUT" || exit 1
 }
 run C2 --env-id DroneHoverBulletFreeEnvWithConstWind-v0 --envs-per-gpu 4096
