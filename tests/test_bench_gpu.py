@@ -115,3 +115,18 @@ def test_pipelined_gather_matches_env_obs(gpu, tmp_path):
     out = str(tmp_path / "res.txt")
     mp.spawn(_pipe_worker, args=(1, _port(), out), nprocs=1, join=True)
     assert open(out).read() == "ok"
+
+
+def test_bench_hj_config_runs_the_node_shard_probe(gpu):
+    # every BASELINE config goes through the same line (tools/all_configs.sh): on the HJ-adversary
+    # env the node-shard exchange probe's own env must have value tables bound too
+    assert SHORT[-2:] == ["--exchange-probe", "0"]
+    args = SHORT[:-2] + ["--exchange-probe", "1"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--env-id",
+                        "DroneHoverBulletFreeEnvWithAdversary-v0", *args], env=_env(), capture_output=True,
+                       text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    assert d["value"] > 0 and "synthetic 15^6 HJ value tables" in d["data"]
+    x = d["delta_exchange"]
+    assert x["node_shard_step_us"] > 0 and x["node_shard_step_packed_us"] > 0
