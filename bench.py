@@ -16,17 +16,18 @@ streams from HBM every step, as under a training loop's fresh action and rollout
 
 Multi-GPU: one process per GPU.  Under torchrun the ranks come from the environment; with
 `--gpus N` and no launcher, bench.py starts its own N ranks as child processes before anything
-touches the GPU (the role of the reference's mpi_fork, utils/mpi_tools.py:47-99).  The envs are
-independent (no collective for the physics), so every rank steps BASELINE's
-262 144-env workload on its own global ids with no data-path collective ("scaling": "weak"; value =
-all ranks' env-steps / the max over ranks of the timed region).  Extra keys of the line:
-"strong_scaling" (the 262 144 envs split over the ranks, 32 768 per GPU at N = 8) and "gather", the
-north star's optional per-step RCCL all-gather of the observations over xGMI for those split envs
-(--gather-obs, default on at N > 1): delta rows (o_k of every env, a reset bitmap and the reset
-rows' first halves; every rank advances the envs' ages and materialises any rows bit-identically
-on request), 2.36x fewer xGMI bytes than the full rows (--gather-mode full), with the env-steps
-back to back (the pack fused into the env-step kernel) and one all-gather + consume per batch of
-16 env-steps on the library's own RCCL communicator (PipelinedObsGather.run / cf2_xchg_run).
+touches the GPU (the role of the reference's mpi_fork, utils/mpi_tools.py:47-99).  At N > 1 the
+headline is BASELINE configs[3] itself: the 262 144 envs split over the ranks (32 768 per GPU at
+N = 8, contiguous global-id shards, "scaling": "strong") with the north star's RCCL all-gather of
+the observations over xGMI inside the timed region -- delta rows (o_k of every env, a reset bitmap
+and the reset rows' first halves; every rank advances the envs' ages and materialises any rows
+bit-identically on request), 2.36x fewer xGMI bytes than the full rows, the env-steps back to back
+with the pack fused into the env-step kernel and one all-gather + consume per batch of 16 on the
+library's own RCCL communicator (PipelinedObsGather.run / cf2_xchg_run); `value` = 262 144 x K
+env-steps / the max over ranks of the timed region.  Extra keys: "collective_free" (the same split
+without the gather: the fallback headline, with "gather_obs": false and the error stated, if the
+gather fails) and "weak_scaling" (every rank stepping 262 144 envs of its own).  --scaling weak
+makes the weak run the headline instead (the gather then an extra key).
 """
 from __future__ import annotations
 
@@ -251,25 +252,29 @@ def parse_args(argv=None):
     # env-steps 50-250); after ~1000 env-steps the reset rate is stationary (tools/reset_rate.py)
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=1000)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak (default): every rank steps BASELINE's 262 144 envs (its own global ids), no data-path "
-                         "collective; strong: --global-envs split over the ranks")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default): BASELINE's --global-envs (262 144) split over the ranks, at N > 1 with the "
+                         "RCCL observation all-gather in the timed region (configs[3]); weak: every rank steps 262 144 "
+                         "envs of its own global ids, no data-path collective")
     ap.add_argument("--global-envs", type=int, default=METRIC_GLOBAL_ENVS,
                     help="--scaling strong: envs over the whole job, each rank stepping its contiguous shard")
     ap.add_argument("--envs-per-gpu", type=int, default=None,
                     help="weak scaling with this many envs on every rank (default 262 144)")
     ap.add_argument("--gather-obs", dest="gather_obs", action="store_true", default=None,
-                    help="also time the north star's per-step RCCL all-gather of the observations over the 262 144 envs "
-                         "split across the ranks (the line's gather key; default: on at N > 1; at N = 1 under a "
-                         "launcher: one RCCL rank)")
+                    help="the north star's per-step RCCL all-gather of the observations over the 262 144 envs split "
+                         "across the ranks (default: on at N > 1, where it is the headline; at N = 1 under a launcher: "
+                         "one RCCL rank, the gather key)")
     ap.add_argument("--no-gather-obs", dest="gather_obs", action="store_false")
     ap.add_argument("--gather-mode", choices=("delta", "full"), default="delta",
                     help="delta: o_k + reset side slab, rows materialised on request (default); full: the rows")
-    ap.add_argument("--gather-steps", type=int, default=2000, help="env-steps the gather key times")
+    ap.add_argument("--gather-steps", type=int, default=2000,
+                    help="env-steps the gather key times when the gather is not the headline (the headline times --steps)")
     ap.add_argument("--gather-envs", type=int, default=METRIC_GLOBAL_ENVS,
                     help="envs over the whole job in the gather key (split over the ranks)")
     ap.add_argument("--strong-steps", type=int, default=1000,
-                    help="N > 1: the strong_scaling key times 262 144 envs split over the ranks; 0 = skip")
+                    help="N > 1, --scaling weak: the strong_scaling key times 262 144 envs split over the ranks; 0 = skip")
+    ap.add_argument("--weak-steps", type=int, default=1000,
+                    help="N > 1, --scaling strong: the weak_scaling key times 262 144 envs on every rank; 0 = skip")
     ap.add_argument("--oc-envs", type=int, default=1 << 20,
                     help="N = 1: the out-of-cache line steps this many envs (working set far beyond the 256 MB "
                          "Infinity Cache, so state traffic is HBM traffic); 0 = skip")
@@ -322,14 +327,16 @@ def working_set_bytes(env, ring: int) -> int:
     return n * 480 + ring * n * 16 + n * (4 * od + 4 + 1 + 1 + 4 + 4)
 
 
-def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks) -> dict:
+def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks, steps=None,
+                  warmup=None) -> dict:
     """The north star's per-step all-gather of the observations ("RCCL all-gather over xGMI only for
     the returned observation tensor"): --gather-envs (262 144) envs split over the ranks, every
     env-step's observations made available on every rank (cf2sim.dist.PipelinedObsGather: the delta
     rows, 2.36x fewer bytes than the full rows; over RCCL the native exchange, env-steps back to back
     with the pack fused in and one all-gather + consume per batch of 16).  Timed like the headline:
-    barrier + synchronize on both sides of exactly --gather-steps env-steps, max over ranks.  The
-    rows of the last step, materialised on every rank, must equal a full all-gather of them."""
+    barrier + synchronize on both sides of exactly `steps` (default --gather-steps) env-steps after
+    `warmup` (default --warmup), max over ranks.  The rows of the last step, materialised on every
+    rank, must equal a full all-gather of them."""
     import torch
     import torch.distributed as dist
     from cf2sim.dist import PipelinedObsGather, delta_supported, gather_rows, shard_range
@@ -368,11 +375,12 @@ def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_ove
                 env.step_raw(act_p[k % ring], obs_ptr=b.data_ptr())
             pipe.publish()
 
-    steps_of(args.warmup)
+    steps = args.gather_steps if steps is None else int(steps)
+    steps_of(args.warmup if warmup is None else int(warmup))
     pipe.drain()
     barrier_sync()
     t0 = time.perf_counter()
-    steps_of(args.gather_steps)
+    steps_of(steps)
     pipe.drain()
     torch.cuda.synchronize()
     dist.barrier()
@@ -398,9 +406,9 @@ def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_ove
         del full, rows
     per_rank = pipe.bytes_per_rank_per_step
     rx = (world - 1) * per_rank                       # bytes this rank receives per step
-    ms = el / args.gather_steps * 1e3
-    out = {"value": args.gather_envs * args.gather_steps / el, "unit": "env-steps/s", "ms_per_step": ms,
-           "steps": args.gather_steps, "global_envs": args.gather_envs, "envs_per_gpu": n, "scaling": "strong",
+    ms = el / steps * 1e3
+    out = {"value": args.gather_envs * steps / el, "unit": "env-steps/s", "ms_per_step": ms,
+           "steps": steps, "global_envs": args.gather_envs, "envs_per_gpu": n, "scaling": "strong",
            "mode": ("delta rows (o_k + reset bitmap + side slab of the crash budget + predicted time-outs); "
                     "every rank advances the ages, rows on request" if delta else "full rows"),
            "exchange": pipe.exchange,
@@ -418,6 +426,31 @@ def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_ove
     pipe.close()
     env.close()
     return out
+
+
+def merge_gather(line: dict, info: dict, headline: bool, world: int, backend) -> dict:
+    """Put the gather's result into the line.  As the headline (N > 1, BASELINE configs[3]) a
+    successful gather replaces the collective-free value, step count and time per step and marks
+    the config gather_obs; a failed one leaves the collective-free split as the headline
+    (gather_obs false) with the error stated in config.gather_error -- never the weak figure."""
+    line["gather"] = info
+    if not headline:
+        return line
+    cf = line["config"]
+    if "error" in info:
+        cf["gather_obs"] = False
+        cf["gather_error"] = info["error"]
+        return line
+    line["value"] = info["value"]
+    line["ms_per_step"] = info["ms_per_step"]
+    line["steps"] = info["steps"]
+    cf["gather_obs"] = True
+    cf.pop("gather_error", None)
+    cf["workload"] += (f", the observations of every env-step all-gathered to every rank "
+                       f"({info['exchange']} exchange, {info['mode'].split(' (')[0]})")
+    cf["parallelism"] = (f"env-shard x{world}, {'RCCL' if backend == 'nccl' else backend} all-gather of the "
+                         "observations every env-step")
+    return line
 
 
 def main(argv=None):
@@ -459,11 +492,12 @@ def main(argv=None):
 
     from cf2sim.vec_env import BatchedCrazyflieEnv
 
-    # the timed workload: BASELINE's metric config (262 144 envs, C4 gust) on every GPU.  The envs
-    # are independent (no collective for the physics), so at N > 1 every rank
-    # steps its own 262 144 global ids with no data-path collective ("scaling": "weak"; --scaling
-    # strong splits the 262 144 over the ranks instead).  The north star's optional per-step
-    # all-gather of the observations is its own measured object of the line ("gather", below).
+    # the timed workload: BASELINE's metric config, 262 144 envs (C4 gust) over the whole job, each
+    # rank stepping its contiguous global-id shard ("scaling": "strong"; at N = 1 all of them).  At
+    # N > 1 the headline also carries the north star's per-step RCCL all-gather of the observations
+    # (configs[3]); the env-steps of the shard without it are timed first here ("collective_free":
+    # the headline's fallback and the step kernel's roofline at the shard size).  --scaling weak:
+    # every rank steps 262 144 envs of its own, no data-path collective, the gather an extra key.
     if args.scaling == "strong" and not args.envs_per_gpu:
         off, n = shard_range(args.global_envs, rank, world)
         shards = [shard_range(args.global_envs, r, world)[1] for r in range(world)]
@@ -474,6 +508,10 @@ def main(argv=None):
     global_envs = sum(shards)
     gather = (world > 1) if args.gather_obs is None else bool(args.gather_obs)
     gather = gather and use_pg
+    # the gather is the headline at N > 1 under strong scaling (BASELINE configs[3])
+    headline_gather = gather and world > 1 and scaling == "strong"
+    if headline_gather and args.gather_envs != global_envs:
+        raise SystemExit("bench.py: the gathered headline splits --global-envs; pass the same --gather-envs")
 
     def max_over_ranks(x: float) -> float:
         if not use_pg:
@@ -539,6 +577,30 @@ def main(argv=None):
     # ---- timed region: exactly K steps between barrier + synchronize, max over ranks ----
     elapsed, ev_ms = run(args.steps, graph)
     kern_ms = ev_ms / args.steps
+
+    weak = None
+    if world > 1 and scaling == "strong" and args.weak_steps > 0:
+        # every rank stepping 262 144 envs of its own global ids, no collective (weak scaling)
+        wn = METRIC_GLOBAL_ENVS
+        wenv = BatchedCrazyflieEnv(args.env_id, wn, seed=args.seed, env_id_offset=rank * wn, device=dev, **env_kw)
+        bind_synthetic_tables(wenv, dev)
+        wenv.reset()
+        wacts = torch.rand(ring, wn, 4, device=dev, generator=g) * 2 - 1
+        wp = [wacts[r].data_ptr() for r in range(ring)]
+        for k in range(args.warmup):
+            wenv.step_raw(wp[k % ring])
+        barrier_sync()
+        t0 = time.perf_counter()
+        for k in range(args.weak_steps):
+            wenv.step_raw(wp[k % ring])
+        torch.cuda.synchronize()
+        dist.barrier()
+        wel = max_over_ranks(time.perf_counter() - t0)
+        weak = {"envs_per_gpu": wn, "global_envs": wn * world, "steps": args.weak_steps, "gather_obs": False,
+                "scaling": "weak", "value": wn * world * args.weak_steps / wel, "unit": "env-steps/s",
+                "ms_per_step": wel / args.weak_steps * 1e3}
+        wenv.close()
+        del wacts
 
     strong = None
     if world > 1 and scaling == "weak" and args.strong_steps > 0:
@@ -893,7 +955,7 @@ def main(argv=None):
                                    f" ({n} per GPU)",
                        "envs_per_gpu": n, "global_envs": global_envs, "aggregate_phy_steps": 2,
                        "parallelism": f"env-shard x{world}, no data-path collective",
-                       "gather_obs": bool(gather),
+                       "gather_obs": bool(gather) and not headline_gather,
                        "graph": bool(args.graph)},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS,
@@ -908,33 +970,51 @@ def main(argv=None):
                          "out_of_cache": out_of_cache},
             "cpu_baseline": cpu,
             "gather": None,
+            "collective_free": None,
             "strong_scaling": strong,
+            "weak_scaling": weak,
             "fused_rollout": fused,
             "collect": collect_line,
             "streaming_actions": streaming,
             "two_streams": two_streams,
             "delta_exchange": exchange,
         }
+    if line is not None and headline_gather:
+        # the collective-free split stands as the headline until the gathered run has succeeded
+        line["collective_free"] = {"value": value, "unit": "env-steps/s", "steps": args.steps,
+                                   "ms_per_step": elapsed / args.steps * 1e3, "kernel_ms_per_launch": kern_ms,
+                                   "envs_per_gpu": n, "global_envs": global_envs, "gather_obs": False}
+        line["config"]["gather_error"] = "the gathered run had not completed"
     if gather:
         # measured last, under a watchdog: the line above is complete without it, and a rank that
         # fails or stalls inside the exchange's collectives must not cost the line
         import threading
 
         def stalled():
+            # a stalled collective: the line goes out with the collective-free headline and the
+            # error stated, and the process ends non-zero so the stall is visible to the caller
             if line is not None:
                 line["gather"] = {"error": f"no result after {GATHER_TIMEOUT_S} s"}
+                if headline_gather:
+                    line["config"]["gather_error"] = line["gather"]["error"]
                 print(json.dumps(line), flush=True)
-            os._exit(0)
+            os._exit(3)
         dog = threading.Timer(GATHER_TIMEOUT_S, stalled)
         dog.daemon = True
         dog.start()
         try:
-            gather_info = exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks)
+            if headline_gather:
+                # BASELINE configs[3]: exactly --steps env-steps of the split envs after --warmup,
+                # the all-gather of every env-step's observations inside the timed region
+                gather_info = exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks,
+                                            steps=args.steps, warmup=args.warmup)
+            else:
+                gather_info = exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_over_ranks)
         except Exception as e:          # every rank reports; a stall on the others ends at the watchdog
             gather_info = {"error": repr(e)[:300]}
         dog.cancel()
         if line is not None:
-            line["gather"] = gather_info
+            merge_gather(line, gather_info, headline_gather, world, backend)
     if line is not None:
         print(json.dumps(line), flush=True)
     env.check_device_errors()

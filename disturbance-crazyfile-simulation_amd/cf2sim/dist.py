@@ -77,7 +77,9 @@ def run_ranks(plan, timeout: float | None = None) -> int:
 PACK_BLOCK = 64       # envs per pack block: one block-table word each (the side slot of the block's first reset)
 PACK_DROPPED = -1     # block-table word (int32 view of 0xFFFFFFFF): the block's resets past its quota got no slot
 PACK_SCRATCH_WORDS = 32    # the spill counter of a pack (csrc/cf2sim_pack.h), past the largest packed buffer
-ZERO_AHEAD = 8        # a consume zeroes the look-ahead rows of the 8 steps after its own
+ZERO_AHEAD = 16       # a consume zeroes the look-ahead rows of up to 16 steps after its own (CONSUME_MAX of
+                      # csrc/cf2sim_exchange.hip: the native consume's count; the torch ops zero one)
+NPRED_MIN = 2 * ZERO_AHEAD + 1    # cf2_xchg_register's smallest count ring when the time-out watch is on
 NO_WATCH = 0xFFFFFFFF
 PRED_BATCH = 4        # eager exchange: the time-out count ring is copied to the host every 4 env-steps
 RUN_UNIT = 16         # native exchange: env-steps per batch of PipelinedObsGather.run (one all-gather each)
@@ -197,8 +199,9 @@ def pack_obs(obs, reset, cap: int, out=None, scratch=None, next_scratch=None):
 
 
 def pack_quota(n: int, cap: int) -> int:
-    """Side slots each 64-env pack block owns (PackLayout::quota): min(cap // blocks, 64)."""
-    return min(int(cap) // ((int(n) + PACK_BLOCK - 1) // PACK_BLOCK), PACK_BLOCK)
+    """Side slots each 64-env pack block owns (PackLayout::quota): min(cap, default_cap(n)) // blocks,
+    at most 64.  Capacity above the default crash budget (predicted time-outs) is all spill area."""
+    return min(min(int(cap), default_cap(n)) // ((int(n) + PACK_BLOCK - 1) // PACK_BLOCK), PACK_BLOCK)
 
 
 def _slots(pk, n: int, ol: int, cap: int, rs):
@@ -335,26 +338,32 @@ def _close_live_exchanges():
         g.close()
 
 
+def _pg_device(group, device):
+    """Where the process group's collectives take their tensors: the GPU over RCCL, the host over gloo."""
+    import torch.distributed as dist
+    return device if dist.get_backend(group) == "nccl" else "cpu"
+
+
 def _agree(ok: bool, group, device) -> bool:
     """True on every rank iff ok on every rank (all_reduce MIN over the group)."""
     import torch
     import torch.distributed as dist
-    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_pg_device(group, device))
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return bool(int(t.item()))
 
 
-def _native_exchange(lib, group, world: int, depth: int, device):
+def _native_exchange(lib, group, world: int, depth: int, device, rccl_path: str | None = None):
     """The RCCL communicator of cf2_xchg_* for this group, created on `device` (collective: every
     rank calls it).  Every stage ends with an agreement over the process group, so a failure on one
     rank makes every rank fall back together (returns None) instead of leaving the others blocked
     in the id broadcast or in the communicator's rendezvous.  PyTorch's own RCCL instance where it
-    ships one; rank 0's id broadcast over the process group."""
+    ships one (or the library at rccl_path); rank 0's id broadcast over the process group."""
     import ctypes
     import torch
     import torch.distributed as dist
     from . import _native
-    path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    path = rccl_path or os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
     ok = lib.cf2_xchg_bind(path.encode() if os.path.exists(path) else None) == 0
     rank = dist.get_rank(group)
     idb = (ctypes.c_uint8 * 128)()
@@ -362,7 +371,7 @@ def _native_exchange(lib, group, world: int, depth: int, device):
         ok = lib.cf2_xchg_unique_id(idb, 128) == 0
     if not _agree(ok, group, device):
         return None
-    t = torch.tensor(list(bytes(idb)), dtype=torch.uint8, device=device)
+    t = torch.tensor(list(bytes(idb)), dtype=torch.uint8, device=_pg_device(group, device))
     dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
     idb = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(t.cpu().tolist()))
     h = ctypes.c_void_p()
@@ -395,6 +404,9 @@ class PipelinedObsGather:
     (cf2_obs_rows) from the gathered buffers of that step and the one before and the actions of
     the last three steps ([world * n, 4], the policy's own outputs); they are valid until the next
     publish / run.  ``start(obs)`` gathers the observations of a reset of every env in full first.
+    The native exchange runs over RCCL process groups; ``rccl_path`` binds it to another library
+    with RCCL's four entry points instead (cf2_xchg_bind), also under a gloo group (the tests'
+    world-size-2 stand-in on one GPU).
     The side capacity of step k is ``cap`` (the crash budget, default_cap) plus the time-outs the
     step can have at most (max_steps: the env's TimeLimit; the receivers count the envs that reach
     max_steps - lookahead, every rank the same, and the host reads the count ``lookahead`` steps
@@ -405,7 +417,8 @@ class PipelinedObsGather:
     publish / batch.  Shards must be equal (ValueError otherwise)."""
 
     def __init__(self, n: int, obs_dim: int, device, group=None, depth: int = 2, delta: bool = False,
-                 cap: int | None = None, max_steps: int = 0, lookahead: int | None = None, unit: int = RUN_UNIT):
+                 cap: int | None = None, max_steps: int = 0, lookahead: int | None = None, unit: int = RUN_UNIT,
+                 rccl_path: str | None = None):
         import torch
         import torch.distributed as dist
         if not 2 <= int(depth) <= 8:
@@ -424,7 +437,8 @@ class PipelinedObsGather:
         self.device = torch.device(device)
         cuda = self.device.type == "cuda"
         self.obs = [torch.empty(n, obs_dim, device=device) for _ in range(self.depth)]
-        self.comm = torch.cuda.Stream(device=self.device) if (self.nccl and cuda) else None
+        native_ok = cuda and (self.nccl or (self.delta and rccl_path is not None))
+        self.comm = torch.cuda.Stream(device=self.device) if native_ok else None
         self.k = 0
         self.started = not self.delta
         self.bytes_sent = 0                  # this rank's contribution to every gather since start()
@@ -450,7 +464,7 @@ class PipelinedObsGather:
         self.watch = self.max_steps - self.L if self.max_steps > self.L else NO_WATCH
         # ring of per-step counts: a consume writes its steps' rows and zeroes the ZERO_AHEAD rows after
         # them, so a host copy made after step e holds the counts of steps e - npred + ZERO_AHEAD + 1 .. e
-        self.npred = self.L + 2 * ZERO_AHEAD + 1
+        self.npred = max(self.L + 2 * ZERO_AHEAD + 1, NPRED_MIN)
         self.done = [torch.zeros(n, dtype=torch.uint8, device=device) for _ in range(self.depth)]
         self.age = torch.zeros(self.world * n, dtype=torch.int16 if cuda else torch.int32, device=device)
         self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
@@ -470,10 +484,12 @@ class PipelinedObsGather:
             # the whole exchange natively on our own RCCL communicator (cf2_xchg_*), unless
             # CF2SIM_EXCHANGE=torch asks for the process group's all-gather between the launches
             if os.environ.get("CF2SIM_EXCHANGE", "native") == "native":
-                self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device)
+                self._xchg = _native_exchange(self._lib, group, self.world, self.depth, self.device, rccl_path)
                 if self._xchg is None:
                     import warnings
                     warnings.warn("native exchange unavailable on some rank; using the process group's all-gather")
+            if self._xchg is None and not self.nccl:
+                self.comm = None             # a gloo group without the native exchange: via the host
         # buffers: `depth` regions, each the packed buffers of a batch of up to kmax steps; the side-slot
         # counters of every (region, slot) after them (csrc/cf2sim_exchange.hip, cf2_xchg_register)
         self.kmax = self.unit if self._xchg is not None else 1

@@ -311,7 +311,10 @@ int cf2_bind_hj_tables(cf2_ctx* ctx, const float* V_dev, int num_tables, const i
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     KTables T = ctx->T;
     for (int l = 0; l < ctx->cfg.num_levels; ++l) T.table_of_level[l] = table_of_level[l];
-    if (e == hipSuccess) e = hipMemcpy(ctx->tab_dev, &T, sizeof(KTables), hipMemcpyHostToDevice);
+    // only the level -> table map: a whole-block upload would also clear the device error word, and
+    // with it any flag the kernels recorded before the rebind (cf2_device_errors reports them)
+    if (e == hipSuccess)
+        e = hipMemcpy(ctx->tab_dev->table_of_level, T.table_of_level, sizeof(T.table_of_level), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         if (fresh) (void)hipFree(bits);
         else {   // the old buffer was partly overwritten: the context has no valid tables now

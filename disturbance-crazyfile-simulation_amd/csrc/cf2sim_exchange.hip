@@ -694,10 +694,18 @@ extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb,
     for (uint32_t a = 0; a < nact; ++a)
         if (!act_dev[a] || ((uintptr_t)act_dev[a] & 15u)) return CF2_ERR_INVALID_ARG;
     int st = cf2_xchg_begin(x, cap, region, env_stream);
+    if (st != CF2_OK) return st;           // nothing taken
     for (uint32_t s = 0; st == CF2_OK && s < nb; ++s)
         st = cf2_xchg_step(x, ctx, act_dev[(k0 + s) % nact], rew_dev, trunc_dev, cost_dev, level_dev, env_stream);
     if (st != CF2_OK) {
-        x->open = false;      // the region stays taken; the caller's count moved on with it
+        // the batch is abandoned: the region is given back (the caller's count, which a failed call
+        // does not advance, stays in step with ours) and the spill counters its packs took so far
+        // are zeroed, so the region's next use starts from empty counters as after an exchange
+        x->open = false;
+        --x->next_region;
+        if (x->open_steps > 0)
+            (void)hipMemsetAsync(xchg_scratch(x, region, 0), 0, (size_t)x->open_steps * PACK_SCRATCH_WORDS * sizeof(uint32_t),
+                                 (hipStream_t)env_stream);
         return st;
     }
     return cf2_xchg_end(x, k0, pred_host, env_stream);

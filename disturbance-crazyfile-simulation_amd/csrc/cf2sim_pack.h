@@ -11,11 +11,16 @@
 //                                       resets past its quota (or PACK_DROPPED: the spill area had no
 //                                       room for them; 0 when the block has no more than its quota)
 //   [.., + cap (OL + 5))                side entries: local env index, o_0[OL], A[4]
-// Side slots: the first nblk * quota slots belong to the pack blocks, quota = min(cap / nblk, 64)
-// consecutive slots each, taken by the block's first quota resets in env order with no atomic; the
-// rest of the capacity is a shared spill area, where a block with more resets than its quota takes
-// the excess as consecutive slots with one atomic on a counter.  At the default capacity (7.5 % of
-// the shard: quota 4) 88 % of the blocks of the steady 4.1 % reset rate need no atomic.  Every block
+// Side slots: the first nblk * quota slots belong to the pack blocks, quota consecutive slots each,
+// taken by the block's first quota resets in env order with no atomic; the rest of the capacity is
+// a shared spill area, where a block with more resets than its quota takes the excess as
+// consecutive slots with one atomic on a counter.  quota = min(cap, default crash budget) / nblk
+// (at most 64), the default budget being 7.5 % of the shard (cf2sim.dist.default_cap): at it the
+// quota is 4 and 88 % of the blocks of the steady 4.1 % reset rate need no atomic.  Capacity above
+// the budget (the predicted time-outs the caller adds) all goes to the spill area, so predicted
+// time-outs fit however they fall over the blocks.  (With quota = cap / nblk, a capacity just above
+// a multiple of nblk -- 2575 at 32 768 envs -- left a spill area of 15 slots: quota 5 instead of 4
+// and overflows at a reset count half the capacity, tools/xchg_watch_probe.py, gpurun_out/r06b.)  Every block
 // taking its slots from one counter serialised at the memory-side atomic unit (~35 ns per atomic on
 // one address: 19.5 us for a 32 768-env pack, round 4); eight per-XCD counters (round 5) still cost
 // the fused step ~2 us at 32 768 envs.
@@ -42,8 +47,16 @@ struct PackLayout {
     __host__ __device__ uint32_t entry() const { return ol + 5u; }
     __host__ __device__ uint32_t words() const { return (side() + cap * entry() + 3u) & ~3u; }
     __host__ __device__ uint32_t nblk() const { return (n + XB_PACK - 1u) / XB_PACK; }
+    // the default crash budget of an n-env shard: 7.5 %, at least 64, at most n (dist.default_cap)
+    __host__ __device__ uint32_t budget() const {
+        const uint32_t c = (3u * n + 39u) / 40u;
+        return c < 64u ? (n < 64u ? n : 64u) : (c < n ? c : n);
+    }
     // side slots each pack block owns, then the start and size of the shared spill area
-    __host__ __device__ uint32_t quota() const { const uint32_t q = cap / nblk(); return q < XB_PACK ? q : XB_PACK; }
+    __host__ __device__ uint32_t quota() const {
+        const uint32_t c = cap < budget() ? cap : budget(), q = c / nblk();
+        return q < XB_PACK ? q : XB_PACK;
+    }
     __host__ __device__ uint32_t spill_base() const { return nblk() * quota(); }
     __host__ __device__ uint32_t spill() const { return cap - spill_base(); }
 };

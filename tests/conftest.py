@@ -17,6 +17,7 @@ def pytest_configure(config):
 @pytest.fixture(scope="session", autouse=True)
 def _build_oracle():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "standin_rccl")], check=True)
 
 
 @pytest.fixture(scope="session")

@@ -1,10 +1,10 @@
 """bench.py's multi-rank measurement path on a GPU box.
 
 - `bench.py --gpus 2` without a launcher starts its own two ranks (CF2_BENCH_BACKEND=gloo: both
-  ranks share the one MI355X of the test box), each stepping BASELINE's metric config (262 144
-  envs) with no collective, and prints one line with n_gpus = world_size = 2, "scaling": "weak",
-  the strong-scaling key and the gather key (the observation exchange over the 262 144 envs split
-  across the ranks).
+  ranks share the one MI355X of the test box) and prints one line with n_gpus = world_size = 2
+  whose value is BASELINE configs[3]: the 262 144 envs split over the ranks with the observation
+  all-gather in the timed region ("scaling": "strong"), plus the collective-free split and the
+  weak-scaling key.
 - Under torchrun with one rank and --gather-obs, the RCCL ("nccl") native exchange runs (batches
   of env-steps with the pack fused in, one all-gather + consume each), the path the 8-GPU run
   takes; its rows equal a full all-gather.
@@ -21,7 +21,7 @@ import torch
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = ["--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--rollout-k", "0", "--streaming-ring", "0",
-         "--oc-envs", "0", "--strong-steps", "20", "--gather-steps", "40", "--collect-steps", "0",
+         "--oc-envs", "0", "--strong-steps", "20", "--weak-steps", "20", "--gather-steps", "40", "--collect-steps", "0",
          "--exchange-probe", "0"]
 
 
@@ -49,16 +49,25 @@ def test_bench_self_launches_two_ranks(gpu):
     assert p.returncode == 0, p.stderr[-3000:]
     d = _line(p.stdout)
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
-    assert d["config"]["global_envs"] == 2 * 262144 and d["config"]["envs_per_gpu"] == 262144
-    assert d["scaling"] == "weak" and d["value"] > 0 and d["config"]["gather_obs"] is True
-    assert d["strong_scaling"]["global_envs"] == 262144 and d["strong_scaling"]["value"] > 0
-    # the delta exchange (default) of the 262 144 envs split over the ranks: 2.3x fewer bytes than
-    # the rows, no side-slab overflow, the rows on request equal to a full all-gather
+    # the headline is BASELINE configs[3]: the 262 144 envs split over the ranks with the
+    # observation all-gather of every env-step inside the timed region (strong scaling)
+    assert d["config"]["global_envs"] == 262144 and d["config"]["envs_per_gpu"] == 131072
+    assert d["scaling"] == "strong" and d["config"]["gather_obs"] is True and "gather_error" not in d["config"]
     gi = d["gather"]
+    assert d["value"] == gi["value"] > 0 and d["ms_per_step"] == gi["ms_per_step"]
+    assert gi["global_envs"] == 262144 and gi["steps"] == d["steps"] == 20
+    # the delta exchange (default): 2.3x fewer bytes than the rows, no side-slab overflow, the rows
+    # on request equal to a full all-gather
     assert gi["mode"].startswith("delta rows") and gi["exchange"] == "gloo" and gi["envs_per_gpu"] == 131072
     assert gi["full_rows_bytes_per_rank_per_step"] == 131072 * 34 * 4
     assert gi["bytes_per_rank_per_step"] * 2.3 <= gi["full_rows_bytes_per_rank_per_step"]
     assert gi["overflows"] == 0 and gi["rows_on_request"]["equal_to_full_gather"] is True
+    # the extra keys: the same split without the gather (the fallback headline) and every rank
+    # stepping 262 144 envs of its own (weak scaling)
+    cf = d["collective_free"]
+    assert cf["global_envs"] == 262144 and cf["gather_obs"] is False and cf["value"] > 0
+    w = d["weak_scaling"]
+    assert w["global_envs"] == 2 * 262144 and w["envs_per_gpu"] == 262144 and w["value"] > 0
 
 
 def test_bench_rccl_gather_path_one_rank(gpu):

@@ -80,10 +80,10 @@ def test_metric_config_shards(world):
 
 def test_bench_defaults_are_the_metric_config():
     a = bench.parse_args([])
-    # every rank steps BASELINE's 262 144 envs, no data-path collective; the north
-    # star's all-gather splits the 262 144 over the ranks in its own key
-    assert a.scaling == "weak" and a.envs_per_gpu is None and a.gather_envs == 262144
-    assert a.global_envs == 262144 and bench.parse_args(["--scaling", "strong"]).scaling == "strong"
+    # BASELINE configs[3]: 262 144 envs over the whole job, split over the ranks, with the north
+    # star's observation all-gather (the headline at N > 1); --scaling weak: 262 144 on every rank
+    assert a.scaling == "strong" and a.envs_per_gpu is None and a.gather_envs == 262144
+    assert a.global_envs == 262144 and bench.parse_args(["--scaling", "weak"]).scaling == "weak"
     assert a.gather_obs is None          # on at N > 1, off at N = 1
     assert a.steps == 10000 and a.warmup == 1000
     assert bench.parse_args(["--no-gather-obs"]).gather_obs is False
@@ -105,3 +105,32 @@ def test_self_launch_propagates_rank_failure(tmp_path, monkeypatch):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert "JSONDecodeError" in p.stderr                  # a child ran and failed
+
+
+def _line(value=1.0):
+    return {"value": value, "steps": 10, "ms_per_step": 0.5, "config": {
+        "workload": "w", "parallelism": "env-shard x8, no data-path collective", "gather_obs": False,
+        "gather_error": "the gathered run had not completed"}}
+
+
+def test_gathered_headline_replaces_the_collective_free_value():
+    """N > 1: a successful gather is the headline (BASELINE configs[3]: 262 144 envs split over the
+    ranks, the observation all-gather in the timed region)."""
+    info = {"value": 2e10, "ms_per_step": 0.013, "steps": 10, "exchange": "native",
+            "mode": "delta rows (o_k + ...)", "global_envs": 262144}
+    line = bench.merge_gather(_line(), info, True, 8, "nccl")
+    assert line["value"] == 2e10 and line["ms_per_step"] == 0.013 and line["gather"] is info
+    cf = line["config"]
+    assert cf["gather_obs"] is True and "gather_error" not in cf and "RCCL all-gather" in cf["parallelism"]
+
+
+def test_failed_gather_keeps_the_collective_free_split_never_the_weak_figure():
+    line = bench.merge_gather(_line(7.0), {"error": "RuntimeError('x')"}, True, 8, "nccl")
+    assert line["value"] == 7.0 and line["config"]["gather_obs"] is False
+    assert line["config"]["gather_error"] == "RuntimeError('x')"
+
+
+def test_gather_as_an_extra_key_leaves_the_headline():
+    info = {"value": 3.0, "ms_per_step": 1.0, "steps": 40, "exchange": "native", "mode": "delta rows"}
+    line = bench.merge_gather(_line(5.0), info, False, 1, "nccl")
+    assert line["value"] == 5.0 and line["gather"] is info and line["steps"] == 10

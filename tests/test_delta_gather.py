@@ -184,7 +184,7 @@ def test_exchange_rejects_depth_one_and_short_lookahead():
     """depth 1 would let a pack clear its own count word (and a step's rows need the gathered
     buffers of the step before); a look-ahead shorter than the copy cadence could not be served."""
     import torch.distributed as dist
-    from cf2sim.dist import PipelinedObsGather
+    from cf2sim.dist import NO_WATCH, NPRED_MIN, ZERO_AHEAD, PipelinedObsGather
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
@@ -196,7 +196,12 @@ def test_exchange_rejects_depth_one_and_short_lookahead():
             PipelinedObsGather(64, 34, "cpu", delta=True, unit=8, lookahead=16)
         p = PipelinedObsGather(64, 34, "cpu", delta=True, max_steps=100)
         assert p.unit == 16 and p.L == 48 and p.depth == 2 and p.kmax == 1 and p.exchange == "gloo"
-        assert p.npred == p.L + 17 and p.watch == 52
+        assert p.npred == p.L + 33 and p.watch == 52
+        # short units: the count ring still covers the native consume's zeroing of the 16 rows after
+        # its steps (cf2_xchg_register needs npred >= 33 whenever the time-out watch is on)
+        for unit in (2, 3, 4, 5):
+            q = PipelinedObsGather(64, 34, "cpu", delta=True, unit=unit, max_steps=500)
+            assert q.watch != NO_WATCH and q.npred >= NPRED_MIN == 33 and q.npred >= q.L + 2 * ZERO_AHEAD + 1
         # the batched and per-step-batch calls need the native (RCCL) exchange; local rows need start()
         with pytest.raises(RuntimeError):
             p.step(None, 0)
@@ -216,3 +221,30 @@ def test_packed_words_match_the_c_abi():
     lib = _native.load()
     for n, ol, cap in ((32768, 13, 2458), (5, 17, 3), (1000, 13, 75), (333, 17, 40), (256, 13, 256), (257, 13, 1)):
         assert lib.cf2_obs_packed_words(n, ol, cap) == packed_words(n, ol, cap), (n, ol, cap)
+
+
+def test_zero_ahead_is_the_native_consume_count():
+    """The host's count-ring window (ZERO_AHEAD) is the number of rows the native consume zeroes
+    after its steps (CONSUME_MAX in csrc/cf2sim_exchange.hip)."""
+    import re
+    from cf2sim.dist import ZERO_AHEAD
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "disturbance-crazyfile-simulation_amd", "csrc", "cf2sim_exchange.hip")).read()
+    assert int(re.search(r"constexpr uint32_t CONSUME_MAX = (\d+);", src).group(1)) == ZERO_AHEAD
+
+
+def test_capacity_above_the_crash_budget_is_all_spill_area():
+    """The quota comes from the crash budget only: raising the capacity by the predicted time-outs
+    grows the spill area by exactly that much, so they fit however they fall over the blocks (with
+    quota = cap // blocks, cap 2575 at 32 768 envs left 15 spill slots)."""
+    from cf2sim.dist import PACK_BLOCK, default_cap, pack_quota
+    for n in (4096, 32768, 40000, 131072):
+        nblk = (n + PACK_BLOCK - 1) // PACK_BLOCK
+        base = default_cap(n)
+        q = pack_quota(n, base)
+        assert q == 4
+        for extra in (1, 117, 600, n - base):
+            cap = base + extra
+            assert pack_quota(n, cap) == q
+            assert cap - nblk * q == base - nblk * q + extra
+    assert pack_quota(3000, 100) == 2 and pack_quota(333, 40) == 6 and pack_quota(5000, 10) == 0

@@ -152,11 +152,15 @@ def test_overflow_nans_exactly_the_reset_rows_that_got_no_slot(gpu):
     assert torch.equal(rows[~nan_part], exp[~nan_part]), "everything else is exact"
 
 
-def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
+STANDIN = os.path.join(ROOT, "tests", "standin_rccl", "_build", "libstandin_rccl.so")
+
+
+def _run_env(rank, world, port, out, backend, n, T, exchange="native", standin=False, fail_rank=-1):
     sys.path.insert(0, os.path.join(ROOT, "disturbance-crazyfile-simulation_amd"))
     os.environ["CF2SIM_EXCHANGE"] = "torch" if exchange == "torch" else "native"
+    os.environ["CF2_STANDIN_FAIL_RANK"] = str(fail_rank)
     import torch.distributed as dist
-    from cf2sim.dist import PipelinedObsGather, gather_rows
+    from cf2sim.dist import NO_WATCH, PipelinedObsGather, _pg_device, gather_rows
     from cf2sim.vec_env import BatchedCrazyflieEnv
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -168,8 +172,21 @@ def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
     N = world * n
     env = BatchedCrazyflieEnv(ENV_ID, n, seed=3, env_id_offset=rank * n, device=dev, max_episode_steps=41)
     obs0 = env.reset().clone()
-    # every env still flying at env-step 41 times out at once: the look-ahead sizes that step's capacity
-    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=41)
+    # every env still flying at env-step 41 times out at once: the look-ahead (33 steps: the shortest
+    # the batches of 16 allow, so the watch age 8 is inside the episode) sizes that step's capacity
+    # from the receivers' counts, the other steps run at the 7.5 % crash budget (default_cap)
+    # (the policy-in-the-loop runs crash up to ~10 % of the envs in one env-step, past the 7.5 %
+    # default budget: a 25 % budget there; the quota stays that of the default budget)
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=True, max_steps=41, lookahead=33,
+                              cap=n // 4 if exchange == "step" else None, rccl_path=STANDIN if standin else None)
+    assert pipe.watch != NO_WATCH and pipe.npred >= 33
+    caps = []
+    _after = pipe._after
+
+    def _rec(k0, nb, cap, q, copied):
+        caps.append(cap)
+        return _after(k0, nb, cap, q, copied)
+    pipe._after = _rec
     g = torch.Generator(device=dev)
     g.manual_seed(5)
     ring = torch.rand(8, N, 4, device=dev, generator=g) * 2 - 1      # every rank holds every action
@@ -258,22 +275,25 @@ def _run_env(rank, world, port, out, backend, n, T, exchange="native"):
                 bad.append(k)
     torch.cuda.synchronize()
     how = pipe.exchange
-    graphs = 0
     ovf = pipe.overflows()
     pipe.close()
+    # every rank's mismatches and overflows count (rank 0 writes the sums)
+    tot = torch.tensor([len(bad), ovf], dtype=torch.int64, device=_pg_device(None, dev))
+    dist.all_reduce(tot)
     if rank == 0:
         with open(out, "w") as f:
-            f.write(f"{len(bad)} {resets} {ovf} {how} {checked} {graphs} {bad[:3]}")
+            f.write(f"{int(tot[0])} {resets} {int(tot[1])} {how} {checked} {len(set(caps))} {bad[:3]}")
     dist.destroy_process_group()
 
 
 def _check(out, how, min_checked=200):
-    nbad, resets, ovf, got, checked, graphs = open(out).read().split()[:6]
+    nbad, resets, ovf, got, checked, ncaps = open(out).read().split()[:6]
     assert int(nbad) == 0, open(out).read()
     assert int(resets) > 0 and int(ovf) == 0
     assert got == how
     assert int(checked) >= min_checked
-    return int(graphs)
+    # the side capacity varies: the crash budget, and the predicted time-outs at the TimeLimit steps
+    assert int(ncaps) >= 2, open(out).read()
 
 
 def test_delta_exchange_one_rccl_rank(gpu, tmp_path):
@@ -383,6 +403,37 @@ def test_delta_exchange_two_gloo_ranks_on_one_gpu(gpu, tmp_path):
     out = str(tmp_path / "r.txt")
     mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 240), nprocs=2, join=True)
     _check(out, "gloo")
+
+
+def test_native_exchange_two_ranks_batched_run(gpu, tmp_path):
+    """The native exchange at world size 2 (two processes sharing the box's GPU over a gloo group;
+    the four RCCL entry points bound to the test stand-in, tests/standin_rccl): cf2_xchg_run's
+    batches -- the [world][nb][words] receive layout with a rank stride of nb * words, both ranks'
+    look-ahead counts agreeing on every step's capacity through ~6 TimeLimit periods -- give rows
+    equal to the full gather of an eagerly stepped twin's observations after every batch, with no
+    overflow, on both ranks."""
+    assert os.path.exists(STANDIN), "build the stand-in first (tests/standin_rccl: make; __graft_entry__.build())"
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 240, "run", True), nprocs=2, join=True)
+    _check(out, "native", min_checked=16)
+
+
+def test_native_exchange_two_ranks_policy_in_the_loop(gpu, tmp_path):
+    """The same two ranks through step() / flush(): the batch's env-steps issued one at a time from
+    the local rows, the exchange at each batch end and at irregular flushes; rows equal at every
+    flush on both ranks."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 240, "step", True), nprocs=2, join=True)
+    _check(out, "native", min_checked=30)
+
+
+def test_native_exchange_setup_failure_on_one_rank_falls_back_on_all(gpu, tmp_path):
+    """Rank 1's communicator setup fails: the setup agreement makes both ranks fall back together
+    (to the process group's exchange through the host) instead of leaving rank 0 in the native
+    path, and the rows stay exact."""
+    out = str(tmp_path / "r.txt")
+    mp.spawn(_run_env, args=(2, _port(), out, "gloo", 4096, 96, "native", True, 1), nprocs=2, join=True)
+    _check(out, "gloo", min_checked=96)
 
 
 def test_operands_the_kernels_would_overrun_are_rejected(gpu):
