@@ -427,14 +427,29 @@ __device__ __forceinline__ void stage_hj_grid(const double (*src)[HJ_PTS], doubl
 // state streaming from HBM and 36.3 -> 36.0 us with it cache-resident; the rollout caller, whose
 // policy reads these rows next, unchanged (bf16x3) to 1 % faster (fp32). Non-temporal loads of
 // the actions helped the streaming case and cost +2 us in the resident one, so they were not kept.
-__device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, uint32_t nvalid, uint32_t epb,
-                                               uint32_t od, uint32_t tid, uint32_t nthreads) {
+// The full-block path is unrolled: every LDS read of the thread's chunks is issued before the first
+// global store, so the chunks pay one LDS round trip instead of one each (the rolled loop waited
+// lgkmcnt(0) before every store: ~3.2k cycles of the small-N env wave for its 9 chunks, r05 timeline).
+template <uint32_t EPB, uint32_t OD, uint32_t NT>
+__device__ __forceinline__ void write_obs_rows(float* dst, const float* s_obs, uint32_t nvalid, uint32_t tid) {
     typedef float f4x __attribute__((ext_vector_type(4)));
     typedef float f2x __attribute__((ext_vector_type(2)));
-    if (nvalid == epb && (epb * od) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
+    constexpr uint32_t epb = EPB, od = OD, nthreads = NT;
+    if ((EPB * OD) % 4 == 0 && nvalid == epb && ((uintptr_t)dst & 15u) == 0) {
+        constexpr uint32_t NQ = EPB * OD / 4, IT = (NQ + NT - 1) / NT;
         const f4x* src4 = reinterpret_cast<const f4x*>(s_obs);
         f4x* dst4 = reinterpret_cast<f4x*>(dst);
-        for (uint32_t k = tid; k < epb * od / 4; k += nthreads) __builtin_nontemporal_store(src4[k], dst4 + k);
+        f4x v[IT];
+#pragma unroll
+        for (uint32_t it = 0; it < IT; ++it) {
+            const uint32_t k = tid + it * NT;
+            v[it] = src4[k < NQ ? k : NQ - 1u];
+        }
+#pragma unroll
+        for (uint32_t it = 0; it < IT; ++it) {
+            const uint32_t k = tid + it * NT;
+            if (NQ % NT == 0 || k < NQ) __builtin_nontemporal_store(v[it], dst4 + k);
+        }
     } else {
         const f2x* src2 = reinterpret_cast<const f2x*>(s_obs);
         f2x* dst2 = reinterpret_cast<f2x*>(dst);
@@ -472,23 +487,32 @@ __device__ __forceinline__ void write_obs_rows_part(float* dst, const float* s_o
     typedef float f4x __attribute__((ext_vector_type(4)));
     typedef float f2x __attribute__((ext_vector_type(2)));
     if (nvalid == 64u && (64u * OD) % 4 == 0 && ((uintptr_t)dst & 15u) == 0) {
+        // unrolled: the chunks' LDS reads all issue before the first store (one LDS round trip)
+        constexpr uint32_t NQ = 64u * OD / 4, IT = (NQ + 63u) / 64u;
         const f4x* a4 = reinterpret_cast<const f4x*>(s_obs);
         const f4x* b4 = reinterpret_cast<const f4x*>(s_rrow);
         f4x* dst4 = reinterpret_cast<f4x*>(dst);
-        for (uint32_t k = lane; k < 64u * OD / 4; k += 64u) {
-            const uint32_t r0 = 4u * k / OD, r1 = (4u * k + 3u) / OD;
-            const bool s0 = (mask >> r0) & 1ull, s1 = (mask >> r1) & 1ull;
-            if ((s0 || s1) != dirty) continue;
-            f4x v = (s0 ? b4 : a4)[k];
-            if (s0 != s1) {
-                const f4x w = (s1 ? b4 : a4)[k];
-                const uint32_t cut = r1 * OD - 4u * k;        // first component of row r1
+        f4x v[IT];
+        bool on[IT];
 #pragma unroll
-                for (uint32_t j = 1; j < 4; ++j)
-                    if (j >= cut) v[j] = w[j];
+        for (uint32_t it = 0; it < IT; ++it) {
+            const uint32_t k = lane + 64u * it, kc = k < NQ ? k : NQ - 1u;
+            const uint32_t r0 = 4u * kc / OD, r1 = (4u * kc + 3u) / OD;
+            const bool s0 = (mask >> r0) & 1ull, s1 = (mask >> r1) & 1ull;
+            on[it] = k < NQ && (s0 || s1) == dirty;
+            if (!dirty) {
+                v[it] = a4[kc];                  // clean chunks: no row of theirs reset
+            } else {
+                // a dirty chunk straddling a reset and a non-reset row is merged from both
+                const f4x x = a4[kc], y = b4[kc];
+                const uint32_t cut = r1 * OD - 4u * kc;        // first component of row r1
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) v[it][j] = (j >= cut ? s1 : s0) ? y[j] : x[j];
             }
-            __builtin_nontemporal_store(v, dst4 + k);
         }
+#pragma unroll
+        for (uint32_t it = 0; it < IT; ++it)
+            if (on[it]) __builtin_nontemporal_store(v[it], dst4 + lane + 64u * it);
     } else {
         const f2x* a2 = reinterpret_cast<const f2x*>(s_obs);
         const f2x* b2 = reinterpret_cast<const f2x*>(s_rrow);
@@ -1847,7 +1871,7 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
     } else {
         __syncthreads();         // every obs row of the block is in LDS
     }
-    write_obs_rows(io.obs + (size_t)base * OD, s_obs, P.N - base < B ? P.N - base : B, B, OD, tid, B);
+    write_obs_rows<B, OD, B>(io.obs + (size_t)base * OD, s_obs, P.N - base < B ? P.N - base : B, tid);
 }
 
 // The delta exchange's pack fused into the large-N env-step (cf2_step_packed above 32 768 envs):
@@ -2611,8 +2635,8 @@ __global__ void __launch_bounds__(STEP_BLOCK, ROLL_MIN_WAVES) rollout_kernel(KPa
         if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false>(P, io, i, E, obs_row, rs, s_hjgrid);
         rollout_resets<NOISE, DR, PHYS, B, C>(P, E, base, tid, i, do_reset, rs, &s_cnt, s_list, s_ctr, s_rand, obs_row);
         // coalesced write of the block's obs rows into step k's slab
-        write_obs_rows(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs, P.N - base < EPB ? P.N - base : EPB,
-                       EPB, OD, tid, B);
+        write_obs_rows<EPB, OD, B>(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs,
+                                   P.N - base < EPB ? P.N - base : EPB, tid);
         __syncthreads();             // the write-out read s_obs before the next step's rows
     }
     if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
@@ -2850,8 +2874,8 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
             small_roll_env_step<NOISE, DR, PHYS, SPEC>(P, io, i, lane, live, E, L, s_hjgrid);
             // this wave's 64 rows, written by this wave only: its LDS writes land before its reads
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            write_obs_rows(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs, P.N - base < 64u ? P.N - base : 64u,
-                           64u, OD, lane, 64u);
+            write_obs_rows<64u, OD, 64u>(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs,
+                                         P.N - base < 64u ? P.N - base : 64u, lane);
         }
         if (live) store_env<NOISE, DR, PHYS>(P, io0.sf, i, E, /*params_dirty=*/true);
         return;
