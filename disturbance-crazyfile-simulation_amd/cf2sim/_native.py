@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "cf2_hbm_probe", "cf2_step_packed", "cf2_obs_packed_words", "cf2_xchg_send_words", "cf2_obs_pack", "cf2_obs_consume", "cf2_obs_rows",
     "cf2_xchg_bind", "cf2_xchg_unique_id", "cf2_xchg_create", "cf2_xchg_destroy", "cf2_xchg_register",
     "cf2_xchg_publish", "cf2_xchg_wait_free", "cf2_xchg_wait", "cf2_xchg_pred_to_host", "cf2_xchg_begin", "cf2_xchg_step", "cf2_xchg_end", "cf2_xchg_env_step", "cf2_xchg_run",
+    "cf2_xchg_host_times", "cf2_xchg_copy_sync",
     "cf2_xchg_recv_words",
 )
 
@@ -118,8 +119,10 @@ def load() -> ctypes.CDLL:
     lib.cf2_xchg_begin.argtypes = [vp, u32, u32, vp]
     lib.cf2_xchg_step.argtypes = [vp] * 8
     lib.cf2_xchg_end.argtypes = [vp, ctypes.c_uint64, vp, vp]
-    lib.cf2_xchg_env_step.argtypes = [vp, vp, ctypes.c_uint64, u32, u32, vp, vp, vp, vp, vp, vp]
+    lib.cf2_xchg_env_step.argtypes = [vp, vp, ctypes.c_uint64, u32, u32, vp, vp, vp, vp, vp, vp, vp]
     lib.cf2_xchg_run.argtypes = [vp, vp, ctypes.c_uint64, u32, u32, u32, vp, u32, vp, vp, vp, vp, vp, vp]
+    lib.cf2_xchg_host_times.argtypes = [vp, vp, u32, vp, ctypes.c_int]
+    lib.cf2_xchg_copy_sync.argtypes = [vp, vp]
     for name in EXPORTED_SYMBOLS:
         if name not in ("cf2_abi_version", "cf2_config_sizeof", "cf2_status_string", "cf2_last_hip_error",
                         "cf2_policy_weights_count", "cf2_policy_packed_count", "cf2_obs_packed_words",

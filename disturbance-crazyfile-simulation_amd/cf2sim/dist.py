@@ -331,6 +331,28 @@ def obs_rows(recv, cap: int, recv_prev, cap_prev: int, world: int, n: int, ol: i
 
 
 _LIVE_XCHG = _weakref.WeakSet()     # native exchanges not closed yet: destroyed at exit, before the runtime unloads
+XCHG_MAX_COPIES = 64                 # host count buffers one native exchange tracks (cf2_xchg_copy_sync)
+
+
+class _NativeCopy:
+    """The completion of a look-ahead count copy the native exchange made into a host buffer
+    (the event the library records after it: cf2_xchg_copy_sync).  A torch event per copy plus a
+    stream wait cost ~8 us of host time per copy."""
+    __slots__ = ("lib", "x", "ptr")
+
+    def __init__(self, lib, x, ptr: int):
+        self.lib, self.x, self.ptr = lib, x, ptr
+
+    def synchronize(self):
+        from . import _native
+        _native.check(self.lib.cf2_xchg_copy_sync(self.x, self.ptr), "cf2_xchg_copy_sync")
+
+
+def _raw_stream(device) -> int:
+    """The current HIP stream of `device` as a raw handle (torch.cuda.current_stream(d).cuda_stream
+    without building a Stream object: ~0.2 instead of ~1.9 us per call)."""
+    import torch
+    return torch._C._cuda_getCurrentRawStream(device.index if device.index is not None else torch.cuda.current_device())
 
 
 def _close_live_exchanges():
@@ -470,7 +492,10 @@ class PipelinedObsGather:
         self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
         self.pred = torch.zeros(self.npred, self.world, dtype=torch.int32, device=device)
         npool = self.L // min(PRED_BATCH, self.unit) + 3
+        if npool > XCHG_MAX_COPIES:
+            raise ValueError(f"lookahead {self.L} needs {npool} count buffers, more than {XCHG_MAX_COPIES}")
         self._pred_pool = [torch.zeros(self.npred, self.world, dtype=torch.int32, pin_memory=cuda) for _ in range(npool)]
+        self._pred_ptrs = [b.data_ptr() for b in self._pred_pool]
         self._pool_i = 0
         self._copies = []                    # (last step e covered, host buffer, event or None) in issue order
         self._counts = {}                    # step -> max count over ranks (the look-ahead window)
@@ -478,6 +503,7 @@ class PipelinedObsGather:
         self._region = 0                     # publishes / batches so far (their region: % depth)
         self._start_rows = None
         self._batch = None                   # step(): [k0, nb, cap, region, steps issued] of the open batch
+        self._words = {}                     # capacity -> packed words (bookkeeping cache)
         if self.comm is not None:
             from . import _native
             self._lib = _native.load()
@@ -645,6 +671,12 @@ class PipelinedObsGather:
         self._pool_i += 1
         return b
 
+    def _next_pool_ptr(self):
+        """(buffer, its address) of the next count buffer."""
+        j = self._pool_i % len(self._pred_pool)
+        self._pool_i += 1
+        return self._pred_pool[j], self._pred_ptrs[j]
+
     def _count(self, s: int) -> int:
         """The look-ahead count of step s (max over ranks), from the first host copy made at or
         after step s (waiting for it on the host)."""
@@ -690,7 +722,10 @@ class PipelinedObsGather:
             del self._where[t]
         self._region += 1
         self.k = k0 + nb
-        self.bytes_sent += 4 * packed_words(self.n, self.ol, cap) * nb
+        w = self._words.get(cap)
+        if w is None:
+            w = self._words[cap] = packed_words(self.n, self.ol, cap)
+        self.bytes_sent += 4 * w * nb
         self.steps_sent += nb
         e = k0 + nb - 1
         if not copied and self.watch != NO_WATCH and self.k // PRED_BATCH != k0 // PRED_BATCH:
@@ -779,23 +814,36 @@ class PipelinedObsGather:
     def step_and_publish(self, env, act_ptr: int):
         """Native exchange: env-step k of `env` (this rank's shard; act_ptr its [n, 4] actions, a raw
         device pointer, not checked) with its pack fused in, then that step's exchange, in one C call
-        (cf2_xchg_env_step: what buffer() + env.step_raw(...) + publish() do).  Returns k."""
-        if self._xchg is None:
+        (cf2_xchg_env_step: what buffer() + env.step_raw(...) + publish() do; every PRED_BATCH-th
+        step it also copies the look-ahead counts to a host buffer).  The exchange runs inline on the
+        current stream: the caller wants each step's rows before the next step, so there is nothing
+        to overlap, and the fork / join events it saves are host time of the eager loop.  Returns k."""
+        x = self._xchg
+        if x is None:
             raise RuntimeError("step_and_publish needs the native exchange (RCCL, delta=True)")
         if not self.started:
             raise RuntimeError("delta exchange: call start(reset observations) first")
         if env.num_envs != self.n or env.obs_dim != self.od:
             raise ValueError("step_and_publish: the env's shard does not match the exchange's layout")
-        self.flush()
-        k, q = self.k, self._q()
+        if self._batch is not None:
+            self.flush()
+        k = self.k
+        q = self._region % self.depth
         cap = self.step_cap(k)
         rew, trunc, cost, level = env._raw_step_outputs()
-        st = self._lib.cf2_xchg_env_step(self._xchg, env._ctx, k, cap, q, act_ptr, rew, trunc, cost, level,
-                                         self._stream().cuda_stream)
+        sp = _raw_stream(self.device)
+        lib = self._lib
+        if self.watch != NO_WATCH and (k + 1) // PRED_BATCH != k // PRED_BATCH:
+            buf, ptr = self._next_pool_ptr()
+            st = lib.cf2_xchg_env_step(x, env._ctx, k, cap, q, act_ptr, rew, trunc, cost, level, ptr, sp)
+            if st == 0:
+                self._copies.append((k, buf, _NativeCopy(lib, x, ptr)))
+        else:
+            st = lib.cf2_xchg_env_step(x, env._ctx, k, cap, q, act_ptr, rew, trunc, cost, level, None, sp)
         if st != 0:
             from . import _native
             _native.check(st, "cf2_xchg_env_step")
-        self._after(k, 1, cap, q, copied=False)
+        self._after(k, 1, cap, q, copied=True)
         return k
 
     def run(self, env, act_ptrs, steps: int) -> int:
@@ -840,12 +888,9 @@ class PipelinedObsGather:
                 from . import _native
                 _native.check(st, "cf2_xchg_run")
             if w:
-                # the batch's count copy ends on the exchange stream: a side stream waits for it there
-                # and carries the event the host synchronises on when it reads the counts
-                ev = torch.cuda.Event()
-                self._lib.cf2_xchg_wait(self._xchg, self._side_stream().cuda_stream)
-                ev.record(self._side_stream())
-                self._copies.append((k0 + nb - 1, buf, ev))
+                # the batch's count copy ends on the exchange stream with an event of the library's,
+                # which the host synchronises on when it reads the counts
+                self._copies.append((k0 + nb - 1, buf, _NativeCopy(self._lib, self._xchg, buf.data_ptr())))
             self._after(k0, nb, cap, q, copied=True)
             done += nb
         cur.wait_stream(s)
@@ -900,10 +945,7 @@ class PipelinedObsGather:
         _native.check(self._lib.cf2_xchg_end(self._xchg, k0, buf.data_ptr() if w else None,
                                              torch.cuda.current_stream(self.device).cuda_stream), "cf2_xchg_end")
         if w:
-            ev = torch.cuda.Event()
-            self._lib.cf2_xchg_wait(self._xchg, self._side_stream().cuda_stream)
-            ev.record(self._side_stream())
-            self._copies.append((k0 + s - 1, buf, ev))
+            self._copies.append((k0 + s - 1, buf, _NativeCopy(self._lib, self._xchg, buf.data_ptr())))
         self._after(k0, s, cap, q, copied=True)
 
     def local_obs(self):

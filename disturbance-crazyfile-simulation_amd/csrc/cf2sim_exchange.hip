@@ -48,6 +48,8 @@
 #include <stdint.h>
 #include <string.h>
 #include <math.h>
+#include <stdlib.h>
+#include <chrono>
 #include <mutex>
 #include <vector>
 #include "../../include/cf2sim.h"
@@ -140,26 +142,34 @@ __global__ void __launch_bounds__(XB) obs_pack_kernel(const float* __restrict__ 
 // counts of the steps after these).  Every pack block whose resets got no side slot is counted
 // in overflow.
 constexpr uint32_t CONSUME_MAX = 16;
+// The steps of one consume launch, as offsets from its first packed buffer (a batch's steps sit
+// step_words apart within each rank's run, ranks rank_stride apart) and ring rows (round 5 passed
+// CONSUME_MAX pointers of each kind by value: a 456-byte argument block for a one-step consume)
 struct ConsumeSteps {
-    const uint32_t* pk[CONSUME_MAX];       // gathered packed buffers of each step
-    uint32_t words[CONSUME_MAX];           // their per-rank stride
-    uint32_t* pred[CONSUME_MAX];           // [world] look-ahead counts of each step, or null
-    uint32_t* zero[CONSUME_MAX];           // [world] rows to zero, or null
+    const uint32_t* pk0;                   // gathered packed buffer of the first step, rank 0
+    uint32_t step_words, rank_stride, steps;
+    uint32_t* ring;                        // look-ahead counts [npred][world] (null: not counted), or
+    uint32_t npred, row0;                  //   step s counts into row (row0 + s) % npred; then the
+    uint32_t nzero;                        //   nzero rows after the last step are zeroed
+    uint32_t* pred_one;                    // (ring null) the standalone consume's explicit count row
+    uint32_t* zero_one;                    //   and the one row it zeroes, or null
     uint32_t* scratch;                     // the batch's spill counters to zero (its packs are done), or null
     uint32_t scratch_words;
-    uint32_t steps;
 };
-// (the step loops are unrolled: a dynamically indexed by-value kernel argument would be copied to
-// scratch; every step's bitmap word and block-table word are loaded before the dependent chain)
+// (the step loops are unrolled: every step's bitmap word and block-table word are loaded before
+// the dependent chain)
 __global__ void __launch_bounds__(256) obs_consume_kernel(ConsumeSteps S, uint32_t world, PackLayout L,
                                                           uint16_t* __restrict__ age, uint32_t* __restrict__ overflow,
                                                           uint32_t watch_age) {
     const uint32_t tid = threadIdx.x, total = world * L.n;
     const uint32_t i = blockIdx.x * 256u + tid;
     if (blockIdx.x == 0 && tid < world) {
-#pragma unroll
-        for (uint32_t z = 0; z < CONSUME_MAX; ++z)
-            if (S.zero[z]) S.zero[z][tid] = 0u;
+        if (S.ring) {
+            const uint32_t last = S.row0 + S.steps - 1u;
+            for (uint32_t z = 0; z < S.nzero; ++z) S.ring[((last + 1u + z) % S.npred) * world + tid] = 0u;
+        } else if (S.zero_one) {
+            S.zero_one[tid] = 0u;
+        }
     }
     if (blockIdx.x == 0 && S.scratch)
         for (uint32_t k = tid; k < S.scratch_words; k += 256u) S.scratch[k] = 0u;
@@ -168,30 +178,33 @@ __global__ void __launch_bounds__(256) obs_consume_kernel(ConsumeSteps S, uint32
     const uint32_t r = ic / L.n, li = ic - r * L.n;
     const uint32_t r0 = __shfl(r, 0), r63 = __shfl(r, 63);
     const bool head = live && li % XB_PACK == 0;
+    const uint32_t* pr = S.pk0 + (size_t)r * S.rank_stride;
     uint32_t bw[CONSUME_MAX], bt[CONSUME_MAX];
 #pragma unroll
     for (uint32_t s = 0; s < CONSUME_MAX; ++s) {
         bw[s] = 0u;
         bt[s] = 0u;
         if (s < S.steps) {
-            const uint32_t* pk = S.pk[s] + (size_t)r * S.words[s];
+            const uint32_t* pk = pr + (size_t)s * S.step_words;
             bw[s] = pk[L.bits() + li / 32u];
             if (head) bt[s] = pk[L.btab() + li / XB_PACK];
         }
     }
+    const bool counting = S.ring || S.pred_one;
     uint32_t a = age[ic];
 #pragma unroll
     for (uint32_t s = 0; s < CONSUME_MAX; ++s) {
         if (s >= S.steps) break;
         const bool rs = (bw[s] >> (li % 32u)) & 1u;
         a = rs ? 0u : (a < 0xFFFFu ? a + 1u : 0xFFFFu);
-        if (S.pred[s]) {
+        if (counting) {
+            uint32_t* row = S.ring ? S.ring + ((S.row0 + s) % S.npred) * world : S.pred_one;
             const bool hit = live && a == watch_age;
             if (r0 == r63) {
                 const uint64_t m = __ballot(hit);
-                if ((tid & 63u) == 0 && m) atomicAdd(S.pred[s] + r0, (uint32_t)__popcll(m));
+                if ((tid & 63u) == 0 && m) atomicAdd(row + r0, (uint32_t)__popcll(m));
             } else if (hit) {
-                atomicAdd(S.pred[s] + r, 1u);
+                atomicAdd(row + r, 1u);
             }
         }
         if (overflow && head && bt[s] == PACK_DROPPED) atomicAdd(overflow, 1u);
@@ -346,7 +359,8 @@ extern "C" int cf2_obs_consume(const uint32_t* packed_all_dev, uint32_t world, u
     const PackLayout L{n, obs_len, cap};
     ConsumeSteps S;
     memset(&S, 0, sizeof(S));
-    S.pk[0] = packed_all_dev; S.words[0] = L.words(); S.pred[0] = pred_dev; S.zero[0] = pred_next_dev; S.steps = 1;
+    S.pk0 = packed_all_dev; S.step_words = L.words(); S.rank_stride = L.words(); S.steps = 1;
+    S.pred_one = pred_dev; S.zero_one = pred_next_dev;
     return consume_launch(S, world, L, age_dev, overflow_dev, watch_age, (hipStream_t)stream);
 }
 
@@ -394,6 +408,11 @@ struct RcclApi {
 RcclApi g_rccl;
 std::mutex g_rccl_mu;
 constexpr uint32_t XCHG_MAX_DEPTH = 8, XCHG_MAX_PRED = 1024, XCHG_MAX_BATCH = 64;
+// host-time parts: 0 a whole cf2_xchg_run / env_step call, 1 begin (region take), 2 the env-step
+// launches, 3 fork event + stream wait, 4 ncclAllGather, 5 consume launches, 6 the closing events
+// and the count copy
+constexpr int XCHG_HOST_PARTS = 7;
+constexpr uint32_t XCHG_MAX_COPIES = 64;
 }  // namespace
 
 // Buffers (cf2_xchg_register): `depth` regions, each holding the packed buffers of one batch of up
@@ -408,8 +427,16 @@ struct cf2_xchg {
     hipStream_t xs;                    // the exchange stream
     hipEvent_t fork;                   // env stream -> exchange stream
     hipEvent_t free_[XCHG_MAX_DEPTH];  // the all-gather of region q's last batch is done: q may be rewritten
-    hipEvent_t end;                    // every exchange issued so far is complete
+    hipEvent_t last;                   // the end of the latest exchange (its free_ or its count copy's event)
     bool free_rec[XCHG_MAX_DEPTH], end_rec;
+    // the count copies to host buffers: per buffer, the event after its latest copy (cf2_xchg_copy_sync)
+    uint32_t* copy_host[XCHG_MAX_COPIES];
+    hipEvent_t copy_ev[XCHG_MAX_COPIES];
+    uint32_t ncopy;
+    // inline exchanges not yet ordered before other streams: the stream they ran on
+    bool inl;
+    hipStream_t inl_stream;
+    hipEvent_t inl_ev;
     uint64_t next_region;
     // a batch opened by cf2_xchg_begin and filled by cf2_xchg_step (actions given one env-step at a time)
     bool open;
@@ -425,7 +452,24 @@ struct cf2_xchg {
     uint16_t* age;
     uint32_t* overflow;
     uint32_t* pred;                    // [npred][world]
+    // host time per part of the exchange's C calls (CF2_XCHG_HOST_TIMING=1 at create: diagnostics,
+    // cf2_xchg_host_times): ns summed over calls, then the call count
+    bool timing;
+    double host_ns[XCHG_HOST_PARTS];
+    uint64_t host_calls;
 };
+
+namespace {
+struct HostClock {      // accumulates the host time of one part of an exchange call into x->host_ns[part]
+    cf2_xchg* x;
+    int part;
+    std::chrono::steady_clock::time_point t0;
+    HostClock(cf2_xchg* x_, int part_) : x(x_), part(part_) { if (x->timing) t0 = std::chrono::steady_clock::now(); }
+    ~HostClock() {
+        if (x->timing) x->host_ns[part] += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+}  // namespace
 
 extern "C" int cf2_xchg_bind(const char* rccl_path) {
     std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -455,9 +499,11 @@ extern "C" int cf2_xchg_unique_id(uint8_t* id_out, size_t id_len) {
 
 static void xchg_free_events(cf2_xchg* x) {
     if (x->fork) (void)hipEventDestroy(x->fork);
+    if (x->inl_ev) (void)hipEventDestroy(x->inl_ev);
     for (uint32_t k = 0; k < XCHG_MAX_DEPTH; ++k)
         if (x->free_[k]) (void)hipEventDestroy(x->free_[k]);
-    if (x->end) (void)hipEventDestroy(x->end);
+    for (uint32_t k = 0; k < x->ncopy; ++k)
+        if (x->copy_ev[k]) (void)hipEventDestroy(x->copy_ev[k]);
     if (x->xs) (void)hipStreamDestroy(x->xs);
 }
 
@@ -471,6 +517,8 @@ extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world,
     *out = nullptr;
     cf2_xchg* x = new cf2_xchg();
     x->world = world; x->rank = rank; x->depth = depth;
+    const char* tv = getenv("CF2_XCHG_HOST_TIMING");
+    x->timing = tv && tv[0] == '1';
     hipError_t e = hipGetDevice(&x->device);
     // the exchange stream at the highest priority: streams of different priority get hardware
     // queues of their own, so the exchange runs beside the env-steps instead of queued behind them
@@ -480,9 +528,9 @@ extern "C" int cf2_xchg_create(const uint8_t* id, size_t id_len, uint32_t world,
     // (a low or the default priority measured the same per env-step: gpurun_out/r05o)
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->xs, hipStreamNonBlocking, hi_prio);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&x->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x->inl_ev, hipEventDisableTiming);
     for (uint32_t k = 0; e == hipSuccess && k < depth; ++k)
         e = hipEventCreateWithFlags(&x->free_[k], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&x->end, hipEventDisableTiming);
     if (e != hipSuccess) {
         xchg_free_events(x);
         delete x;
@@ -554,57 +602,115 @@ static uint32_t* xchg_scratch(const cf2_xchg* x, uint32_t q, uint32_t s) {
 
 // the receivers' work of the nb steps k0 .. of one batch in region q (capacity cap), consume
 // launches of up to CONSUME_MAX steps on the exchange stream
-static int xchg_consume(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint32_t cap) {
+static int xchg_consume(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint32_t cap, hipStream_t st_) {
     const PackLayout L{x->n, x->ol, cap};
     const uint32_t words = L.words();
     for (uint32_t s0 = 0; s0 < nb; s0 += CONSUME_MAX) {
         ConsumeSteps S;
         memset(&S, 0, sizeof(S));
         S.steps = nb - s0 < CONSUME_MAX ? nb - s0 : CONSUME_MAX;
-        for (uint32_t s = 0; s < S.steps; ++s) {
-            S.pk[s] = xchg_recv(x, q) + (size_t)(s0 + s) * words;
-            S.words[s] = nb * words;                    // rank stride of the batch's [world][nb][words] layout
-            if (x->pred) S.pred[s] = x->pred + (size_t)((k0 + s0 + s) % x->npred) * x->world;
+        S.pk0 = xchg_recv(x, q) + (size_t)s0 * words;
+        S.step_words = words;
+        S.rank_stride = nb * words;                // the batch's [world][nb][words] layout
+        if (x->pred) {
+            S.ring = x->pred;
+            S.npred = x->npred;
+            S.row0 = (uint32_t)((k0 + s0) % x->npred);
+            S.nzero = CONSUME_MAX;                 // the rows after the launch's last step
         }
         if (s0 == 0) {          // the batch's packs are done: zero its spill counters for the region's next use
             S.scratch = xchg_scratch(x, q, 0);
             S.scratch_words = nb * PACK_SCRATCH_WORDS;
         }
-        const uint64_t k1 = k0 + s0 + S.steps - 1;
-        if (x->pred)
-            for (uint32_t z = 0; z < CONSUME_MAX; ++z) S.zero[z] = x->pred + (size_t)((k1 + 1 + z) % x->npred) * x->world;
-        const int st = consume_launch(S, x->world, L, x->age, x->overflow, x->watch, x->xs);
+        const int st = consume_launch(S, x->world, L, x->age, x->overflow, x->watch, st_);
         if (st != CF2_OK) return st;
     }
     return CF2_OK;
 }
 
-// after the env stream's work so far: the all-gather of region q's batch (nb packed buffers at cap),
-// the receivers' work, the look-ahead ring to pred_host (optional), region q's free event
+// the look-ahead count ring to a host buffer on stream st, and the buffer's copy event (recorded
+// after it)
+static int xchg_copy_counts(cf2_xchg* x, uint32_t* pred_host, hipStream_t st_) {
+    uint32_t slot = 0;
+    while (slot < x->ncopy && x->copy_host[slot] != pred_host) ++slot;
+    if (slot == x->ncopy) {
+        if (x->ncopy == XCHG_MAX_COPIES) return CF2_ERR_INVALID_ARG;     // more host buffers than slots
+        const hipError_t e = hipEventCreateWithFlags(&x->copy_ev[slot], hipEventDisableTiming);
+        if (e != hipSuccess) return hip_fail(e);
+        x->copy_host[slot] = pred_host;
+        ++x->ncopy;
+    }
+    const int st = words_to_host(x->pred, pred_host, x->npred * x->world, st_);
+    if (st != CF2_OK) return st;
+    const hipError_t e = hipEventRecord(x->copy_ev[slot], st_);
+    if (e != hipSuccess) return hip_fail(e);
+    if (st_ == x->xs) x->last = x->copy_ev[slot];
+    return CF2_OK;
+}
+
+// Inline exchanges (cf2_xchg_env_step, cf2_xchg_publish) run on the caller's stream and record no
+// event; the library remembers that stream.  A caller on another stream (a region take, a wait)
+// is ordered after it through one event recorded then, on the remembered stream.
+static int xchg_after_inline(cf2_xchg* x, hipStream_t stream) {
+    if (!x->inl || x->inl_stream == stream) return CF2_OK;
+    hipError_t e = hipEventRecord(x->inl_ev, x->inl_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, x->inl_ev, 0);
+    if (e != hipSuccess) return hip_fail(e);
+    x->inl = false;           // everything inline so far is ordered before `stream` from now on
+    return CF2_OK;
+}
+
+// The exchange of region q's batch (nb packed buffers at cap) after the env stream's work so far:
+// the all-gather, the receivers' work and the look-ahead ring to pred_host (optional).  Batched
+// (inl false): on the exchange stream, forked from the env stream, closed by region q's free event,
+// so the next batch's env-steps overlap it.  Inline: on the env stream itself, for a consumer that
+// needs every step's rows before it issues the next step (nothing to overlap): no fork, no event
+// (each HIP event record or stream wait costs 2-6 us of host time; the eager step is host-bound).
 static int xchg_exchange(cf2_xchg* x, uint64_t k0, uint32_t nb, uint32_t q, uint32_t cap, hipStream_t es,
-                         uint32_t* pred_host) {
-    hipError_t e = hipEventRecord(x->fork, es);
-    if (e == hipSuccess) e = hipStreamWaitEvent(x->xs, x->fork, 0);
+                         uint32_t* pred_host, bool inl) {
+    hipError_t e = hipSuccess;
+    const hipStream_t xs = inl ? es : x->xs;
+    if (!inl) {
+        HostClock hc(x, 3);
+        e = hipEventRecord(x->fork, es);
+        if (e == hipSuccess) e = hipStreamWaitEvent(x->xs, x->fork, 0);
+    }
     if (e != hipSuccess) return hip_fail(e);
     const size_t words = PackLayout{x->n, x->ol, cap}.words();
-    if (g_rccl.all_gather(xchg_send(x, q), xchg_recv(x, q), nb * words, ncclUint32, x->comm, x->xs) != ncclSuccess)
-        return CF2_ERR_HIP;
-    int st = xchg_consume(x, k0, nb, q, cap);
+    {
+        HostClock hc(x, 4);
+        if (g_rccl.all_gather(xchg_send(x, q), xchg_recv(x, q), nb * words, ncclUint32, x->comm, xs) != ncclSuccess)
+            return CF2_ERR_HIP;
+    }
+    int st;
+    {
+        HostClock hc(x, 5);
+        st = xchg_consume(x, k0, nb, q, cap, xs);
+    }
     if (st != CF2_OK) return st;
-    e = hipEventRecord(x->free_[q], x->xs);     // the region's buffers are read and its counters zeroed
-    if (e != hipSuccess) return hip_fail(e);
+    HostClock hc(x, 6);
+    if (inl) {
+        x->free_rec[q] = false;          // its readers are ordered on es (xchg_after_inline for others)
+        x->inl = true;
+        x->inl_stream = es;
+    } else {
+        e = hipEventRecord(x->free_[q], x->xs);     // the region's buffers are read and its counters zeroed
+        if (e != hipSuccess) return hip_fail(e);
+        x->free_rec[q] = true;
+        x->last = x->free_[q];       // one event closes a batch without a count copy
+        x->end_rec = true;
+    }
     if (pred_host && x->pred) {
-        st = words_to_host(x->pred, pred_host, x->npred * x->world, x->xs);
+        st = xchg_copy_counts(x, pred_host, xs);
         if (st != CF2_OK) return st;
     }
-    e = hipEventRecord(x->end, x->xs);
-    if (e != hipSuccess) return hip_fail(e);
-    x->free_rec[q] = x->end_rec = true;
     return CF2_OK;
 }
 
 static int xchg_take_region(cf2_xchg* x, uint32_t region, hipStream_t es) {
     if (region != x->next_region % x->depth) return CF2_ERR_INVALID_ARG;     // the caller lost count
+    int st = xchg_after_inline(x, es);
+    if (st != CF2_OK) return st;
     ++x->next_region;
     if (!x->free_rec[region]) return CF2_OK;
     const hipError_t e = hipStreamWaitEvent(es, x->free_[region], 0);     // the all-gather that last read it
@@ -616,16 +722,20 @@ extern "C" int cf2_xchg_publish(cf2_xchg* x, uint64_t k, uint32_t cap, uint32_t 
         return CF2_ERR_INVALID_ARG;
     if (region != x->next_region % x->depth) return CF2_ERR_INVALID_ARG;
     const hipStream_t es = (hipStream_t)env_stream;
+    int st = xchg_after_inline(x, es);
+    if (st != CF2_OK) return st;
     ++x->next_region;
     // the caller's env-step wrote obs / done of the region (after cf2_xchg_wait_free): pack it here
-    int st = cf2_obs_pack(x->obs[region], x->done[region], x->n, x->ol, cap, xchg_send(x, region),
-                          xchg_scratch(x, region, 0), nullptr, es);
+    st = cf2_obs_pack(x->obs[region], x->done[region], x->n, x->ol, cap, xchg_send(x, region),
+                      xchg_scratch(x, region, 0), nullptr, es);
     if (st != CF2_OK) return st;
-    return xchg_exchange(x, k, 1, region, cap, es, nullptr);
+    return xchg_exchange(x, k, 1, region, cap, es, nullptr, /*inl=*/true);
 }
 
 extern "C" int cf2_xchg_wait_free(cf2_xchg* x, uint32_t region, void* stream) {
     if (!x || region >= x->depth) return CF2_ERR_INVALID_ARG;
+    const int st = xchg_after_inline(x, (hipStream_t)stream);
+    if (st != CF2_OK) return st;
     if (!x->free_rec[region]) return CF2_OK;
     const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->free_[region], 0);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
@@ -633,24 +743,41 @@ extern "C" int cf2_xchg_wait_free(cf2_xchg* x, uint32_t region, void* stream) {
 
 extern "C" int cf2_xchg_wait(cf2_xchg* x, void* stream) {
     if (!x) return CF2_ERR_INVALID_ARG;
+    const int st = xchg_after_inline(x, (hipStream_t)stream);
+    if (st != CF2_OK) return st;
     if (!x->end_rec) return CF2_OK;
-    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->end, 0);
+    const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, x->last, 0);
     return e == hipSuccess ? CF2_OK : hip_fail(e);
 }
 
 extern "C" int cf2_xchg_pred_to_host(cf2_xchg* x, uint32_t* pred_host, void* stream) {
     if (!x || !x->registered || !x->pred || !pred_host) return CF2_ERR_INVALID_ARG;
     const hipStream_t st = (hipStream_t)stream;
+    const int s2 = xchg_after_inline(x, st);
+    if (s2 != CF2_OK) return s2;
     if (x->end_rec) {
-        const hipError_t e = hipStreamWaitEvent(st, x->end, 0);
+        const hipError_t e = hipStreamWaitEvent(st, x->last, 0);
         if (e != hipSuccess) return hip_fail(e);
     }
     return words_to_host(x->pred, pred_host, x->npred * x->world, st);
 }
 
+// The host waits until the latest count copy into pred_host (cf2_xchg_run / cf2_xchg_end with that
+// buffer) is complete.  CF2_ERR_INVALID_ARG if no exchange ever copied into it.
+extern "C" int cf2_xchg_copy_sync(cf2_xchg* x, const uint32_t* pred_host) {
+    if (!x || !pred_host) return CF2_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < x->ncopy; ++k)
+        if (x->copy_host[k] == pred_host) {
+            const hipError_t e = hipEventSynchronize(x->copy_ev[k]);
+            return e == hipSuccess ? CF2_OK : hip_fail(e);
+        }
+    return CF2_ERR_INVALID_ARG;
+}
+
 extern "C" int cf2_xchg_begin(cf2_xchg* x, uint32_t cap, uint32_t region, void* env_stream) {
     if (!x || !x->registered || x->open || region >= x->depth || !layout_ok(x->n, x->ol, cap))
         return CF2_ERR_INVALID_ARG;
+    HostClock hc(x, 1);
     const int st = xchg_take_region(x, region, (hipStream_t)env_stream);
     if (st != CF2_OK) return st;
     x->open = true;
@@ -668,6 +795,7 @@ extern "C" int cf2_xchg_step(cf2_xchg* x, cf2_ctx* ctx, const float* act_dev, fl
     const uint32_t q = x->open_region, s = x->open_steps, cap = x->open_cap;
     uint32_t* pk = xchg_send(x, q) + (size_t)s * PackLayout{x->n, x->ol, cap}.words();
     uint32_t* scr = xchg_scratch(x, q, s);
+    HostClock hc(x, 2);
     int st = cf2_step_packed(ctx, act_dev, x->obs[q], rew_dev, x->done[q], trunc_dev, cost_dev, level_dev, pk, scr,
                              cap, es);
     if (st == CF2_ERR_UNSUPPORTED) {      // a shape without the fused pack: the env-step, then the pack
@@ -682,17 +810,20 @@ extern "C" int cf2_xchg_step(cf2_xchg* x, cf2_ctx* ctx, const float* act_dev, fl
 extern "C" int cf2_xchg_end(cf2_xchg* x, uint64_t k0, uint32_t* pred_host, void* env_stream) {
     if (!x || !x->open || x->open_steps == 0) return CF2_ERR_INVALID_ARG;
     x->open = false;
-    return xchg_exchange(x, k0, x->open_steps, x->open_region, x->open_cap, (hipStream_t)env_stream, pred_host);
+    return xchg_exchange(x, k0, x->open_steps, x->open_region, x->open_cap, (hipStream_t)env_stream, pred_host,
+                         /*inl=*/false);
 }
 
-extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
-                            const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev,
-                            float* cost_dev, float* level_dev, uint32_t* pred_host, void* env_stream) {
+static int xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
+                    const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
+                    float* level_dev, uint32_t* pred_host, void* env_stream, bool inl) {
     if (!x || !x->registered || x->open || !ctx || !act_dev || nact == 0 || nb == 0 || nb > x->kmax ||
         region >= x->depth || !layout_ok(x->n, x->ol, cap) || !rew_dev)
         return CF2_ERR_INVALID_ARG;
     for (uint32_t a = 0; a < nact; ++a)
         if (!act_dev[a] || ((uintptr_t)act_dev[a] & 15u)) return CF2_ERR_INVALID_ARG;
+    HostClock hc(x, 0);
+    if (x->timing) ++x->host_calls;
     int st = cf2_xchg_begin(x, cap, region, env_stream);
     if (st != CF2_OK) return st;           // nothing taken
     for (uint32_t s = 0; st == CF2_OK && s < nb; ++s)
@@ -708,12 +839,39 @@ extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb,
                                  (hipStream_t)env_stream);
         return st;
     }
-    return cf2_xchg_end(x, k0, pred_host, env_stream);
+    if (!inl) return cf2_xchg_end(x, k0, pred_host, env_stream);
+    x->open = false;
+    return xchg_exchange(x, k0, x->open_steps, x->open_region, x->open_cap, (hipStream_t)env_stream, pred_host,
+                         /*inl=*/true);
 }
 
+extern "C" int cf2_xchg_run(cf2_xchg* x, cf2_ctx* ctx, uint64_t k0, uint32_t nb, uint32_t cap, uint32_t region,
+                            const float* const* act_dev, uint32_t nact, float* rew_dev, uint8_t* trunc_dev,
+                            float* cost_dev, float* level_dev, uint32_t* pred_host, void* env_stream) {
+    return xchg_run(x, ctx, k0, nb, cap, region, act_dev, nact, rew_dev, trunc_dev, cost_dev, level_dev, pred_host,
+                    env_stream, /*inl=*/false);
+}
+
+// One env-step and its exchange, all on env_stream (inline: for a consumer that needs each step's
+// gathered rows before it issues the next step, so there is nothing to overlap); pred_host, if
+// given, receives the look-ahead counts (cf2_xchg_copy_sync)
 extern "C" int cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, uint32_t region,
                                  const float* act_dev, float* rew_dev, uint8_t* trunc_dev, float* cost_dev,
-                                 float* level_dev, void* env_stream) {
-    return cf2_xchg_run(x, ctx, k, 1, cap, region, &act_dev, 1, rew_dev, trunc_dev, cost_dev, level_dev, nullptr,
-                        env_stream);
+                                 float* level_dev, uint32_t* pred_host, void* env_stream) {
+    return xchg_run(x, ctx, k, 1, cap, region, &act_dev, 1, rew_dev, trunc_dev, cost_dev, level_dev, pred_host,
+                    env_stream, /*inl=*/true);
+}
+
+// Diagnostics: the host time of the exchange's C calls by part (XCHG_HOST_PARTS ns sums, see the
+// constant's comment) and the number of cf2_xchg_run / env_step calls they cover; all zero unless
+// CF2_XCHG_HOST_TIMING=1 was set when the exchange was created.  reset != 0 clears them.
+extern "C" int cf2_xchg_host_times(cf2_xchg* x, double* ns_out, uint32_t n_out, uint64_t* calls_out, int reset) {
+    if (!x || !ns_out || n_out < (uint32_t)XCHG_HOST_PARTS || !calls_out) return CF2_ERR_INVALID_ARG;
+    for (int p = 0; p < XCHG_HOST_PARTS; ++p) ns_out[p] = x->host_ns[p];
+    *calls_out = x->host_calls;
+    if (reset) {
+        for (int p = 0; p < XCHG_HOST_PARTS; ++p) x->host_ns[p] = 0.0;
+        x->host_calls = 0;
+    }
+    return CF2_OK;
 }

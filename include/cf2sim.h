@@ -402,11 +402,16 @@ int  cf2_obs_rows(const uint32_t* packed_all_dev, uint32_t cap, uint32_t stride,
  * stride nb * words.
  * cf2_xchg_publish(x, k, cap, region, env_stream): the exchange of env-step k, whose env-step the
  * caller issued on env_stream into obs / reset of `region` (after cf2_xchg_wait_free(x, region,
- * env_stream)); packs it on env_stream.  cf2_xchg_run: env-steps k0 .. k0 + nb - 1 of ctx (nb <=
+ * env_stream)); packs it on env_stream, and the exchange runs inline on env_stream too.
+ * cf2_xchg_run: env-steps k0 .. k0 + nb - 1 of ctx (nb <=
  * kmax; actions of step k at act_dev[k % nact]) issued back to back on env_stream with their pack
  * fused in (cf2_step_packed), then the batch's exchange at
  * capacity cap; pred_host (pinned, npred x world words, or NULL) receives the look-ahead ring after
- * the batch's consume.  cf2_xchg_env_step: cf2_xchg_run of one step.  The same batch with its
+ * the batch's consume; the batch's exchange runs on the library's exchange stream (forked from
+ * env_stream), so the next batch's env-steps overlap it.  cf2_xchg_env_step: one env-step and its
+ * exchange inline on env_stream (no fork, no event: for a consumer that needs every step's rows
+ * before it issues the next step; pred_host as for cf2_xchg_run).  Callers on other streams are
+ * ordered after inline exchanges by cf2_xchg_wait / wait_free / the next region take.  The same batch with its
  * actions given one env-step at a time (a policy in the loop, acting on each step's local rows):
  * cf2_xchg_begin(x, cap, region, env_stream) opens it (takes the region), cf2_xchg_step(x, ctx, act,
  * rew, trunc, cost, level, env_stream) issues its next env-step (up to kmax), cf2_xchg_end(x, k0,
@@ -439,7 +444,18 @@ int  cf2_xchg_step(cf2_xchg* x, cf2_ctx* ctx, const float* act_dev, float* rew_d
                    float* level_dev, void* env_stream);
 int  cf2_xchg_end(cf2_xchg* x, uint64_t k0, uint32_t* pred_host, void* env_stream);
 int  cf2_xchg_env_step(cf2_xchg* x, cf2_ctx* ctx, uint64_t k, uint32_t cap, uint32_t region, const float* act_dev,
-                       float* rew_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, void* env_stream);
+                       float* rew_dev, uint8_t* trunc_dev, float* cost_dev, float* level_dev, uint32_t* pred_host,
+                       void* env_stream);
+/* cf2_xchg_copy_sync: the host waits for the latest look-ahead count copy into pred_host (a buffer
+ * an exchange of cf2_xchg_run / cf2_xchg_end was given; up to 64 distinct buffers per exchange);
+ * CF2_ERR_INVALID_ARG for a buffer no exchange copied into. */
+int  cf2_xchg_copy_sync(cf2_xchg* x, const uint32_t* pred_host);
+/* Diagnostics (no reference counterpart): host time of the exchange's C calls by part, ns summed
+ * over the cf2_xchg_run / cf2_xchg_env_step calls counted in *calls_out -- [0] whole calls, [1] the
+ * region take, [2] env-step launches, [3] the fork to the exchange stream, [4] ncclAllGather, [5]
+ * consume launches, [6] closing events and count copy (n_out >= 7).  Recorded only when
+ * CF2_XCHG_HOST_TIMING=1 was set at cf2_xchg_create; reset != 0 clears them. */
+int  cf2_xchg_host_times(cf2_xchg* x, double* ns_out, uint32_t n_out, uint64_t* calls_out, int reset);
 
 /* Measurement support (no reference counterpart): streaming kernels over `bytes` (a multiple of
  * 16, both pointers 16-B aligned) with non-temporal accesses.  mode 0: copy src -> dst; mode 1:

@@ -74,7 +74,15 @@ def main():
         pipe.drain()
     if not args.skip_eager:
         eager(args.warmup)
-        res["eager_us"], _ = timed(eager, args.steps)
+        import ctypes
+        ns, calls = (ctypes.c_double * 7)(), ctypes.c_uint64()
+        pipe._lib.cf2_xchg_host_times(pipe._xchg, ns, 7, ctypes.byref(calls), 1)
+        res["eager_us"], res["eager_gpu_us"] = timed(eager, args.steps)
+        pipe._lib.cf2_xchg_host_times(pipe._xchg, ns, 7, ctypes.byref(calls), 1)
+        if calls.value:
+            parts = ("c_call", "region_take", "env_step_launch", "fork", "all_gather", "consume_launch", "close_events")
+            res["eager_host_us"] = {p: ns[i] / calls.value / 1e3 for i, p in enumerate(parts)}
+            res["eager_host_us"]["python_and_rest"] = res["eager_us"] - res["eager_host_us"]["c_call"]
 
     def batched(steps):
         pipe.run(env, ptrs, steps)
