@@ -357,7 +357,10 @@ def exchange_line(args, env_kw, rank, world, dev, backend, barrier_sync, max_ove
     acts = acts_g[:, off:off + n]
     act_p = [acts[r].data_ptr() for r in range(ring)]
     delta = args.gather_mode == "delta" and delta_supported(env.cfg)
-    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps))
+    # CF2SIM_RCCL_PATH: the library with RCCL's entry points the native exchange binds (default:
+    # PyTorch's RCCL; the GPU tests bind their stand-in to run this path with two ranks on one GPU)
+    pipe = PipelinedObsGather(n, env.obs_dim, dev, delta=delta, max_steps=int(env.cfg.max_episode_steps),
+                              rccl_path=os.environ.get("CF2SIM_RCCL_PATH") or None)
     native = delta and pipe.exchange == "native"
     if delta:
         pipe.start(env.obs)

@@ -70,6 +70,28 @@ def test_bench_self_launches_two_ranks(gpu):
     assert w["global_envs"] == 2 * 262144 and w["envs_per_gpu"] == 262144 and w["value"] > 0
 
 
+def test_bench_two_ranks_native_exchange_headline(gpu):
+    """The 8-GPU headline's code path at world size 2 on one GPU: bench.py --gpus 2 over gloo with the
+    native exchange bound to the tests' RCCL stand-in (CF2SIM_RCCL_PATH), so the gathered headline
+    runs PipelinedObsGather.run's batches (cf2_xchg_run: the [world][nb][words] receive layout,
+    both ranks' look-ahead counts) inside the timed region; the rows of the last step equal a full
+    all-gather and nothing overflows."""
+    standin = os.path.join(ROOT, "tests", "standin_rccl", "_build", "libstandin_rccl.so")
+    assert os.path.exists(standin)
+    # a batch of 16 packed buffers of 131 072 envs is ~120 MB per rank: the stand-in's slots are sized for it
+    env = dict(_env(), CF2_BENCH_BACKEND="gloo", CF2SIM_RCCL_PATH=standin, CF2_STANDIN_SLOT_MB="160")
+    args = [a if a != "20" else "48" for a in SHORT]          # three batches of 16 timed env-steps
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *args], env=env,
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    gi = d["gather"]
+    assert gi["exchange"] == "native" and "cf2_xchg_run" in gi["launch"], gi
+    assert d["config"]["gather_obs"] is True and d["value"] == gi["value"] > 0 and gi["global_envs"] == 262144
+    assert gi["steps"] == d["steps"] == 48 and gi["envs_per_gpu"] == 131072
+    assert gi["overflows"] == 0 and gi["rows_on_request"]["equal_to_full_gather"] is True
+
+
 def test_bench_rccl_gather_path_one_rank(gpu):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--gather-obs",
