@@ -436,6 +436,43 @@ def test_native_exchange_setup_failure_on_one_rank_falls_back_on_all(gpu, tmp_pa
     _check(out, "gloo", min_checked=96)
 
 
+def test_rows_from_a_batched_receive_layout_with_rank_stride(gpu):
+    """cf2_obs_rows on the batched receive layout [world][nb][words] built by hand (world 3, a
+    batch of 4 steps, a ragged shard of 1000 envs): rank r's pack of step j sits at
+    (r * nb + j) * words, so step j's rows read rank r at a stride of nb * words from j * words, and
+    step j - 1's likewise.  Every step of the batch, whole and in a window spanning two ranks, equals
+    the CPU restatement at the same stride bit for bit (NaN rows included: one block overflows)."""
+    from cf2sim.dist import obs_rows, pack_obs, packed_words
+    world, nb, n, ol, cap = 3, 4, 1000, 13, 75
+    od = 2 * (ol + 4)
+    words = packed_words(n, ol, cap)
+    stride = nb * words
+    g = torch.Generator().manual_seed(31)
+    recv = torch.zeros(world * nb * words, dtype=torch.int32, device=gpu)
+    for r in range(world):
+        for j in range(nb):
+            obs = torch.randn(n, od, generator=g)
+            rs = (torch.rand(n, generator=g) < 0.06).to(torch.uint8)
+            if r == 1 and j == 2:
+                rs[128:192] = 1                     # a whole block resets: its excess overflows the spill area
+            k = r * nb + j
+            pack_obs(obs.to(gpu), rs.to(gpu), cap, out=recv[k * words:(k + 1) * words])
+    torch.cuda.synchronize()
+    recv_c = recv.cpu()
+    N = world * n
+    for j in range(1, nb):
+        age = torch.randint(0, 6, (N,), generator=g, dtype=torch.int32)
+        acts = [torch.randn(N, 4, generator=g) for _ in range(3)]
+        for row0, nrows in ((0, N), (n - 7, n + 20)):
+            want = obs_rows(recv_c[j * words:], cap, recv_c[(j - 1) * words:], cap, world, n, ol, age, *acts,
+                            row0=row0, nrows=nrows, stride=stride, stride_prev=stride)
+            got = obs_rows(recv[j * words:], cap, recv[(j - 1) * words:], cap, world, n, ol,
+                           age.to(torch.int16).to(gpu), *[a.to(gpu) for a in acts],
+                           row0=row0, nrows=nrows, stride=stride, stride_prev=stride)
+            torch.testing.assert_close(got.cpu(), want, rtol=0, atol=0, equal_nan=True)
+        assert torch.isnan(want).any() or j != 2, "step 2 of rank 1 overflowed"
+
+
 def test_operands_the_kernels_would_overrun_are_rejected(gpu):
     """Host-side checks before the launch: a uint8 age vector (half the bytes the kernel indexes),
     short rows / packed buffers, or a pack whose next counters are its own raise ValueError instead
