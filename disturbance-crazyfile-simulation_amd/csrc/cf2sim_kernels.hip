@@ -1419,6 +1419,38 @@ __device__ __forceinline__ uint64_t* timing_row() {
 #define TREADY(...) do { } while (0)
 #endif
 
+// The env-step's kernel parameters that only its epilogue reads (done, reward and cost thresholds
+// and weights), re-read from the kernarg segment where they are used: every kernel that steps envs
+// takes its KParams first, so the segment starts with them.  Through the opaque pointer the loads
+// cannot be hoisted to the kernel's entry, where the compiler otherwise issues every kernarg load
+// and, with ~100 scalar registers of live values across the physics, spills them to VGPR lanes
+// (87 v_writelane / 279 v_readlane sites in the 262 144-env kernel; 81 writelane sites with these
+// and the final sensor call's parameters read late, and fewer live across the physics).  The
+// large-N step kernel only (LATEP):
+// 262 144 envs 36.3 -> 34.9-35.2 us, HJ 41.1 -> 40.2, 65 536 envs 14.7 -> 14.3; the small-N
+// kernel, whose spills are few, measured +0.3 us with it (profiles/r06_ab_late_params.txt).
+__device__ __forceinline__ KParams late_params() {
+#if defined(__HIP_DEVICE_COMPILE__)      // (the host pass of this TU has no kernarg address space)
+    typedef const __attribute__((address_space(4))) KParams* KernargParams;
+    KernargParams p = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+#else
+    return KParams{};
+#endif
+}
+
+// P with the sensor model's parameters re-read from the kernarg segment (the final sensor call of
+// the large-N step kernel: the values are the same, their registers are free during the physics)
+__device__ __forceinline__ KParams late_sensor(const KParams& P) {
+    KParams Q = P;
+    const KParams K = late_params();
+    Q.pos_std = K.pos_std; Q.pos_unif = K.pos_unif; Q.vel_std = K.vel_std; Q.rot_std = K.rot_std;
+    Q.rot_unif = K.rot_unif; Q.pgd = K.pgd; Q.sbgd = K.sbgd; Q.gyro_rw = K.gyro_rw; Q.gyro_ton = K.gyro_ton;
+    Q.lpf_gain = K.lpf_gain; Q.lpf_ratio = K.lpf_ratio;
+    return Q;
+}
+
 // One env-step of env i (aggregate_phy_steps physics sub-steps, observation, reward, done);
 // returns whether the env finished and must be auto-reset.
 // What an auto-reset consumes from the finished episode (handed to the resetting lane in LDS, so
@@ -1435,7 +1467,8 @@ enum { SEED_WORDS = 13 };
 // HD (small-N kernel, reference-default shape with sensor noise): the draws after the first
 // sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
 // env wave joins the helpers' LDS barrier before its second sub-step.
-template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0>
+template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0,
+          bool LATEP = false>
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
                                               float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
                                               const float* hd = nullptr) {
@@ -1578,11 +1611,13 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         compute_observation<NOISE>(P, E, RowRng<64>{hdw + HD_FINAL * 64, fbase}, fbase, (E.ep_step + 1) * P.agg, onx);
     } else if (pre_final) {
         const RowRng<1> gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
-        compute_observation<NOISE>(P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>(LATEP ? late_sensor(P) : P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
     } else {
-        compute_observation<NOISE>(P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>(LATEP ? late_sensor(P) : P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
     }
-    const bool term = compute_done(P, E);
+    // LATEP (the large-N step kernel): the epilogue's parameters re-read here (late_params)
+    const KParams PL = LATEP ? late_params() : P;
+    const bool term = compute_done(PL, E);
     E.ep_step += 1;
     const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
     const bool done = term || trunc;
@@ -1595,8 +1630,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     // the reset waves' stores to the same groups (skipping them cost 0.6 us there)
     if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS, ST_AUX>(P, io.sf, i, E);
     {
-        const float r = compute_reward(P, E, a, term);
-        const float cost = io.cost ? compute_cost(P, E) : 0.0f;     // info['cost'] only when asked for
+        const float r = compute_reward(PL, E, a, term);
+        const float cost = io.cost ? compute_cost(PL, E) : 0.0f;    // info['cost'] only when asked for
         io.rew[i] = r;
         io.done[i] = (uint8_t)done;
         if (io.trunc) io.trunc[i] = (uint8_t)trunc;
@@ -1628,7 +1663,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     return do_reset;
 }
 
-template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0>
+template <bool NOISE, bool DR, int PHYS, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0,
+          bool LATEP = false>
 __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uint32_t i, float* __restrict__ obs_row,
                                          ResetSeed& rs, const double* hj_grid, const float* hd = nullptr) {
     Env E;
@@ -1636,7 +1672,7 @@ __device__ __forceinline__ bool step_env(const KParams& P, const StepIO& io, uin
     // so a load issued after the state stores would wait for the whole store burst to drain (the
     // history is loaded after the physics sub-steps, still ahead of store_core, in step_env_body)
     load_env<NOISE, DR, PHYS>(P, io.sf, i, E, P.need_level || io.level != nullptr, /*with_hist=*/false);
-    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD, ST_AUX>(P, io, i, E, obs_row, rs, hj_grid, hd);
+    return step_env_body<NOISE, DR, PHYS, true, SKIP_RESETTING, HD, ST_AUX, LATEP>(P, io, i, E, obs_row, rs, hj_grid, hd);
 }
 
 // Reset one env in place: reads only what a reset consumes from the finished episode (the
@@ -1967,7 +2003,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) step_kernel(KParam
     ResetSeed rs;
     __shared__ double s_hjgrid[6 * HJ_PTS];
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
-    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
+    if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX, true>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
     block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
     if (X.pk) pack_epilogue_block<NOISE ? 13u : 17u, (uint32_t)OD, B>(X, P.N, base, tid, do_reset, s_obs);
 #ifdef CF2_TIMING
