@@ -1183,6 +1183,27 @@ __device__ __forceinline__ float downwash(const KParams& P, const float p[3], ui
     return F;
 }
 
+// The env-step's kernel parameters that only its epilogue reads (done, reward and cost thresholds
+// and weights), re-read from the kernarg segment where they are used: every kernel that steps envs
+// takes its KParams first, so the segment starts with them.  Through the opaque pointer the loads
+// cannot be hoisted to the kernel's entry, where the compiler otherwise issues every kernarg load
+// and, with ~100 scalar registers of live values across the physics, spills them to VGPR lanes
+// (87 v_writelane / 279 v_readlane sites in the 262 144-env kernel).  The large-N step kernel
+// re-reads the epilogue's and the final sensor call's parameters (LATEP) and the auto-reset's
+// reset-only ones (reset_src<2>): 24 writelane sites left, 262 144 envs 36.3 -> 33.9 us, HJ
+// 41.1 -> 39.6, 65 536 envs 14.7 -> 13.9 (profiles/r06_ab_late_params.txt); the small-N kernel,
+// whose spills are few, measured +0.3 us with the epilogue part.
+__device__ __forceinline__ KParams late_params() {
+#if defined(__HIP_DEVICE_COMPILE__)      // (the host pass of this TU has no kernarg address space)
+    typedef const __attribute__((address_space(4))) KParams* KernargParams;
+    KernargParams p = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+#else
+    return KParams{};
+#endif
+}
+
 // ------------------------------------------------------------------------------------
 // reset (base.py:420-464 + task_specific_reset + apply_domain_randomization)
 // ------------------------------------------------------------------------------------
@@ -1193,16 +1214,18 @@ __device__ __forceinline__ float downwash(const KParams& P, const float p[3], ui
 //   reset_params      domain randomisation (base.py:241-298), const-wind draw, Boltzmann level;
 //   reset_observe     the two reset sensor calls (base.py:444-456 incl. the stale-rpy_dot LPF
 //                     seed) and the history / observation row.
-// where the reset-only parameters are read: TAB = the device tables (P.tab; the fused rollout,
-// whose register budget cannot hold them from kernel entry), else the kernarg block (the step
-// kernel: its reset tail would wait on the scalar loads)
-template <bool TAB>
+// where the reset-only parameters are read: TAB 1 = the device tables (P.tab; the fused rollout,
+// whose register budget cannot hold them from kernel entry), 2 = the kernarg block re-read at the
+// reset (late_params: the large-N step kernel, where holding them from kernel entry spilled them
+// to VGPR lanes), else the kernarg block as loaded at kernel entry
+template <int TAB>
 __device__ __forceinline__ decltype(auto) reset_src(const KParams& P) {
-    if constexpr (TAB) return (*P.tab);
+    if constexpr (TAB == 1) return (*P.tab);
+    else if constexpr (TAB == 2) return late_params();
     else return (P);
 }
 
-template <int PHYS, bool TAB = false, class G>
+template <int PHYS, int TAB = 0, class G>
 __device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const G& g, uint32_t gid) {
     const U4 b0 = g.block(0), b1 = g.block(1), b2 = g.block(2), b3 = g.block(3);
     const uint32_t u[16] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w,
@@ -1273,7 +1296,7 @@ __device__ __forceinline__ void reset_kinematics(const KParams& P, Env& E, const
     }
 }
 
-template <bool DR, bool TAB = false, class G>
+template <bool DR, int TAB = 0, class G>
 __device__ __forceinline__ void reset_params(const KParams& P, Env& E, const G& g) {
     E.dt = P.time_step; E.m = P.mass; E.J[0] = P.ixx; E.J[1] = P.iyy; E.J[2] = P.izz;
     E.k0 = P.ft0; E.k1 = P.ft1;
@@ -1362,7 +1385,7 @@ __device__ __forceinline__ void reset_observe(const KParams& P, Env& E, const G&
     compute_history<NOISE>(P, E, o1, out);
 }
 
-template <bool NOISE, bool DR, int PHYS, bool TAB = false, class G>
+template <bool NOISE, bool DR, int PHYS, int TAB = 0, class G>
 __device__ __forceinline__ void reset_env(const KParams& P, Env& E, const G& g, uint32_t gid, float* out) {
     const float stale[3] = {E.wb[0], E.wb[1], E.wb[2]};
     reset_kinematics<PHYS, TAB>(P, E, g, gid);
@@ -1418,27 +1441,6 @@ __device__ __forceinline__ uint64_t* timing_row() {
 #define TSTAMP(k) do { } while (0)
 #define TREADY(...) do { } while (0)
 #endif
-
-// The env-step's kernel parameters that only its epilogue reads (done, reward and cost thresholds
-// and weights), re-read from the kernarg segment where they are used: every kernel that steps envs
-// takes its KParams first, so the segment starts with them.  Through the opaque pointer the loads
-// cannot be hoisted to the kernel's entry, where the compiler otherwise issues every kernarg load
-// and, with ~100 scalar registers of live values across the physics, spills them to VGPR lanes
-// (87 v_writelane / 279 v_readlane sites in the 262 144-env kernel; 81 writelane sites with these
-// and the final sensor call's parameters read late, and fewer live across the physics).  The
-// large-N step kernel only (LATEP):
-// 262 144 envs 36.3 -> 34.9-35.2 us, HJ 41.1 -> 40.2, 65 536 envs 14.7 -> 14.3; the small-N
-// kernel, whose spills are few, measured +0.3 us with it (profiles/r06_ab_late_params.txt).
-__device__ __forceinline__ KParams late_params() {
-#if defined(__HIP_DEVICE_COMPILE__)      // (the host pass of this TU has no kernarg address space)
-    typedef const __attribute__((address_space(4))) KParams* KernargParams;
-    KernargParams p = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(p));
-    return *p;
-#else
-    return KParams{};
-#endif
-}
 
 // P with the sensor model's parameters re-read from the kernarg segment (the final sensor call of
 // the large-N step kernel: the values are the same, their registers are free during the physics)
@@ -1766,7 +1768,7 @@ __device__ __forceinline__ void store_reset_params(const KParams& P, const Tile&
 //   3: domain randomisation, disturbance, level -> store_reset_params
 // Roles 1 and 2 recompute the reset pose from the same table entries, so the critical path is one
 // pose + one sensor call instead of the whole reset.
-template <bool NOISE, bool DR, int PHYS>
+template <bool NOISE, bool DR, int PHYS, int TAB = 0>
 __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__ sf, uint32_t i, const ResetSeed& rs,
                                            const TableRng& g, float* __restrict__ obs_row, uint32_t role) {
     constexpr int OL = NOISE ? 13 : 17;
@@ -1780,11 +1782,11 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
     if (role == 3) {
         E.level = rs.level;
         E.level_idx = rs.level_idx;
-        reset_params<DR>(P, E, g);
+        reset_params<DR, TAB>(P, E, g);
         store_reset_params<DR>(P, T, E);
         return;
     }
-    reset_kinematics<PHYS>(P, E, g, gid);
+    reset_kinematics<PHYS, TAB>(P, E, g, gid);
     TREADY("v"(E.q[3]), "v"(E.w[0]));
     TSTAMP(7);   // reset pose computed
     if (role == 0) {
@@ -1810,7 +1812,7 @@ __device__ __forceinline__ void reset_role(const KParams& P, float* __restrict__
 // End of a block's env-step: list the finished envs (wave ballots into per-wave lists), reset
 // them block-cooperatively (see step_kernel) and write the block's obs rows out coalesced.  Every
 // thread of the block calls it.
-template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C>
+template <bool NOISE, bool DR, int PHYS, uint32_t B, uint32_t C, int TAB = 0>
 __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& io, uint32_t base, uint32_t tid,
                                                bool do_reset, const ResetSeed& rs, float* s_obs, uint32_t* s_list,
                                                uint32_t* s_rand, uint32_t* s_wcnt) {
@@ -1899,7 +1901,7 @@ __device__ __forceinline__ void block_epilogue(const KParams& P, const StepIO& i
             // with the block index so the co-resident blocks' roles spread over the SIMDs
             if (act) {
                 const TableRng tg{s_rand + rl, C};
-                reset_role<NOISE, DR, PHYS>(P, io.sf, base + t, q, tg, s_obs + t * OD, role);
+                reset_role<NOISE, DR, PHYS, TAB>(P, io.sf, base + t, q, tg, s_obs + t * OD, role);
             }
             __syncthreads();     // the next chunk reuses s_rand
         }
@@ -2004,7 +2006,7 @@ __global__ void __launch_bounds__(STEP_BLOCK, STEP_MIN_WAVES) step_kernel(KParam
     __shared__ double s_hjgrid[6 * HJ_PTS];
     if (P.dstb_mode == DSTB_HJ_T) stage_hj_grid(P.tab->hj_grid, s_hjgrid);     // uniform branch
     if (i < P.N) do_reset = step_env<NOISE, DR, PHYS, false, false, ST_AUX, true>(P, io, i, s_obs + tid * OD, rs, s_hjgrid);
-    block_epilogue<NOISE, DR, PHYS, B, C>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
+    block_epilogue<NOISE, DR, PHYS, B, C, 2>(P, io, base, tid, do_reset, rs, s_obs, s_list, s_rand, s_wcnt);
     if (X.pk) pack_epilogue_block<NOISE ? 13u : 17u, (uint32_t)OD, B>(X, P.N, base, tid, do_reset, s_obs);
 #ifdef CF2_TIMING
     TSTAMP(5);   // resets done
