@@ -1193,15 +1193,39 @@ __device__ __forceinline__ float downwash(const KParams& P, const float p[3], ui
 // reset-only ones (reset_src<2>): 24 writelane sites left, 262 144 envs 36.3 -> 33.9 us, HJ
 // 41.1 -> 39.6, 65 536 envs 14.7 -> 13.9 (profiles/r06_ab_late_params.txt); the small-N kernel,
 // whose spills are few, measured +0.3 us with the epilogue part.
-__device__ __forceinline__ KParams late_params() {
-#if defined(__HIP_DEVICE_COMPILE__)      // (the host pass of this TU has no kernarg address space)
-    typedef const __attribute__((address_space(4))) KParams* KernargParams;
+typedef const __attribute__((address_space(4))) KParams* KernargParams;
+__device__ __forceinline__ KernargParams kernarg_params() {
     KernargParams p = (KernargParams)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(p));
-    return *p;
-#else
-    return KParams{};
-#endif
+    return p;
+}
+// P with the epilogue's fields re-read (done, reward, cost; the others as in P)
+__device__ __forceinline__ KParams late_epilogue(const KParams& P) {
+    KParams Q = P;
+    const KernargParams k = kernarg_params();
+    Q.pen_action = k->pen_action; Q.pen_angle = k->pen_angle; Q.pen_spin = k->pen_spin; Q.pen_term = k->pen_term;
+    Q.pen_vel = k->pen_vel; Q.pen_z = k->pen_z; Q.pen_arp = k->pen_arp; Q.pen_dist = k->pen_dist;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        Q.target_pos[j] = k->target_pos[j]; Q.target_rpy[j] = k->target_rpy[j]; Q.target_rate[j] = k->target_rate[j];
+    }
+    Q.done_rp = k->done_rp; Q.done_rate_deg = k->done_rate_deg; Q.done_zmin = k->done_zmin;
+    Q.cost_xy = k->cost_xy; Q.cost_z = k->cost_z; Q.cost_rp = k->cost_rp; Q.cost_vel = k->cost_vel;
+    Q.cost_rate = k->cost_rate;
+    return Q;
+}
+// P with the reset-only fields re-read (reset_src<2>)
+__device__ __forceinline__ KParams late_reset(const KParams& P) {
+    KParams Q = P;
+    const KernargParams k = kernarg_params();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Q.init_xyz[j] = k->init_xyz[j];
+    Q.pos_lim = k->pos_lim; Q.angle_lim = k->angle_lim; Q.yaw_lim = k->yaw_lim; Q.vel_lim = k->vel_lim;
+    Q.rate_lim = k->rate_lim; Q.yaw_rate_lim = k->yaw_rate_lim; Q.action_std = k->action_std;
+    Q.motor_std = k->motor_std; Q.hover_x = k->hover_x; Q.hover_action = k->hover_action;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) { Q.dr_lo[j] = k->dr_lo[j]; Q.dr_hi[j] = k->dr_hi[j]; }
+    return Q;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1216,12 +1240,12 @@ __device__ __forceinline__ KParams late_params() {
 //                     seed) and the history / observation row.
 // where the reset-only parameters are read: TAB 1 = the device tables (P.tab; the fused rollout,
 // whose register budget cannot hold them from kernel entry), 2 = the kernarg block re-read at the
-// reset (late_params: the large-N step kernel, where holding them from kernel entry spilled them
+// reset (late_reset: the large-N step kernel, where holding them from kernel entry spilled them
 // to VGPR lanes), else the kernarg block as loaded at kernel entry
 template <int TAB>
 __device__ __forceinline__ decltype(auto) reset_src(const KParams& P) {
     if constexpr (TAB == 1) return (*P.tab);
-    else if constexpr (TAB == 2) return late_params();
+    else if constexpr (TAB == 2) return late_reset(P);
     else return (P);
 }
 
@@ -1446,10 +1470,10 @@ __device__ __forceinline__ uint64_t* timing_row() {
 // the large-N step kernel: the values are the same, their registers are free during the physics)
 __device__ __forceinline__ KParams late_sensor(const KParams& P) {
     KParams Q = P;
-    const KParams K = late_params();
-    Q.pos_std = K.pos_std; Q.pos_unif = K.pos_unif; Q.vel_std = K.vel_std; Q.rot_std = K.rot_std;
-    Q.rot_unif = K.rot_unif; Q.pgd = K.pgd; Q.sbgd = K.sbgd; Q.gyro_rw = K.gyro_rw; Q.gyro_ton = K.gyro_ton;
-    Q.lpf_gain = K.lpf_gain; Q.lpf_ratio = K.lpf_ratio;
+    const KernargParams k = kernarg_params();
+    Q.pos_std = k->pos_std; Q.pos_unif = k->pos_unif; Q.vel_std = k->vel_std; Q.rot_std = k->rot_std;
+    Q.rot_unif = k->rot_unif; Q.pgd = k->pgd; Q.sbgd = k->sbgd; Q.gyro_rw = k->gyro_rw; Q.gyro_ton = k->gyro_ton;
+    Q.lpf_gain = k->lpf_gain; Q.lpf_ratio = k->lpf_ratio;
     return Q;
 }
 
@@ -1617,8 +1641,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     } else {
         compute_observation<NOISE>(LATEP ? late_sensor(P) : P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
     }
-    // LATEP (the large-N step kernel): the epilogue's parameters re-read here (late_params)
-    const KParams PL = LATEP ? late_params() : P;
+    // LATEP (the large-N step kernel): the epilogue's parameters re-read here (late_epilogue)
+    const KParams PL = LATEP ? late_epilogue(P) : P;
     const bool term = compute_done(PL, E);
     E.ep_step += 1;
     const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
