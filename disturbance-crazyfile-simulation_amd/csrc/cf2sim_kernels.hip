@@ -1214,6 +1214,18 @@ __device__ __forceinline__ KParams late_epilogue(const KParams& P) {
     Q.cost_rate = k->cost_rate;
     return Q;
 }
+// io with the per-env output pointers re-read (StepIO is the second kernel argument of every
+// kernel that passes LATEP: step_kernel, collect_kernel)
+typedef const __attribute__((address_space(4))) StepIO* KernargIO;
+__device__ __forceinline__ StepIO late_outputs(const StepIO& io) {
+    constexpr size_t off = (sizeof(KParams) + alignof(StepIO) - 1) / alignof(StepIO) * alignof(StepIO);
+    KernargIO k = (KernargIO)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + off);
+    asm volatile("" : "+s"(k));
+    StepIO o = io;
+    o.rew = k->rew; o.done = k->done; o.trunc = k->trunc; o.cost = k->cost; o.level = k->level;
+    o.final_obs = k->final_obs;
+    return o;
+}
 // P with the reset-only fields re-read (reset_src<2>)
 __device__ __forceinline__ KParams late_reset(const KParams& P) {
     KParams Q = P;
@@ -1655,14 +1667,15 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     // resets follow __syncthreads, whose workgroup-scope release/acquire orders these stores before
     // the reset waves' stores to the same groups (skipping them cost 0.6 us there)
     if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS, ST_AUX>(P, io.sf, i, E);
+    const StepIO IL = LATEP ? late_outputs(io) : io;
     {
         const float r = compute_reward(PL, E, a, term);
-        const float cost = io.cost ? compute_cost(PL, E) : 0.0f;    // info['cost'] only when asked for
-        io.rew[i] = r;
-        io.done[i] = (uint8_t)done;
-        if (io.trunc) io.trunc[i] = (uint8_t)trunc;
-        if (io.cost) io.cost[i] = cost;
-        if (io.level) io.level[i] = level_used;
+        const float cost = IL.cost ? compute_cost(PL, E) : 0.0f;    // info['cost'] only when asked for
+        IL.rew[i] = r;
+        IL.done[i] = (uint8_t)done;
+        if (IL.trunc) IL.trunc[i] = (uint8_t)trunc;
+        if (IL.cost) IL.cost[i] = cost;
+        if (IL.level) IL.level[i] = level_used;
     }
     {
         float o[OD];
@@ -1672,7 +1685,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
 #pragma unroll
         for (int k = 0; k < OD; k += 2)
             *reinterpret_cast<float2*>(obs_row + k) = make_float2(o[k], o[k + 1]);
-        if (do_reset && io.final_obs) write_obs<NOISE>(io.final_obs, i, o);
+        if (do_reset && IL.final_obs) write_obs<NOISE>(IL.final_obs, i, o);
     }
     if (do_reset) {
 #pragma unroll
