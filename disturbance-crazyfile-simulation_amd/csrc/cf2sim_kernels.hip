@@ -1226,6 +1226,29 @@ __device__ __forceinline__ StepIO late_outputs(const StepIO& io) {
     o.final_obs = k->final_obs;
     return o;
 }
+// every pointer of io re-read (the fused rollout derives each env-step's output slabs from them)
+__device__ __forceinline__ StepIO late_io(const StepIO& io) {
+    constexpr size_t off = (sizeof(KParams) + alignof(StepIO) - 1) / alignof(StepIO) * alignof(StepIO);
+    KernargIO k = (KernargIO)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + off);
+    asm volatile("" : "+s"(k));
+    StepIO o = io;
+    o.sf = k->sf; o.act = k->act; o.dstb = k->dstb; o.obs = k->obs; o.rew = k->rew; o.done = k->done;
+    o.trunc = k->trunc; o.cost = k->cost; o.level = k->level; o.final_obs = k->final_obs;
+    return o;
+}
+// P with the physics sub-step's constants re-read (the fused rollout, LATEX: its K-step loop kept
+// them live across the whole loop body, spilled with the rest)
+__device__ __forceinline__ KParams late_physics(const KParams& P) {
+    KParams Q = P;
+    const KernargParams k = kernarg_params();
+    Q.time_step = k->time_step; Q.mass = k->mass; Q.ixx = k->ixx; Q.iyy = k->iyy; Q.izz = k->izz;
+    Q.ft0 = k->ft0; Q.ft1 = k->ft1; Q.K = k->K; Q.B = k->B; Q.ou_sigma = k->ou_sigma;
+    Q.drag_xy = k->drag_xy; Q.drag_z = k->drag_z; Q.g_world = k->g_world; Q.arm = k->arm;
+    Q.prop_xy = k->prop_xy; Q.prop_z = k->prop_z; Q.prop_mass = k->prop_mass; Q.prop_inertia = k->prop_inertia;
+    Q.prop_speed_gain = k->prop_speed_gain; Q.lin_damping = k->lin_damping; Q.ang_damping = k->ang_damping;
+    Q.vmax = k->vmax;
+    return Q;
+}
 // P with the reset-only fields re-read (reset_src<2>)
 __device__ __forceinline__ KParams late_reset(const KParams& P) {
     KParams Q = P;
@@ -1506,7 +1529,10 @@ enum { SEED_WORDS = 13 };
 // sub-step come from the helper waves' LDS table (hd = its column of this env, HD_* layout); the
 // env wave joins the helpers' LDS barrier before its second sub-step.
 template <bool NOISE, bool DR, int PHYS, bool STORE, bool SKIP_RESETTING = false, bool HD = false, int ST_AUX = 0,
-          bool LATEP = false>
+          bool LATEP = false, bool LATEX = false>
+// LATEP: the epilogue's, the final sensor call's parameters and the output pointers re-read where
+// used (step_kernel, collect_kernel); LATEX: the epilogue's, the sensor call's and the physics
+// sub-steps' parameters (the fused rollout, whose output pointers change per env-step)
 __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io, uint32_t i, Env& E,
                                               float* __restrict__ obs_row, ResetSeed& rs, const double* hj_grid,
                                               const float* hd = nullptr) {
@@ -1620,8 +1646,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         float dw = 0.0f;
         if (PHYS == PHYS_BULLET_T && P.num_drones > 1 && P.downwash_on)
             dw = downwash(P, E.p, gid % (uint32_t)P.num_drones);   // mates' positions before this sub-step
-        if (PHYS == PHYS_BULLET_T) bullet_substep(P, E, a, d, on, E.ep_step == 0 && s == 0 && !E.props_on, dw);
-        else simple_substep(P, E, a, on);
+        if (PHYS == PHYS_BULLET_T) bullet_substep(LATEX ? late_physics(P) : P, E, a, d, on, E.ep_step == 0 && s == 0 && !E.props_on, dw);
+        else simple_substep(LATEX ? late_physics(P) : P, E, a, on);
         float dummy[17];
         // a sub-step's held measurement reaches an observation only if the final measurement
         // of the env-step is not a full one (aggregate_phy_steps % obs_rate != 0)
@@ -1649,12 +1675,12 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         compute_observation<NOISE>(P, E, RowRng<64>{hdw + HD_FINAL * 64, fbase}, fbase, (E.ep_step + 1) * P.agg, onx);
     } else if (pre_final) {
         const RowRng<1> gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
-        compute_observation<NOISE>(LATEP ? late_sensor(P) : P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>((LATEP || LATEX) ? late_sensor(P) : P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
     } else {
-        compute_observation<NOISE>(LATEP ? late_sensor(P) : P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>((LATEP || LATEX) ? late_sensor(P) : P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
     }
     // LATEP (the large-N step kernel): the epilogue's parameters re-read here (late_epilogue)
-    const KParams PL = LATEP ? late_epilogue(P) : P;
+    const KParams PL = (LATEP || LATEX) ? late_epilogue(P) : P;
     const bool term = compute_done(PL, E);
     E.ep_step += 1;
     const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
@@ -2698,17 +2724,18 @@ __global__ void __launch_bounds__(STEP_BLOCK, ROLL_MIN_WAVES) rollout_kernel(KPa
     float* obs_row = s_obs + tid * OD;
     for (uint32_t k = 0; k < K; ++k) {
         if (tid == 0) s_cnt = 0;     // every reader of the previous step passed its last barrier
-        StepIO io = io0;
-        io.act = io0.act + (size_t)k * act_stride;
-        io.rew = io0.rew + (size_t)k * n;
-        io.done = io0.done + (size_t)k * n;
-        if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
-        if (io0.cost) io.cost = io0.cost + (size_t)k * n;
-        if (io0.level) io.level = io0.level + (size_t)k * n;
-        if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+        const StepIO I0 = late_io(io0);
+        StepIO io = I0;
+        io.act = I0.act + (size_t)k * act_stride;
+        io.rew = I0.rew + (size_t)k * n;
+        io.done = I0.done + (size_t)k * n;
+        if (I0.trunc) io.trunc = I0.trunc + (size_t)k * n;
+        if (I0.cost) io.cost = I0.cost + (size_t)k * n;
+        if (I0.level) io.level = I0.level + (size_t)k * n;
+        if (I0.final_obs) io.final_obs = I0.final_obs + (size_t)k * n * OD;
         bool do_reset = false;
         ResetSeed rs;
-        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false>(P, io, i, E, obs_row, rs, s_hjgrid);
+        if (live) do_reset = step_env_body<NOISE, DR, PHYS, false, false, false, 0, false, true>(P, io, i, E, obs_row, rs, s_hjgrid);
         rollout_resets<NOISE, DR, PHYS, B, C>(P, E, base, tid, i, do_reset, rs, &s_cnt, s_list, s_ctr, s_rand, obs_row);
         // coalesced write of the block's obs rows into step k's slab
         write_obs_rows<EPB, OD, B>(io0.obs + (size_t)k * n * OD + (size_t)base * OD, s_obs,
