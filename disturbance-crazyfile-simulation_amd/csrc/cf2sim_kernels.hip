@@ -1512,6 +1512,20 @@ __device__ __forceinline__ KParams late_sensor(const KParams& P) {
     return Q;
 }
 
+// the late_* copies when L, else the argument itself (no copy of the 624-byte block: a
+// conditional expression would materialise one, and that changed the small-N kernel's code)
+template <bool L> __device__ __forceinline__ decltype(auto) late_epilogue_if(const KParams& P) {
+    if constexpr (L) return late_epilogue(P); else return (P);
+}
+template <bool L> __device__ __forceinline__ decltype(auto) late_sensor_if(const KParams& P) {
+    if constexpr (L) return late_sensor(P); else return (P);
+}
+template <bool L> __device__ __forceinline__ decltype(auto) late_physics_if(const KParams& P) {
+    if constexpr (L) return late_physics(P); else return (P);
+}
+template <bool L> __device__ __forceinline__ decltype(auto) late_outputs_if(const StepIO& io) {
+    if constexpr (L) return late_outputs(io); else return (io);
+}
 // One env-step of env i (aggregate_phy_steps physics sub-steps, observation, reward, done);
 // returns whether the env finished and must be auto-reset.
 // What an auto-reset consumes from the finished episode (handed to the resetting lane in LDS, so
@@ -1646,8 +1660,8 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         float dw = 0.0f;
         if (PHYS == PHYS_BULLET_T && P.num_drones > 1 && P.downwash_on)
             dw = downwash(P, E.p, gid % (uint32_t)P.num_drones);   // mates' positions before this sub-step
-        if (PHYS == PHYS_BULLET_T) bullet_substep(LATEX ? late_physics(P) : P, E, a, d, on, E.ep_step == 0 && s == 0 && !E.props_on, dw);
-        else simple_substep(LATEX ? late_physics(P) : P, E, a, on);
+        if (PHYS == PHYS_BULLET_T) bullet_substep(late_physics_if<LATEX>(P), E, a, d, on, E.ep_step == 0 && s == 0 && !E.props_on, dw);
+        else simple_substep(late_physics_if<LATEX>(P), E, a, on);
         float dummy[17];
         // a sub-step's held measurement reaches an observation only if the final measurement
         // of the env-step is not a full one (aggregate_phy_steps % obs_rate != 0)
@@ -1675,12 +1689,12 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
         compute_observation<NOISE>(P, E, RowRng<64>{hdw + HD_FINAL * 64, fbase}, fbase, (E.ep_step + 1) * P.agg, onx);
     } else if (pre_final) {
         const RowRng<1> gr{reinterpret_cast<const uint32_t*>(obs_row), fbase};
-        compute_observation<NOISE>((LATEP || LATEX) ? late_sensor(P) : P, E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>(late_sensor_if<LATEP || LATEX>(P), E, gr, fbase, (E.ep_step + 1) * P.agg, onx);
     } else {
-        compute_observation<NOISE>((LATEP || LATEX) ? late_sensor(P) : P, E, g, fbase, (E.ep_step + 1) * P.agg, onx);
+        compute_observation<NOISE>(late_sensor_if<LATEP || LATEX>(P), E, g, fbase, (E.ep_step + 1) * P.agg, onx);
     }
     // LATEP (the large-N step kernel): the epilogue's parameters re-read here (late_epilogue)
-    const KParams PL = (LATEP || LATEX) ? late_epilogue(P) : P;
+    const auto& PL = late_epilogue_if<LATEP || LATEX>(P);
     const bool term = compute_done(PL, E);
     E.ep_step += 1;
     const bool trunc = P.max_steps > 0 && E.ep_step >= P.max_steps && !term;
@@ -1693,7 +1707,7 @@ __device__ __forceinline__ bool step_env_body(const KParams& P, const StepIO& io
     // resets follow __syncthreads, whose workgroup-scope release/acquire orders these stores before
     // the reset waves' stores to the same groups (skipping them cost 0.6 us there)
     if (STORE && !(SKIP_RESETTING && do_reset)) store_core<NOISE, DR, PHYS, ST_AUX>(P, io.sf, i, E);
-    const StepIO IL = LATEP ? late_outputs(io) : io;
+    const auto& IL = late_outputs_if<LATEP>(io);
     {
         const float r = compute_reward(PL, E, a, term);
         const float cost = IL.cost ? compute_cost(PL, E) : 0.0f;    // info['cost'] only when asked for
