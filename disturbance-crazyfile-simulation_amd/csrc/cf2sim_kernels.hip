@@ -2802,7 +2802,8 @@ __device__ __forceinline__ void small_roll_env_step(const KParams& P, const Step
     bool do_reset = false;
     ResetSeed rs;
     if (live)
-        do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD>(P, io, i, E, obs_row, rs, s_hjgrid, L.draw + lane);
+        do_reset = step_env_body<NOISE, DR, PHYS, false, false, HD, 0, false, true>(P, io, i, E, obs_row, rs, s_hjgrid,
+                                                                                    L.draw + lane);
     const uint64_t m = __ballot(do_reset);
     if (lane == 0) { L.mask[0] = (uint32_t)m; L.mask[1] = (uint32_t)(m >> 32); }
     lds_barrier();                           // B_k: the helpers' records of step k are in LDS
@@ -2980,14 +2981,15 @@ __global__ void __launch_bounds__(256, 2) rollout_kernel_small(KParams P0, StepI
         Env E;
         if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, need_level, /*with_hist=*/true);
         for (uint32_t k = 0; k < K; ++k) {
-            StepIO io = io0;
-            io.act = io0.act + (size_t)k * act_stride;
-            io.rew = io0.rew + (size_t)k * n;
-            io.done = io0.done + (size_t)k * n;
-            if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
-            if (io0.cost) io.cost = io0.cost + (size_t)k * n;
-            if (io0.level) io.level = io0.level + (size_t)k * n;
-            if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+            const StepIO I0 = late_io(io0);
+            StepIO io = I0;
+            io.act = I0.act + (size_t)k * act_stride;
+            io.rew = I0.rew + (size_t)k * n;
+            io.done = I0.done + (size_t)k * n;
+            if (I0.trunc) io.trunc = I0.trunc + (size_t)k * n;
+            if (I0.cost) io.cost = I0.cost + (size_t)k * n;
+            if (I0.level) io.level = I0.level + (size_t)k * n;
+            if (I0.final_obs) io.final_obs = I0.final_obs + (size_t)k * n * OD;
             small_roll_env_step<NOISE, DR, PHYS, SPEC>(P, io, i, lane, live, E, L, s_hjgrid);
             // this wave's 64 rows, written by this wave only: its LDS writes land before its reads
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -3095,12 +3097,13 @@ __global__ void __launch_bounds__(CROLL_SMALL_BLOCK, 1) collect_rollout_kernel_s
         Env E;
         if (live) load_env<NOISE, DR, PHYS>(P, io0.sf, i, E, P.need_level, /*with_hist=*/true);
         for (uint32_t k = 0; k < K; ++k) {
-            StepIO io = io0;
+            const StepIO I0 = late_io(io0);
+            StepIO io = I0;
             io.act = pio.act + (size_t)k * n * 4;
-            io.rew = io0.rew + (size_t)k * n;
-            io.done = io0.done + (size_t)k * n;
-            if (io0.trunc) io.trunc = io0.trunc + (size_t)k * n;
-            if (io0.final_obs) io.final_obs = io0.final_obs + (size_t)k * n * OD;
+            io.rew = I0.rew + (size_t)k * n;
+            io.done = I0.done + (size_t)k * n;
+            if (I0.trunc) io.trunc = I0.trunc + (size_t)k * n;
+            if (I0.final_obs) io.final_obs = I0.final_obs + (size_t)k * n * OD;
             small_roll_env_step<NOISE, DR, PHYS, SPEC>(P, io, i, lane, live, E, L, s_hjgrid);
             lds_barrier();                       // P_k: every row of the block is in LDS
             write_rows(k);
